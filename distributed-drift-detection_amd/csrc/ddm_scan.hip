@@ -1,0 +1,215 @@
+// DDM scan over error streams: run_DDM (DDM_Process.py:135-159) batch after batch.
+//
+// One lane owns one stream and runs scikit-multiflow's DDM recurrence exactly
+// (fp64, no FMA contraction: built with -ffp-contract=off), so p, s and every
+// decision are bit-identical to the reference arithmetic.  Throughput comes from
+// (a) many streams in flight (C4: 1M streams = 16k waves) and (b) the zero-run
+// fast path: while the detector is in its trivial state (every error so far 0:
+// p = s = p_min = s_min = 0 after the gate) a 0 leaves the state unchanged except
+// sample_count, so runs of zeros are skipped with `ctz` over 16-byte chunks and,
+// with the `first_nz` hint produced by the predict kernel, in one jump.
+//
+// HBM layout: err is one uint8 per row in DDM order (the shuffled order of
+// DDM_Process.py:190), streams back to back; events are int32 pairs per batch.
+#include "common.h"
+
+namespace {
+
+struct Det {
+    double p, s, pmin, smin, psmin;
+    int64_t n;
+    int chg, warn;
+};
+
+__device__ __forceinline__ void det_reset(Det& d) {
+    d.p = 1.0;
+    d.s = 0.0;
+    d.pmin = d.smin = d.psmin = __builtin_huge_val();
+    d.n = 1;
+    d.chg = 0;
+    d.warn = 0;
+}
+
+// skmultiflow DDM.add_element (restated in SURVEY.md Appendix A).
+__device__ __forceinline__ void det_add(Det& d, int x, int min_inst, double wl, double cl) {
+    if (d.chg) det_reset(d);
+    const double n = (double)d.n;
+    const double p = d.p + ((double)x - d.p) / n;
+    const double s = sqrt(p * (1.0 - p) / n);
+    d.p = p;
+    d.s = s;
+    d.n += 1;
+    d.chg = 0;
+    d.warn = 0;
+    if (d.n < min_inst) return;
+    const double ps = p + s;
+    if (ps <= d.psmin) {
+        d.pmin = p;
+        d.smin = s;
+        d.psmin = ps;
+    }
+    if (ps > d.pmin + cl * d.smin) d.chg = 1;
+    else if (ps > d.pmin + wl * d.smin) d.warn = 1;
+}
+
+// Every error so far was 0 and the gate has set the minimum: adding a 0 keeps
+// (p, s, p_min, s_min, ps_min) = 0 and raises no flag.
+__device__ __forceinline__ bool det_trivial(const Det& d) {
+    return d.p == 0.0 && d.psmin == 0.0 && d.pmin == 0.0 && d.smin == 0.0 && d.chg == 0;
+}
+
+// First byte index t in [k, limit) of the 16-byte chunk (lo | hi << 64) that is
+// nonzero, or limit.
+__device__ __forceinline__ int first_nonzero_byte(uint64_t lo, uint64_t hi, int k, int limit) {
+    if (k >= 8) {
+        lo = 0;
+        hi &= ~0ull << (8 * (k - 8));
+    } else {
+        lo &= ~0ull << (8 * k);
+    }
+    int t = lo ? (__builtin_ctzll(lo) >> 3) : (hi ? 8 + (__builtin_ctzll(hi) >> 3) : 16);
+    return t < limit ? t : limit;
+}
+
+__global__ __launch_bounds__(256) void k_scan_streams(
+    const uint8_t* __restrict__ err, const int64_t* __restrict__ off, int64_t n_streams,
+    ddm_params P, ddm_state* __restrict__ state, const uint64_t* __restrict__ first_nz,
+    const int64_t* __restrict__ batch_base, int32_t* __restrict__ ev, int32_t* __restrict__ stop_out,
+    int64_t* __restrict__ nev_out, int mode, double* __restrict__ ps_out) {
+    const int64_t sid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (sid >= n_streams) return;
+    const int64_t lo = off[sid], hi = off[sid + 1];
+    const int64_t pb = P.per_batch;
+    const int min_inst = P.min_num_instances;
+    const double wl = P.warning_level, cl = P.out_control_level;
+
+    Det d;
+    {
+        const ddm_state st = state[sid];
+        d.p = st.miss_prob;
+        d.s = st.miss_std;
+        d.pmin = st.miss_prob_min;
+        d.smin = st.miss_sd_min;
+        d.psmin = st.miss_prob_sd_min;
+        d.n = st.sample_count;
+        d.chg = st.in_concept_change;
+        d.warn = st.in_warning_zone;
+    }
+    const uint64_t hint = first_nz ? first_nz[sid] : 0ull;
+    int32_t* evs = ev + 2 * batch_base[sid];
+    int64_t nev = 0;
+    int32_t stop = -1;
+    int64_t b = 0, bstart = lo, bend = min(lo + pb, hi);
+    int wpos = -1;
+    int64_t i = lo;
+    int64_t cbase = -1;
+    uint64_t clo = 0, chi = 0;
+
+    while (i < hi) {
+        if (det_trivial(d)) {
+            // Jump over a zero run: to the hinted first nonzero row, or past the zero
+            // bytes of the current chunk (never past the current batch).
+            int64_t j = i;
+            if (hint > (uint64_t)i) {
+                j = hint < (uint64_t)hi ? (int64_t)hint : hi;
+            } else {
+                const int64_t cb = i & ~(int64_t)15;
+                if (cb != cbase) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(err + cb);
+                    clo = (uint64_t)v.x | ((uint64_t)v.y << 32);
+                    chi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+                    cbase = cb;
+                }
+                const int lim = (int)min((int64_t)16, min(hi, bend) - cb);
+                j = cb + first_nonzero_byte(clo, chi, (int)(i - cb), lim);
+            }
+            if (j > i) {
+                if (ps_out)
+                    for (int64_t k = i; k < j; ++k) ps_out[2 * k] = ps_out[2 * k + 1] = 0.0;
+                d.n += j - i;
+                d.warn = 0;
+                i = j;
+                if (i >= bend) {  // whole batches of zeros: no event can have occurred
+                    b = (i - lo) / pb;
+                    bstart = lo + b * pb;
+                    bend = min(bstart + pb, hi);
+                    wpos = -1;
+                }
+                continue;
+            }
+        }
+        const int64_t cb = i & ~(int64_t)15;
+        if (cb != cbase) {
+            const uint4 v = *reinterpret_cast<const uint4*>(err + cb);
+            clo = (uint64_t)v.x | ((uint64_t)v.y << 32);
+            chi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+            cbase = cb;
+        }
+        const int k = (int)(i - cb);
+        const int x = (int)(((k < 8 ? clo >> (8 * k) : chi >> (8 * (k - 8)))) & 0xff) != 0;
+        det_add(d, x, min_inst, wl, cl);
+        if (ps_out) {
+            ps_out[2 * i] = d.p;
+            ps_out[2 * i + 1] = d.s;
+        }
+        if (d.warn && wpos < 0) wpos = (int)(i - bstart);
+        ++i;
+        if (d.chg) {
+            evs[2 * b] = wpos;
+            evs[2 * b + 1] = (int)(i - 1 - bstart);
+            ++nev;
+            if (mode == 0) {
+                stop = (int32_t)b;
+                break;
+            }
+            det_reset(d);  // DDM dropped (DDM_Process.py:209), fresh one next batch
+            i = bend;
+        } else if (i >= bend && wpos >= 0) {
+            evs[2 * b] = wpos;
+            ++nev;
+        }
+        if (i >= bend) {
+            ++b;
+            bstart = bend;
+            bend = min(bstart + pb, hi);
+            wpos = -1;
+        }
+    }
+
+    ddm_state st;
+    st.miss_prob = d.p;
+    st.miss_std = d.s;
+    st.miss_prob_min = d.pmin;
+    st.miss_sd_min = d.smin;
+    st.miss_prob_sd_min = d.psmin;
+    st.sample_count = d.n;
+    st.in_concept_change = d.chg;
+    st.in_warning_zone = d.warn;
+    state[sid] = st;
+    if (stop_out) stop_out[sid] = stop;
+    if (nev_out) nev_out[sid] = nev;
+}
+
+}  // namespace
+
+extern "C" int ddm_scan_streams(const uint8_t* err, const int64_t* stream_off, int64_t n_streams,
+                                const ddm_params* prm, ddm_state* state_io, const uint64_t* first_nz,
+                                const int64_t* batch_base, int64_t n_batches_total, int32_t* ev_out,
+                                int32_t* stop_out, int64_t* nev_out, int32_t mode, double* ps_out,
+                                ddm_stream_t stream) {
+    if (!err || !stream_off || !prm || !state_io || !batch_base || !ev_out || n_streams < 0 ||
+        n_batches_total < 0 || prm->per_batch <= 0 || (mode != 0 && mode != 1)) {
+        ddm::set_error("ddm_scan_streams: invalid argument");
+        return DDM_E_ARG;
+    }
+    if (n_streams == 0) return 0;
+    hipStream_t s = ddm::as_hip(stream);
+    if (int rc = ddm::hip_status(hipMemsetAsync(ev_out, 0xff, (size_t)n_batches_total * 2 * sizeof(int32_t), s),
+                                 "ddm_scan_streams: memset"))
+        return rc;
+    const int threads = n_streams >= 256 ? 256 : 64;
+    const int64_t blocks = ddm::ceil_div(n_streams, threads);
+    hipLaunchKernelGGL(k_scan_streams, dim3((unsigned)blocks), dim3(threads), 0, s, err, stream_off, n_streams, *prm,
+                       state_io, first_nz, batch_base, ev_out, stop_out, nev_out, (int)mode, ps_out);
+    return ddm::launch_status("ddm_scan_streams");
+}

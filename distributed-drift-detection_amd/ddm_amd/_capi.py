@@ -1,0 +1,83 @@
+"""ctypes binding of libddm_amd.so (the C-ABI declared in include/ddm_amd.h).
+
+torch is imported first so that the process holds torch's HIP runtime; the library's
+`libamdhip64.so.7` dependency then resolves to that same runtime, and kernels launched
+here run on torch streams against torch allocations.  There is no fallback: if the
+library is missing this module raises at import time, and the product path fails.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads the HIP runtime the library binds to)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
+ABI_VERSION = 1
+
+DDM_E_ARG = 1001
+DDM_E_FOREST = 1002
+
+
+class DdmParams(ctypes.Structure):
+    _fields_ = [("min_num_instances", ctypes.c_int32), ("per_batch", ctypes.c_int32),
+                ("warning_level", ctypes.c_double), ("out_control_level", ctypes.c_double)]
+
+
+class DdmState(ctypes.Structure):
+    _fields_ = [("miss_prob", ctypes.c_double), ("miss_std", ctypes.c_double),
+                ("miss_prob_min", ctypes.c_double), ("miss_sd_min", ctypes.c_double),
+                ("miss_prob_sd_min", ctypes.c_double), ("sample_count", ctypes.c_int64),
+                ("in_concept_change", ctypes.c_int32), ("in_warning_zone", ctypes.c_int32)]
+
+
+class DdmForest(ctypes.Structure):
+    _fields_ = [("nodes", ctypes.c_void_p), ("roots", ctypes.c_void_p), ("leaf_value", ctypes.c_void_p),
+                ("classes", ctypes.c_void_p), ("n_trees", ctypes.c_int32), ("n_classes", ctypes.c_int32),
+                ("n_nodes", ctypes.c_int32), ("pure", ctypes.c_int32)]
+
+
+assert ctypes.sizeof(DdmState) == 56 and ctypes.sizeof(DdmParams) == 24 and ctypes.sizeof(DdmForest) == 48
+
+_vp, _i32, _i64, _u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
+_f32, _pi32 = ctypes.c_float, ctypes.POINTER(ctypes.c_int32)
+
+# name -> (restype, argtypes); every symbol include/ddm_amd.h declares.
+SIGNATURES = {
+    "ddm_abi_version": (ctypes.c_int, []),
+    "ddm_last_error": (ctypes.c_char_p, []),
+    "ddm_forest_predict": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _i64, _i64, _i32, ctypes.POINTER(DdmForest),
+                                          _vp, _vp, _vp, _vp]),
+    "ddm_scan_streams": (ctypes.c_int, [_vp, _vp, _i64, ctypes.POINTER(DdmParams), _vp, _vp, _vp, _i64, _vp, _vp,
+                                        _vp, _i32, _vp, _vp]),
+    "ddm_mt_perms": (ctypes.c_int, [_vp, _pi32, _vp, _i64, _vp, _vp]),
+    "ddm_mt_randint31": (ctypes.c_int, [_vp, _pi32, _i64, _vp]),
+    "ddm_mt_skip": (ctypes.c_int, [_vp, _pi32, _i64]),
+    "ddm_synth_block_labels": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i32, _vp]),
+    "ddm_synth_features": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _i64, _i64, _u64, _f32, _vp]),
+    "ddm_synth_bernoulli_streams": (ctypes.c_int, [_vp, _i64, _i64, _u64, _vp]),
+}
+
+
+class DdmError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is not built; run `python __graft_entry__.py` (build) or "
+                          f"`make -C distributed-drift-detection_amd/csrc` first")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    if lib.ddm_abi_version() != ABI_VERSION:
+        raise ImportError(f"libddm_amd.so ABI {lib.ddm_abi_version()} != {ABI_VERSION}")
+    return lib
+
+
+lib = _load()
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib.ddm_last_error().decode(errors="replace")
+        raise DdmError(f"{what} failed (code {rc}): {msg}")

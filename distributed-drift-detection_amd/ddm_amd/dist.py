@@ -1,0 +1,59 @@
+"""Multi-process (one process per GPU) partition execution and the event gather.
+
+Replaces Spark's executor fan-out and the `.toPandas()` collect (DDM_Process.py:226,
+258).  Partition d runs on rank d % world_size (no data moves between ranks: every
+rank builds its partitions from the same stream description), then ONE exchange step
+gathers the events: an all_gather of per-rank record counts followed by an all_gather of
+the padded int64 records [device_id, batch, warn_local, warn_global, change_local,
+change_global].  With the "nccl" backend (RCCL over xGMI) the buffers live in HBM;
+with "gloo" (CPU tests) on the host.  The payload is tiny (<= 48 B per batch), so a
+single padded all_gather beats anything ring-bandwidth-shaped.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+RECORD = 6
+
+
+def local_partitions(parts, rank, world):
+    return [(d, f) for d, f in parts if d % world == rank]
+
+
+def _records(outputs):
+    recs = []
+    for d, ev in sorted(outputs.items()):
+        ev = np.asarray(ev, dtype=np.int64).reshape(-1, 4)
+        r = np.empty((len(ev), RECORD), dtype=np.int64)
+        r[:, 0] = d
+        r[:, 1] = np.arange(len(ev))
+        r[:, 2:] = ev
+        recs.append(r)
+    return np.concatenate(recs) if recs else np.empty((0, RECORD), dtype=np.int64)
+
+
+def gather_events(outputs, group=None, device=None):
+    """outputs: {device_id: int64 [n_batches-1, 4]} of this rank -> the same dict for ALL
+    partitions of all ranks (on every rank)."""
+    world = dist.get_world_size(group)
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
+            else torch.device("cpu")
+    recs = torch.from_numpy(_records(outputs)).to(device)
+    n = torch.tensor([recs.shape[0]], dtype=torch.int64, device=device)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n, group=group)
+    counts = [int(c.item()) for c in counts]
+    cap = max(counts) if counts else 0
+    pad = torch.full((cap, RECORD), -1, dtype=torch.int64, device=device)
+    pad[:recs.shape[0]] = recs
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    allrec = np.concatenate([b[:c].cpu().numpy() for b, c in zip(bufs, counts)]) if cap else \
+        np.empty((0, RECORD), dtype=np.int64)
+    out = {}
+    for d in np.unique(allrec[:, 0]):
+        r = allrec[allrec[:, 0] == d]
+        r = r[np.argsort(r[:, 1])]
+        out[int(d)] = r[:, 2:].copy()
+    return out

@@ -1,0 +1,85 @@
+"""Typed wrappers over the device entry points of the C-ABI (torch tensors in, no copies).
+
+Every function is asynchronous on the given torch stream (default: current stream of
+the tensor's device) and raises DdmError on a non-zero return code.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from ._capi import DdmParams, check, lib
+
+STATE_DTYPE = np.dtype([("miss_prob", "<f8"), ("miss_std", "<f8"), ("miss_prob_min", "<f8"),
+                        ("miss_sd_min", "<f8"), ("miss_prob_sd_min", "<f8"), ("sample_count", "<i8"),
+                        ("in_concept_change", "<i4"), ("in_warning_zone", "<i4")])
+assert STATE_DTYPE.itemsize == 56
+
+
+def fresh_states(n):
+    """`DDM(...)` as constructed at DDM_Process.py:139 (skmultiflow reset())."""
+    st = np.zeros(n, dtype=STATE_DTYPE)
+    st["miss_prob"] = 1.0
+    st["miss_prob_min"] = st["miss_sd_min"] = st["miss_prob_sd_min"] = np.inf
+    st["sample_count"] = 1
+    return st
+
+
+def params_struct(min_num_instances=3, per_batch=100, warning_level=0.5, out_control_level=1.5):
+    return DdmParams(int(min_num_instances), int(per_batch), float(warning_level), float(out_control_level))
+
+
+def _stream(t, stream):
+    s = stream if stream is not None else torch.cuda.current_stream(t.device)
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def forest_predict(X, y, perm, pos_begin, pos_end, per_batch, forest, err, first_err=None, pred=None,
+                   stream=None):
+    """X: float32 [F, ld] (columnar), y int32 [ld], perm/err uint8 indexed by DDM position."""
+    assert X.dtype == torch.float32 and X.dim() == 2 and X.is_contiguous()
+    assert y.dtype == torch.int32 and perm.dtype == torch.uint8 and err.dtype == torch.uint8
+    assert pos_end <= perm.numel() and pos_end <= err.numel()
+    F, ld = X.shape
+    check(lib.ddm_forest_predict(X.data_ptr(), ld, F, y.data_ptr(), perm.data_ptr(), int(pos_begin), int(pos_end),
+                                 int(per_batch), ctypes.byref(forest.desc), err.data_ptr(), _ptr(first_err),
+                                 _ptr(pred), _stream(X, stream)), "ddm_forest_predict")
+
+
+def scan_streams(err, offsets, params, state, batch_base, n_batches_total, ev, first_nz=None, stop=None, nev=None,
+                 mode=0, ps=None, stream=None):
+    """err uint8 (padded to a multiple of 16 past the last offset); offsets/batch_base int64;
+    state: uint8 tensor holding n_streams ddm_state records; ev int32 [n_batches_total, 2]."""
+    check(lib.ddm_scan_streams(err.data_ptr(), _ptr(offsets), offsets.numel() - 1, ctypes.byref(params),
+                               _ptr(state), _ptr(first_nz), _ptr(batch_base), int(n_batches_total), _ptr(ev),
+                               _ptr(stop), _ptr(nev), int(mode), _ptr(ps), _stream(err, stream)),
+          "ddm_scan_streams")
+
+
+def scan_streams_raw(err_ptr, offsets_ptr, n_streams, params, state_ptr, batch_base_ptr, n_batches_total, ev_ptr,
+                     first_nz_ptr, stop_ptr, nev_ptr, mode, ps_ptr, stream):
+    """Pointer-level variant used by the controller (all pointers are device addresses)."""
+    check(lib.ddm_scan_streams(err_ptr, offsets_ptr, n_streams, ctypes.byref(params), state_ptr, first_nz_ptr,
+                               batch_base_ptr, n_batches_total, ev_ptr, stop_ptr, nev_ptr, mode, ps_ptr,
+                               ctypes.c_void_p(stream.cuda_stream)), "ddm_scan_streams")
+
+
+def synth_block_labels(y, part, n_parts, block_rows, n_classes, stream=None):
+    check(lib.ddm_synth_block_labels(y.data_ptr(), y.numel(), part, n_parts, block_rows, n_classes,
+                                     _stream(y, stream)), "ddm_synth_block_labels")
+
+
+def synth_features(X, y, row0, row_stride, seed, noise=0.04, stream=None):
+    F, ld = X.shape
+    check(lib.ddm_synth_features(X.data_ptr(), ld, F, y.data_ptr(), y.numel(), row0, row_stride, seed,
+                                 ctypes.c_float(noise), _stream(X, stream)), "ddm_synth_features")
+
+
+def synth_bernoulli_streams(err, n_streams, length, seed, stream=None):
+    assert err.numel() >= n_streams * length
+    check(lib.ddm_synth_bernoulli_streams(err.data_ptr(), n_streams, length, seed, _stream(err, stream)),
+          "ddm_synth_bernoulli_streams")

@@ -1,0 +1,38 @@
+"""Settings of the hot path, mirroring the reference's module constants
+(DDM_Process.py:25-35).  Spark knobs (URL, INSTANCES, MEMORY) are not part of the
+hot path; `cores` is RandomForestClassifier's n_jobs (DDM_Process.py:102), which
+changes speed, not results."""
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+
+@dataclass
+class DDMSettings:
+    per_batch: int = 100                 # PER_BATCH            DDM_Process.py:25
+    min_num_instances: int = 3           # MIN_NUM_DDM_VALS     DDM_Process.py:27
+    warning_level: float = 0.5           # WARNING_LEVEL        DDM_Process.py:28
+    out_control_level: float = 1.5       # CHANGE_LEVEL         DDM_Process.py:29
+    n_estimators: int = 100              # RandomForestClassifier default (DDM_Process.py:102)
+    cores: int = 1                       # CORES -> n_jobs      DDM_Process.py:8,102
+    x_features: Optional[List[str]] = None   # X_features     DDM_Process.py:33-34 (None: '0','1',... present)
+    target: str = "target"               # y_true               DDM_Process.py:35
+    row_number: str = "full_df_row_number"   # DDM_Process.py:220
+    window_batches: int = 256            # first speculative window (batches); doubles while no drift
+    max_window_batches: int = 1 << 16
+    extra: dict = field(default_factory=dict)
+
+
+SCHEMA = ("warning_flag_local int, warning_flag_global int, change_flag_local int, "
+          "change_flag_global int")                                      # DDM_Process.py:167
+OUTPUT_COLUMNS = ["warning_flag_local", "warning_flag_global", "change_flag_local", "change_flag_global"]
+
+
+def infer_x_features(columns):
+    """The reference's X_features are '0'..str(F-1) (DDM_Process.py:33-34)."""
+    names = set(map(str, columns))
+    out = []
+    while str(len(out)) in names:
+        out.append(str(len(out)))
+    if not out:
+        raise KeyError("no feature columns named '0', '1', ... (DDM_Process.py:34)")
+    return out

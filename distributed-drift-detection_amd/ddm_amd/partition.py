@@ -1,0 +1,87 @@
+"""Partitioning and placement — the MI355X side of DDM_Process.py:220-226.
+
+Reference: `full_df_row_number = df.index` (:220), `device_id = full_df_row_number %
+INSTANCES` (:225, a row-at-a-time Python UDF), `repartition("device_id")
+.groupby("device_id").apply(run_DDM_loop)` (:226): each group is handed to the UDF as a
+pandas frame with a RangeIndex, and the UDF outputs are concatenated.
+
+Here the groups are strided subsets computed with one vectorised modulo, each group's
+rows go to HBM of GPU `device_id % n_gpus` and run on their own HIP stream, and the
+per-partition outputs are concatenated in device_id order.  Partitions are
+independent (the reference shares nothing between them), so there is no collective on
+the data path; `dist.py` adds the one gather of events across processes.
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pandas as pd
+import torch
+
+from .controller import run_partition_frame
+from .params import OUTPUT_COLUMNS, DDMSettings
+from .rng import MTStream
+
+
+def split_partitions(df, instances, row_number="full_df_row_number"):
+    """[(device_id, frame)] in device_id order; frames keep the stream order and get a
+    RangeIndex (grouped-map semantics) plus the full_df_row_number / device_id columns."""
+    full = df.copy()
+    full[row_number] = df.index.to_numpy()
+    dev = (full[row_number].to_numpy() % int(instances)).astype(np.int32)
+    full["device_id"] = dev
+    order = np.argsort(dev, kind="stable")
+    counts = np.bincount(dev, minlength=int(instances))
+    out, start = [], 0
+    for d in range(int(instances)):
+        idx = order[start:start + counts[d]]
+        start += counts[d]
+        if counts[d]:
+            out.append((d, full.iloc[idx].reset_index(drop=True)))
+    return out
+
+
+def placement(device_id, n_gpus):
+    """GPU of a partition: device_id % n_gpus."""
+    return int(device_id) % max(1, int(n_gpus))
+
+
+def run_partitions(parts, seeds, settings=None, devices=None, max_workers=None, fn=None, stats=None):
+    """Run [(device_id, frame)] concurrently, one HIP stream (and host thread) per partition.
+
+    seeds: device_id -> MT19937 seed, the RNG each partition's Spark worker would hold
+    (`np.random.seed(base + device_id)` in the oracle).  fn(frame, rng, device) replaces
+    the GPU partition function (tests only).  Returns {device_id: output frame}."""
+    s = settings or DDMSettings()
+    if devices is None:
+        devices = [torch.device("cuda", i) for i in range(torch.cuda.device_count())]
+    if fn is None:
+        if not devices:
+            raise RuntimeError("no GPU visible: the MI355X partition path needs a HIP device")
+
+        def fn(frame, rng, device, st):
+            stream = torch.cuda.Stream(device)
+            return run_partition_frame(frame, rng, s, device, stream, stats=st)
+
+    def one(item):
+        d, frame = item
+        dev = devices[placement(d, len(devices))] if devices else None
+        st = {}
+        out = fn(frame, MTStream.from_seed(seeds[d]), dev, st)
+        return d, out, st
+
+    workers = max_workers or max(1, min(len(parts), 16))
+    with ThreadPoolExecutor(workers) as ex:
+        res = list(ex.map(one, parts))
+    if stats is not None:
+        for d, _, st in res:
+            stats[d] = st
+    return {d: out for d, out, _ in res}
+
+
+def apply_in_pandas(df, instances, base_seed, settings=None, devices=None, max_workers=None):
+    """`df.groupby(device_id).apply(run_DDM_loop)` (DDM_Process.py:225-226) on the GPUs of
+    this process: concatenated UDF outputs (schema DDM_Process.py:167) in device_id order."""
+    parts = split_partitions(df, instances)
+    outs = run_partitions(parts, {d: base_seed + d for d, _ in parts}, settings, devices, max_workers)
+    frames = [outs[d] for d, _ in parts]
+    return pd.concat(frames) if frames else pd.DataFrame(columns=OUTPUT_COLUMNS)

@@ -1,0 +1,86 @@
+"""numpy-compatible MT19937 stream driven by the native generator (ddm_mt_* in the C-ABI).
+
+The reference consumes ONE global numpy RandomState per Python worker: a
+`permutation(len(batch))` per batch (pandas `sample(frac=1)`, DDM_Process.py:187,
+:190) and 100 `randint(2**31-1)` per refit (RandomForestClassifier with
+random_state=None, DDM_Process.py:102).  `MTStream` holds that state as (key[624],
+pos), generates batch permutations natively and converts to/from numpy's
+`get_state()` tuple so the host refit (sklearn) can draw from exactly the same
+position.
+"""
+import ctypes
+
+import numpy as np
+
+from ._capi import check, lib
+
+
+class MTStream:
+    __slots__ = ("key", "pos")
+
+    def __init__(self, key, pos):
+        self.key = np.ascontiguousarray(key, dtype=np.uint32).copy()
+        self.pos = ctypes.c_int32(int(pos))
+        assert self.key.shape == (624,)
+
+    @classmethod
+    def from_numpy_state(cls, state):
+        name, key, pos = state[0], state[1], state[2]
+        if name != "MT19937":
+            raise ValueError(f"unsupported bit generator {name}")
+        return cls(key, pos)
+
+    @classmethod
+    def from_global(cls):
+        return cls.from_numpy_state(np.random.get_state())
+
+    @classmethod
+    def from_seed(cls, seed):
+        return cls.from_numpy_state(np.random.RandomState(seed).get_state())
+
+    def numpy_state(self):
+        return ("MT19937", self.key.copy(), int(self.pos.value), 0, 0.0)
+
+    def to_random_state(self):
+        rs = np.random.RandomState()
+        rs.set_state(self.numpy_state())
+        return rs
+
+    def load_random_state(self, rs):
+        st = rs.get_state()
+        self.key[:] = st[1]
+        self.pos.value = int(st[2])
+
+    def snapshot(self):
+        return self.key.copy(), int(self.pos.value)
+
+    def restore(self, snap):
+        self.key[:] = snap[0]
+        self.pos.value = snap[1]
+
+    def copy(self):
+        return MTStream(self.key, self.pos.value)
+
+    def perms(self, batch_len, out=None, draws=None):
+        """Legacy `permutation(n)` for each n in batch_len (n <= 256), back to back as uint8."""
+        batch_len = np.ascontiguousarray(batch_len, dtype=np.int32)
+        total = int(batch_len.sum())
+        if out is None:
+            out = np.empty(total, dtype=np.uint8)
+        assert out.dtype == np.uint8 and out.flags.c_contiguous and out.size >= total
+        dptr = None
+        if draws is not None:
+            assert draws.dtype == np.int64 and draws.size >= batch_len.size
+            dptr = draws.ctypes.data
+        check(lib.ddm_mt_perms(self.key.ctypes.data, ctypes.byref(self.pos), batch_len.ctypes.data,
+                               batch_len.size, out.ctypes.data, dptr), "ddm_mt_perms")
+        return out
+
+    def randint31(self, count):
+        out = np.empty(count, dtype=np.int64)
+        check(lib.ddm_mt_randint31(self.key.ctypes.data, ctypes.byref(self.pos), count, out.ctypes.data),
+              "ddm_mt_randint31")
+        return out
+
+    def skip(self, n_draws):
+        check(lib.ddm_mt_skip(self.key.ctypes.data, ctypes.byref(self.pos), int(n_draws)), "ddm_mt_skip")

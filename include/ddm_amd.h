@@ -1,0 +1,157 @@
+/* ddm_amd.h — C-ABI of the MI355X-native predict + DDM hot path.
+ *
+ * The reference hot path is the grouped-map pandas UDF `run_DDM_loop`
+ * (DDM_Process.py:166-213) applied per partition (`groupby("device_id").apply`,
+ * DDM_Process.py:226).  Its inner calls are replaced by these entry points:
+ *
+ *   ddm_forest_predict   <- predict_rf (DDM_Process.py:110-128): sklearn forest.predict
+ *                           + `acc = y_pred != y` (:117), rows fed in the shuffled
+ *                           order of `batch_b.sample(frac=1)` (:190)
+ *   ddm_scan_streams     <- run_DDM (DDM_Process.py:135-159) over consecutive batches,
+ *                           DDM state carried (:202), first warning / first change +
+ *                           break per batch (:147-152), DDM dropped after a change
+ *                           (:207-210)
+ *   ddm_mt_perms         <- `DataFrame.sample(frac=1)` (:187, :190) on numpy's global
+ *                           MT19937 (legacy RandomState.permutation)
+ *   ddm_mt_randint31     <- the 100 `randint(2**31-1)` tree seeds RandomForestClassifier
+ *                           .fit draws from the same global RNG (:102-103)
+ *   ddm_mt_skip          <- re-positioning the global RNG after a speculative window
+ *   ddm_synth_*          <- synthetic rialto/outdoor-shaped inputs for the benchmark
+ *                           (rialto.csv is not shipped, .MISSING_LARGE_BLOBS:1)
+ *
+ * Conventions: all device pointers are caller-owned (the library never allocates or
+ * frees); every device entry point takes an explicit hipStream_t and is asynchronous,
+ * re-entrant and stateless.  Return value 0 = ok, otherwise a hipError_t or one of
+ * the DDM_E_* codes below; ddm_last_error() describes the last failure of the calling
+ * thread.  No torch types cross this boundary.
+ */
+#ifndef DDM_AMD_H
+#define DDM_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DDM_AMD_ABI_VERSION 1
+
+#define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
+#define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
+
+typedef struct ihipStream_t* ddm_stream_t;   /* == hipStream_t */
+
+/* DDM parameters: DDM_Process.py:25,27-29 (PER_BATCH, MIN_NUM_DDM_VALS, WARNING_LEVEL,
+ * CHANGE_LEVEL).  Reference values 100 / 3 / 0.5 / 1.5. */
+typedef struct ddm_params {
+    int32_t min_num_instances;
+    int32_t per_batch;
+    double  warning_level;
+    double  out_control_level;
+} ddm_params;
+
+/* One DDM detector (scikit-multiflow DDM field names).  A freshly constructed DDM
+ * (DDM_Process.py:139) is {1.0, 0.0, +inf, +inf, +inf, 1, 0, 0}. */
+typedef struct ddm_state {
+    double  miss_prob;          /* p      */
+    double  miss_std;           /* s      */
+    double  miss_prob_min;      /* p_min  */
+    double  miss_sd_min;        /* s_min  */
+    double  miss_prob_sd_min;   /* min of p+s */
+    int64_t sample_count;       /* n      */
+    int32_t in_concept_change;
+    int32_t in_warning_zone;
+} ddm_state;
+
+/* Forest node, 16 bytes.  feature >= 0: internal node testing (double)x_f32[feature &
+ * 0x3fffffff] <= threshold (bit 30 set: NaN goes left), children at child (left) and
+ * child + 1 (right).  feature == -1: leaf, child = class index (pure forests) or row of
+ * leaf_value (impure forests). */
+typedef struct ddm_node {
+    double  threshold;
+    int32_t feature;
+    int32_t child;
+} ddm_node;
+
+typedef struct ddm_forest {
+    const ddm_node* nodes;       /* device [n_nodes]                               */
+    const int32_t*  roots;       /* device [n_trees] root node of each tree        */
+    const double*   leaf_value;  /* device [n_leaf_rows * n_classes] or NULL (pure) */
+    const int32_t*  classes;     /* device [n_classes] class labels (classes_)     */
+    int32_t n_trees;
+    int32_t n_classes;           /* <= 64                                          */
+    int32_t n_nodes;
+    int32_t pure;                /* 1: every leaf is one-hot and n_trees <= 255    */
+} ddm_forest;
+
+int ddm_abi_version(void);
+const char* ddm_last_error(void);
+
+/* predict_rf + error flag for DDM positions [pos_begin, pos_end) of one partition.
+ * DDM position g lies in batch b = g / per_batch; its row is b*per_batch + perm[g]
+ * (perm = the batch's shuffle, DDM_Process.py:190).  X is columnar float32
+ * (X[f*ld + row], the float32 cast sklearn applies), y int32 labels.
+ * err_out[g] = (classes[argmax] != y[row]); first_err (device uint64, may be NULL) is
+ * set to the smallest g with an error, UINT64_MAX if none (written by this call);
+ * pred_out (may be NULL) receives the predicted label per g. */
+int ddm_forest_predict(const float* X, int64_t ld, int32_t n_features, const int32_t* y,
+                       const uint8_t* perm, int64_t pos_begin, int64_t pos_end,
+                       int32_t per_batch, const ddm_forest* forest, uint8_t* err_out,
+                       uint64_t* first_err, int32_t* pred_out, ddm_stream_t stream);
+
+/* run_DDM over every batch of every stream.  Stream s is err[stream_off[s] ..
+ * stream_off[s+1]) (device int64 offsets; err readable up to the next multiple of 16
+ * bytes past the last offset), cut into batches of per_batch rows (last one short).
+ * state_io[s] (device) is the carried DDM, updated in place.
+ * first_nz (device, may be NULL) is a hint: no nonzero byte of stream s lies in
+ * [stream_off[s], first_nz[s]) (e.g. ddm_forest_predict's first_err).
+ * ev_out (device int32 [n_batches_total][2]) receives per batch (first warning
+ * position, change position) inside the batch, -1 = none; batch b of stream s is
+ * row batch_base[s] + b (device int64).  This call fills ev_out with -1 first.
+ * mode 0: stop a stream after its first batch with a change (controller mode);
+ * mode 1: fresh DDM at the next batch after a change (DDM-only streams).
+ * stop_out (device int32, may be NULL): batch of the first change or -1 (mode 0).
+ * nev_out (device int64, may be NULL): number of batches with an event per stream.
+ * ps_out (device double [rows][2], may be NULL): p and s after each processed row. */
+int ddm_scan_streams(const uint8_t* err, const int64_t* stream_off, int64_t n_streams,
+                     const ddm_params* prm, ddm_state* state_io, const uint64_t* first_nz,
+                     const int64_t* batch_base, int64_t n_batches_total, int32_t* ev_out,
+                     int32_t* stop_out, int64_t* nev_out, int32_t mode, double* ps_out,
+                     ddm_stream_t stream);
+
+/* ---- host-side MT19937 (numpy legacy RandomState layout: key[624], pos) ---------- */
+
+/* Legacy `permutation(len)` for consecutive batches (Fisher-Yates, mask rejection).
+ * batch_len[i] <= 256; perms are written back to back into perm_out (uint8);
+ * draws_out[i] (may be NULL) = 32-bit words consumed by batch i. */
+int ddm_mt_perms(uint32_t* key, int32_t* pos, const int32_t* batch_len, int64_t n_batches,
+                 uint8_t* perm_out, int64_t* draws_out);
+
+/* `randint(2**31 - 1)` x count (the per-tree seeds of RandomForestClassifier.fit). */
+int ddm_mt_randint31(uint32_t* key, int32_t* pos, int64_t count, int64_t* out);
+
+/* Advance the generator by n_draws 32-bit words. */
+int ddm_mt_skip(uint32_t* key, int32_t* pos, int64_t n_draws);
+
+/* ---- synthetic inputs (benchmark configs) ------------------------- */
+
+/* Labels of a class-block stream partitioned as DDM_Process.py:225 (row % n_parts):
+ * partition row r is global row g = r*n_parts + part, class (g / block_rows) % n_classes. */
+int ddm_synth_block_labels(int32_t* y, int64_t n_rows, int64_t part, int64_t n_parts,
+                           int64_t block_rows, int32_t n_classes, ddm_stream_t stream);
+
+/* Noise-free separable features for labels y: X[f*ld + r] = base(y[r], f) + noise*u,
+ * u ~ U[0,1) from a counter hash of (seed, row0 + r*row_stride, f). */
+int ddm_synth_features(float* X, int64_t ld, int32_t n_features, const int32_t* y, int64_t n_rows,
+                       int64_t row0, int64_t row_stride, uint64_t seed, float noise,
+                       ddm_stream_t stream);
+
+/* C4 streams: stream s has Bernoulli(r0) errors, r0 ~ U(0.01, 0.2), switching at a random
+ * row to r0 + U(0.05, 0.3).  err is [n_streams][len] bytes. */
+int ddm_synth_bernoulli_streams(uint8_t* err, int64_t n_streams, int64_t len, uint64_t seed,
+                                ddm_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DDM_AMD_H */

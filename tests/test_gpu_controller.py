@@ -1,0 +1,93 @@
+"""The drop-in `run_DDM_loop` on the GPU vs the reference's own outputs (golden fixtures from
+executing DDM_Process.py:94-213) — bit-exact events for every (MULT, INSTANCES) config."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from conftest import golden_configs, golden_partitions
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("mult,inst", golden_configs())
+def test_drop_in_matches_reference(mult, inst):
+    import ddm_amd
+    for d, part, expect in golden_partitions(mult, inst):
+        np.random.seed(1000 + d)
+        if expect is None:
+            with pytest.raises(ValueError, match="No objects to concatenate"):
+                ddm_amd.run_DDM_loop(part)
+            continue
+        got = ddm_amd.run_DDM_loop(part)
+        assert list(got.columns) == ddm_amd.OUTPUT_COLUMNS
+        assert list(got.index) == [0] * len(expect)
+        assert np.array_equal(got.to_numpy(), expect), (mult, inst, d)
+
+
+def test_global_rng_left_where_reference_leaves_it():
+    import ddm_amd
+    from oracle.controller import run_partition
+    d, part, expect = golden_partitions(2, 4)[2]
+    np.random.seed(5)
+    ddm_amd.run_DDM_loop(part)
+    after_gpu = np.random.get_state()
+    np.random.seed(5)
+    run_partition(part[[str(i) for i in range(21)]].to_numpy(), part["target"].to_numpy(), part.index.to_numpy(),
+                  part["full_df_row_number"].to_numpy())
+    after_ref = np.random.get_state()
+    assert np.array_equal(after_gpu[1], after_ref[1]) and after_gpu[2] == after_ref[2]
+
+
+@pytest.mark.parametrize("win,maxwin", [(1, 1), (1, 4), (3, 1000), (10_000, 1 << 16)])
+def test_window_schedule_does_not_change_results(win, maxwin):
+    import ddm_amd
+    for d, part, expect in golden_partitions(4, 4):
+        np.random.seed(1000 + d)
+        s = ddm_amd.DDMSettings(window_batches=win, max_window_batches=maxwin)
+        got = ddm_amd.run_DDM_loop(part, settings=s)
+        assert np.array_equal(got.to_numpy(), expect)
+
+
+def test_edge_partitions():
+    import ddm_amd
+    part = pd.DataFrame({"0": np.arange(100.0), "target": np.zeros(100, int), "full_df_row_number": np.arange(100)})
+    with pytest.raises(ValueError, match="No objects to concatenate"):
+        ddm_amd.run_DDM_loop(part)
+    with pytest.raises(IndexError):
+        ddm_amd.run_DDM_loop(part.iloc[:0])
+    one = ddm_amd.run_DDM_loop(pd.concat([part, part.iloc[:1]]).reset_index(drop=True))
+    assert one.shape == (1, 4)
+
+
+def test_concurrent_partitions_on_streams():
+    """All partitions of a config at once, one stream + thread each (apply_in_pandas path)."""
+    from ddm_amd.partition import run_partitions
+    parts = golden_partitions(4, 16)
+    outs = run_partitions([(d, p) for d, p, _ in parts], {d: 1000 + d for d, _, _ in parts})
+    for d, _, expect in parts:
+        assert np.array_equal(outs[d].to_numpy(), expect), d
+
+
+def test_synthetic_rialto_stream_vs_oracle():
+    """Device-generated rialto-shaped partition (27 features, class blocks not aligned to
+    batches) through the GPU controller == the oracle on the same rows."""
+    from ddm_amd import kernels
+    from ddm_amd.controller import DevicePartition, PartitionRunner
+    from ddm_amd.params import DDMSettings
+    from ddm_amd.rng import MTStream
+    from oracle.controller import run_partition
+    dev = torch.device("cuda", 0)
+    n, F, parts, block = 30_000, 27, 4, 10_037
+    part = DevicePartition.allocate(n, F, dev)
+    kernels.synth_block_labels(part.y[:n], part=1, n_parts=parts, block_rows=block, n_classes=10)
+    kernels.synth_features(part.X, part.y[:n], row0=1, row_stride=parts, seed=99, noise=0.04)
+    torch.cuda.synchronize()
+    X = part.X[:, :n].t().contiguous().cpu().numpy()
+    y = part.y[:n].cpu().numpy().astype(np.int64)
+    runner = PartitionRunner(part, DDMSettings())
+    got = runner.run(MTStream.from_seed(321))
+    np.random.seed(321)
+    want = run_partition(X.astype(np.float64), y, np.arange(n), np.arange(n))
+    assert np.array_equal(got[:, 0], want[:, 0]) and np.array_equal(got[:, 1], want[:, 2])
+    assert (want[:, 2] >= 0).sum() >= 3
