@@ -1,0 +1,298 @@
+#!/usr/bin/env python
+"""Benchmark: stream rows/s through predict + DDM (BASELINE.json `metric`).
+
+Default workload = BASELINE.json configs[2] per GPU: a synthetic rialto-shaped stream
+(27 float32 features, 10 classes in class blocks, noise-free separable classes ->
+sparse abrupt drifts; rialto.csv is not shipped) partitioned `row % INSTANCES`
+(DDM_Process.py:225) into 8 partitions of 125M rows = 1B rows per GPU, class blocks
+of 10,000,037 global rows (~100 drifts per partition, block edges not batch aligned).
+One step = every partition of this rank through the full reference hot path
+(run_DDM_loop, DDM_Process.py:170-213): batch shuffles from the partition's MT19937,
+forest predict + DDM scan on the GPU, refit on every drift (host sklearn, spawn pool).
+Inputs are resident in HBM before the timed region.  Weak scaling: each rank owns its
+own 8 partitions (global ids rank*8 + p, INSTANCES = 8 * world), no collective on the
+data path; the per-rank event counts are all-reduced once for the self-check.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c4]
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "distributed-drift-detection_amd"))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="c3", choices=["c3", "c4"])
+    ap.add_argument("--parts", type=int, default=8, help="partitions per GPU")
+    ap.add_argument("--rows-per-part", type=int, default=125_000_000)
+    ap.add_argument("--block-rows", type=int, default=10_000_037, help="global class-block length (C3)")
+    ap.add_argument("--features", type=int, default=27)
+    ap.add_argument("--refit", default="native", choices=["native", "sklearn"],
+                    help="native: ddm_rf_fit (identical trees to sklearn 1.7.2); sklearn: host sklearn")
+    ap.add_argument("--refit-workers", type=int, default=8, help="sklearn refit: spawn-pool size (0 = in-process)")
+    ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-sample-rows", type=int, default=150_000)
+    ap.add_argument("--c4-streams", type=int, default=1_000_000)
+    ap.add_argument("--c4-len", type=int, default=4096)
+    return ap.parse_args()
+
+
+def dist_env():
+    return int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")), \
+        int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def traffic_from_profile(name, rows_per_launch):
+    """HBM bytes per launch from the committed PMC summary (profiles/), or None."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f).get(name)
+        return None if d is None else d["hbm_bytes_per_row"] * rows_per_launch
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def cpu_baseline_c3(part, n_rows, seed):
+    """The oracle's pandas/iterrows restatement of run_DDM_loop (kind "port") on the first
+    n_rows of partition 0, one process, n_jobs=1."""
+    import numpy as np
+    import pandas as pd
+    from oracle.controller import run_partition_frames
+    n = min(n_rows, part.n)
+    X = part.X[:, :n].t().contiguous().cpu().numpy().astype(np.float64)
+    y = part.y[:n].cpu().numpy().astype(np.int64)
+    feats = [str(i) for i in range(X.shape[1])]
+    pdf = pd.DataFrame(X, columns=feats)
+    pdf["target"] = y
+    pdf["full_df_row_number"] = np.arange(n)
+    np.random.seed(seed)
+    t0 = time.perf_counter()
+    run_partition_frames(pdf, feats, n_jobs=1)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "rows/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} rows of partition 0 of the same workload, oracle/controller.py "
+                      f"run_partition_frames (pandas sample + sklearn RF n_jobs=1 + iterrows DDM), "
+                      f"{dt:.1f} s"}
+
+
+def run_c3(args, world, rank, dev, torch, dist):
+    import numpy as np
+    from ddm_amd import kernels
+    from ddm_amd.controller import DevicePartition, PartitionRunner
+    from ddm_amd.params import DDMSettings
+    from ddm_amd.refit import RefitPool
+    from ddm_amd.rng import MTStream
+
+    refit = args._pool
+    if args.refit == "sklearn" and refit is None:
+        from ddm_amd.controller import sklearn_refit
+        refit = sklearn_refit(DDMSettings())
+    instances = args.parts * world
+    block = args.block_rows if world == 1 else (args.block_rows // 8) * instances + 37
+    n = args.rows_per_part
+    parts, runners = [], []
+    settings = DDMSettings()
+    for p in range(args.parts):
+        gid = rank * args.parts + p
+        part = DevicePartition.allocate(n, args.features, dev)
+        kernels.synth_block_labels(part.y[:n], gid, instances, block, 10)
+        kernels.synth_features(part.X, part.y[:n], gid, instances, args.seed, 0.04)
+        parts.append((gid, part))
+        runners.append(PartitionRunner(part, settings, torch.cuda.Stream(dev), refit=refit, timing=True))
+    torch.cuda.synchronize()
+
+    results = {}
+
+    def one(i):
+        gid, _ = parts[i]
+        results[gid] = runners[i].run(MTStream.from_seed(args.seed + gid))
+
+    def step():
+        ths = [threading.Thread(target=one, args=(i,)) for i in range(len(parts))]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        if len(results) != len(parts):
+            raise RuntimeError("a partition runner failed")
+
+    for _ in range(args.warmup):
+        step()
+    ref_events = {g: r.copy() for g, r in results.items()}
+    from ddm_amd.controller import RunStats
+    for r in runners:
+        r.stats = RunStats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        results.clear()
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    for g, r in results.items():          # every step reproduces the same events
+        if args.warmup and not np.array_equal(r, ref_events[g]):
+            raise RuntimeError(f"partition {g}: events differ between steps")
+    st = [r.stats for r in runners]
+    agg = {k: sum(getattr(s, k) for s in st) for k in ("epochs", "refits", "predicted_rows", "refit_s",
+                                                        "predict_ms", "predict_bytes", "scan_ms", "scan_rows")}
+    drifts = int(sum((r[:, 1] >= 0).sum() for r in results.values()))
+    warns = int(sum((r[:, 0] >= 0).sum() for r in results.values()))
+    rows_rank = n * args.parts * args.steps
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        cpu = cpu_baseline_c3(parts[0][1], args.cpu_sample_rows, args.seed)
+    launches = max(1, agg["epochs"])
+    rows_per_launch = agg["predicted_rows"] / launches
+    avg_ms = agg["predict_ms"] / launches
+    achieved = (agg["predict_bytes"] / launches) / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    info = {
+        "workload": f"configs[2]: synthetic rialto-shaped stream, {args.features} f32 features, 10 classes, "
+                    f"class blocks of {block} global rows, INSTANCES={instances} (row % INSTANCES), "
+                    f"{args.parts} partitions x {n} rows per GPU",
+        "rows_per_gpu_step": n * args.parts, "partitions_per_gpu": args.parts,
+        "refit": ("native ddm_rf_fit (sklearn 1.7.2 RandomForestClassifier restated, identical trees), "
+                  "one host thread per partition") if args.refit == "native" else
+                 ("host sklearn RandomForestClassifier(100 trees), " + ("spawn pool" if refit else "in-process")),
+    }
+    extra = {"drifts_per_step": drifts, "warnings_per_step": warns,
+             "refits_per_step": agg["refits"] / args.steps, "epochs_per_step": agg["epochs"] / args.steps,
+             "speculation_overhead": agg["predicted_rows"] / max(1, rows_rank),
+             "refit_s_per_step_sum": agg["refit_s"] / args.steps,
+             "predict_kernel_ms_per_step": agg["predict_ms"] / args.steps,
+             "scan_kernel_ms_per_step": agg["scan_ms"] / args.steps}
+    roofline = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_from_profile("ddm_forest_predict", rows_per_launch),
+                "kernel": "ddm_forest_predict", "alg_bytes_per_row": "4*F_used + 6",
+                "avg_launch_ms": avg_ms, "avg_rows_per_launch": rows_per_launch}
+    return rows_rank, elapsed, info, extra, roofline, cpu
+
+
+def run_c4(args, world, rank, dev, torch, dist):
+    """configs[3]: 1M independent error streams x 4096 rows, DDM only, fresh DDM after each change."""
+    import numpy as np
+    from ddm_amd import kernels
+    S, L = args.c4_streams, args.c4_len
+    err = torch.empty(S * L + 16, dtype=torch.uint8, device=dev)
+    kernels.synth_bernoulli_streams(err, S, L, args.seed + rank)
+    off = torch.arange(S + 1, dtype=torch.int64, device=dev) * L
+    nb = (L + 99) // 100
+    base = torch.arange(S, dtype=torch.int64, device=dev) * nb
+    ev = torch.empty((S * nb, 2), dtype=torch.int32, device=dev)
+    state0 = torch.from_numpy(kernels.fresh_states(S).view(np.uint8)).to(dev)
+    state = torch.empty_like(state0)
+    prm = kernels.params_struct()
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def step(timed):
+        state.copy_(state0)
+        if timed:
+            e0.record(stream)
+        kernels.scan_streams(err, off, prm, state, base, S * nb, ev, mode=1, stream=stream)
+        if timed:
+            e1.record(stream)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    kms = 0.0
+    for _ in range(args.steps):
+        step(True)
+        torch.cuda.synchronize()
+        kms += e0.elapsed_time(e1)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    changes = int((ev[:, 1] >= 0).sum().item())
+    rows = S * L * args.steps
+    avg_ms = kms / args.steps
+    alg = S * L * 1.0 + S * nb * 8
+    achieved = alg / (avg_ms * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        from oracle.ddm import scan_stream
+        e = err[:2000 * L].cpu().numpy()
+        t = time.perf_counter()
+        k = 0
+        while time.perf_counter() - t < 10 and k < 2000:
+            scan_stream(e[k * L:(k + 1) * L], mode="restart")
+            k += 1
+        dt = time.perf_counter() - t
+        cpu = {"value": k * L / dt, "unit": "rows/s", "cores": 1, "kind": "port",
+               "sample": f"{k} streams x {L} rows, oracle/ddm.py scan_stream (pure-Python DDM, no iterrows)"}
+    info = {"workload": f"configs[3]: {S} independent streams x {L} rows (Bernoulli r0~U(.01,.2) stepping "
+                        f"by U(.05,.3)), DDM only, fresh DDM at the batch after each change"}
+    extra = {"changes_per_step": changes, "scan_kernel_ms": avg_ms}
+    roofline = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_from_profile("ddm_scan_streams", S * L),
+                "kernel": "ddm_scan_streams", "alg_bytes_per_row": "1 + 8/100",
+                "avg_launch_ms": avg_ms, "note": "fp64-VALU bound: ~45 VALU/row recurrence"}
+    return rows, elapsed, info, extra, roofline, cpu
+
+
+def main():
+    args = parse()
+    world, rank, local_rank = dist_env()
+    args._pool = None
+    if args.workload == "c3" and args.refit == "sklearn" and args.refit_workers > 0:
+        # spawn the host refit workers BEFORE anything initialises the GPU
+        # (--refit-workers 0: in-process refits, for runs under a profiler)
+        from ddm_amd.refit import RefitPool
+        args._pool = RefitPool(args.refit_workers)
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    fn = run_c3 if args.workload == "c3" else run_c4
+    rows_rank, elapsed, info, extra, roofline, cpu = fn(args, world, rank, dev, torch, dist)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor([rows_rank], dtype=torch.float64, device=dev)
+        dist.all_reduce(r)
+        rows_total = float(r.item())
+    else:
+        rows_total = float(rows_rank)
+    if rank == 0:
+        out = {"metric": "stream rows/sec through predict+DDM (node, 1/2/4/8 GPU) + % HBM roofline",
+               "value": rows_total / elapsed, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+               "data": "synthetic (rialto.csv not shipped); generated in HBM by ddm_synth_*",
+               "config": dict(info, parallelism=f"partitions over {world} GPU(s), no data-path collective"),
+               "roofline": roofline, "cpu_baseline": cpu, "breakdown": extra}
+        print(json.dumps(out), flush=True)
+    if args._pool is not None:
+        args._pool.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -20,3 +20,21 @@ void set_error(const char* fmt, ...) {
 extern "C" int ddm_abi_version(void) { return DDM_AMD_ABI_VERSION; }
 
 extern "C" const char* ddm_last_error(void) { return ddm::g_last_error; }
+
+extern "C" int ddm_event_create(ddm_event_t* ev) {
+    if (!ev) return DDM_E_ARG;
+    hipEvent_t e;
+    if (int rc = ddm::hip_status(hipEventCreate(&e), "ddm_event_create")) return rc;
+    *ev = reinterpret_cast<ddm_event_t>(e);
+    return 0;
+}
+
+extern "C" int ddm_event_destroy(ddm_event_t ev) {
+    return ddm::hip_status(hipEventDestroy(reinterpret_cast<hipEvent_t>(ev)), "ddm_event_destroy");
+}
+
+extern "C" int ddm_event_elapsed_ms(ddm_event_t begin, ddm_event_t end, float* ms) {
+    if (!ms) return DDM_E_ARG;
+    return ddm::hip_status(hipEventElapsedTime(ms, reinterpret_cast<hipEvent_t>(begin), reinterpret_cast<hipEvent_t>(end)),
+                           "ddm_event_elapsed_ms");
+}

@@ -196,7 +196,7 @@ extern "C" int ddm_scan_streams(const uint8_t* err, const int64_t* stream_off, i
                                 const ddm_params* prm, ddm_state* state_io, const uint64_t* first_nz,
                                 const int64_t* batch_base, int64_t n_batches_total, int32_t* ev_out,
                                 int32_t* stop_out, int64_t* nev_out, int32_t mode, double* ps_out,
-                                ddm_stream_t stream) {
+                                ddm_stream_t stream, ddm_event_t ev_begin, ddm_event_t ev_end) {
     if (!err || !stream_off || !prm || !state_io || !batch_base || !ev_out || n_streams < 0 ||
         n_batches_total < 0 || prm->per_batch <= 0 || (mode != 0 && mode != 1)) {
         ddm::set_error("ddm_scan_streams: invalid argument");
@@ -209,7 +209,11 @@ extern "C" int ddm_scan_streams(const uint8_t* err, const int64_t* stream_off, i
         return rc;
     const int threads = n_streams >= 256 ? 256 : 64;
     const int64_t blocks = ddm::ceil_div(n_streams, threads);
+    if (ev_begin)
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
     hipLaunchKernelGGL(k_scan_streams, dim3((unsigned)blocks), dim3(threads), 0, s, err, stream_off, n_streams, *prm,
                        state_io, first_nz, batch_base, ev_out, stop_out, nev_out, (int)mode, ps_out);
+    if (ev_end)
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
     return ddm::launch_status("ddm_scan_streams");
 }

@@ -142,7 +142,8 @@ predict_fn pick(bool pure, int k) {
 extern "C" int ddm_forest_predict(const float* X, int64_t ld, int32_t n_features, const int32_t* y,
                                   const uint8_t* perm, int64_t pos_begin, int64_t pos_end, int32_t per_batch,
                                   const ddm_forest* forest, uint8_t* err_out, uint64_t* first_err,
-                                  int32_t* pred_out, ddm_stream_t stream) {
+                                  int32_t* pred_out, ddm_stream_t stream, ddm_event_t ev_begin,
+                                  ddm_event_t ev_end) {
     if (!X || !y || !perm || !forest || !err_out || !forest->nodes || !forest->roots || !forest->classes ||
         per_batch <= 0 || per_batch > 256 || pos_begin < 0 || pos_end < pos_begin || n_features <= 0 ||
         ld <= 0 || forest->n_trees <= 0 || forest->n_nodes <= 0 || forest->n_classes <= 0) {
@@ -166,9 +167,13 @@ extern "C" int ddm_forest_predict(const float* X, int64_t ld, int32_t n_features
     const predict_fn fn = use_lds ? pick<true>(forest->pure, forest->n_classes)
                                   : pick<false>(forest->pure, forest->n_classes);
     const int64_t blocks = std::min<int64_t>(ddm::ceil_div(n, kThreads), 256 * 8);
+    if (ev_begin)
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
     hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kThreads), use_lds ? lds : 0, s, X, ld, y, perm, pos_begin,
                        pos_end, (int64_t)per_batch, forest->nodes, forest->roots, forest->leaf_value,
                        forest->classes, forest->n_trees, forest->n_classes, forest->n_nodes, err_out,
                        reinterpret_cast<unsigned long long*>(first_err), pred_out);
+    if (ev_end)
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
     return ddm::launch_status("ddm_forest_predict");
 }

@@ -5,11 +5,22 @@ Drop-in for the reference's grouped-map partition function `run_DDM_loop`
 (forest predict, DDM scan) behind a C-ABI (include/ddm_amd.h) bound with ctypes;
 PyTorch-ROCm provides device buffers, streams and torch.distributed (RCCL).
 
-Importing the package loads libddm_amd.so and fails loudly if it is not built.
+The package namespace is lazy: `ddm_amd.treepack` / `ddm_amd.refit` stay importable in
+host-only worker processes without torch; everything else loads libddm_amd.so through
+`ddm_amd._capi`, which raises if the library is not built (there is no CPU fallback).
 """
-from ._capi import DdmError, lib  # noqa: F401  (fails loudly without the HIP library)
-from .controller import DevicePartition, PartitionRunner, run_DDM_loop, run_partition_frame  # noqa: F401
-from .params import OUTPUT_COLUMNS, SCHEMA, DDMSettings  # noqa: F401
-from .rng import MTStream  # noqa: F401
+import importlib
 
 __version__ = "0.1.0"
+
+_EXPORTS = {
+    "run_DDM_loop": "controller", "run_partition_frame": "controller", "DevicePartition": "controller",
+    "PartitionRunner": "controller", "DDMSettings": "params", "OUTPUT_COLUMNS": "params", "SCHEMA": "params",
+    "MTStream": "rng", "DdmError": "_capi", "lib": "_capi",
+}
+
+
+def __getattr__(name):
+    if name in _EXPORTS:
+        return getattr(importlib.import_module(f".{_EXPORTS[name]}", __name__), name)
+    raise AttributeError(name)

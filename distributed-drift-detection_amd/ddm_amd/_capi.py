@@ -11,10 +11,12 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
+DDM_E_NAN = 1003
+DDM_E_IMPURE = 1004
 
 
 class DdmParams(ctypes.Structure):
@@ -45,12 +47,16 @@ SIGNATURES = {
     "ddm_abi_version": (ctypes.c_int, []),
     "ddm_last_error": (ctypes.c_char_p, []),
     "ddm_forest_predict": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _i64, _i64, _i32, ctypes.POINTER(DdmForest),
-                                          _vp, _vp, _vp, _vp]),
+                                          _vp, _vp, _vp, _vp, _vp, _vp]),
     "ddm_scan_streams": (ctypes.c_int, [_vp, _vp, _i64, ctypes.POINTER(DdmParams), _vp, _vp, _vp, _i64, _vp, _vp,
-                                        _vp, _i32, _vp, _vp]),
+                                        _vp, _i32, _vp, _vp, _vp, _vp]),
+    "ddm_event_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
+    "ddm_event_destroy": (ctypes.c_int, [_vp]),
+    "ddm_event_elapsed_ms": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(ctypes.c_float)]),
     "ddm_mt_perms": (ctypes.c_int, [_vp, _pi32, _vp, _i64, _vp, _vp]),
     "ddm_mt_randint31": (ctypes.c_int, [_vp, _pi32, _i64, _vp]),
     "ddm_mt_skip": (ctypes.c_int, [_vp, _pi32, _i64]),
+    "ddm_rf_fit": (ctypes.c_int, [_vp, _i32, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp]),
     "ddm_synth_block_labels": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i32, _vp]),
     "ddm_synth_features": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _i64, _i64, _u64, _f32, _vp]),
     "ddm_synth_bernoulli_streams": (ctypes.c_int, [_vp, _i64, _i64, _u64, _vp]),

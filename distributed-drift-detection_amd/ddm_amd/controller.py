@@ -28,6 +28,7 @@ from . import kernels
 from .forest import DeviceForest, pack_sklearn
 from .params import OUTPUT_COLUMNS, DDMSettings, infer_x_features
 from .rng import MTStream
+from .trainer import native_refit
 
 # control block layout (bytes) shared by host (pinned) and device
 _FIRST_ERR, _NEV, _STOP, _OFF, _BASE, _STATE, _CTRL_BYTES = 0, 8, 16, 24, 40, 64, 128
@@ -96,11 +97,12 @@ def sklearn_refit(settings):
 
 
 class RunStats:
-    __slots__ = ("epochs", "refits", "predicted_rows", "refit_s", "gpu_s", "host_s")
+    __slots__ = ("epochs", "refits", "predicted_rows", "refit_s", "gpu_s", "host_s", "predict_ms", "predict_bytes",
+                 "scan_ms", "scan_rows")
 
     def __init__(self):
-        self.epochs = self.refits = self.predicted_rows = 0
-        self.refit_s = self.gpu_s = self.host_s = 0.0
+        self.epochs = self.refits = self.predicted_rows = self.predict_bytes = self.scan_rows = 0
+        self.refit_s = self.gpu_s = self.host_s = self.predict_ms = self.scan_ms = 0.0
 
     def as_dict(self):
         return {k: getattr(self, k) for k in self.__slots__}
@@ -109,11 +111,15 @@ class RunStats:
 class PartitionRunner:
     """Runs the speculative predict+scan epochs of one partition on one HIP stream."""
 
-    def __init__(self, part, settings=None, stream=None, refit=None):
+    def __init__(self, part, settings=None, stream=None, refit=None, timing=False):
         self.part = part
+        self.timing = timing
+        # HIP events recorded by the C-ABI right around each launch on this runner's stream
+        self.t_pred = kernels.LaunchTimer() if timing else None
+        self.t_scan = kernels.LaunchTimer() if timing else None
         self.s = settings or DDMSettings()
         self.stream = stream or torch.cuda.Stream(part.device)
-        self.refit = refit or sklearn_refit(self.s)
+        self.refit = refit or native_refit(self.s)
         self.params = kernels.params_struct(self.s.min_num_instances, self.s.per_batch, self.s.warning_level,
                                             self.s.out_control_level)
         n, dev = part.n, part.device
@@ -190,15 +196,20 @@ class PartitionRunner:
                 self.perm_d[p0:p1].copy_(self.perm_h[p0:p1], non_blocking=True)
                 kernels.forest_predict(part.X, part.y, self.perm_d, p0, p1, pb, forest, self.err_d,
                                        first_err=self.ctrl_d[_FIRST_ERR:_FIRST_ERR + 8].view(torch.int64),
-                                       stream=stream)
+                                       stream=stream, timer=self.t_pred)
                 kernels.scan_streams_raw(self.err_d.data_ptr(), base + _OFF, 1, self.params, base + _STATE,
                                          base + _BASE, b_end - j, self.ev_d.data_ptr(), base + _FIRST_ERR,
-                                         base + _STOP, base + _NEV, 0, None, stream)
+                                         base + _STOP, base + _NEV, 0, None, stream, self.t_scan)
                 self.ctrl_h.copy_(self.ctrl_d, non_blocking=True)
             stream.synchronize()
             stop = int(self._ctrl(_STOP, np.int32)[0])
             nev = int(self._ctrl(_NEV, np.int64)[0])
             last = j + stop if stop >= 0 else b_end - 1
+            if self.timing:
+                st.predict_ms += self.t_pred.elapsed_ms()
+                st.scan_ms += self.t_scan.elapsed_ms()
+                st.predict_bytes += (p1 - p0) * (4 * forest.packed.features_used + 6)
+                st.scan_rows += min(p1, (last + 1) * pb) - p0
             if nev:
                 k = last - j + 1
                 with torch.cuda.stream(stream):
@@ -209,13 +220,13 @@ class PartitionRunner:
                     q = ev[:, c]
                     hit = np.nonzero(q >= 0)[0]
                     b = j + hit
-                    out[b - 1, c] = b * pb + perm[b * pb + q[hit]]
+                    out[b - 1, c] = b * pb + perm[b * pb + q[hit]].astype(np.int64)
             st.gpu_s += time.perf_counter() - t0
             st.epochs += 1
             st.predicted_rows += p1 - p0
             if stop >= 0:
                 d = j + stop
-                train_rows = (d * pb + perm[d * pb:d * pb + blen[d]]).astype(np.int64)
+                train_rows = d * pb + perm[d * pb:d * pb + blen[d]].astype(np.int64)
                 retrain = True
                 rng.restore(snap)                              # RNG right after batch d's shuffle
                 draw(gen_from, d + 1)

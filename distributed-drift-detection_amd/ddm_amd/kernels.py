@@ -38,8 +38,31 @@ def _ptr(t):
     return None if t is None else t.data_ptr()
 
 
+class LaunchTimer:
+    """A (begin, end) HIP event pair recorded by the C-ABI around one kernel launch."""
+
+    def __init__(self):
+        self.ev = [ctypes.c_void_p(), ctypes.c_void_p()]
+        for e in self.ev:
+            check(lib.ddm_event_create(ctypes.byref(e)), "ddm_event_create")
+
+    def elapsed_ms(self):
+        ms = ctypes.c_float()
+        check(lib.ddm_event_elapsed_ms(self.ev[0], self.ev[1], ctypes.byref(ms)), "ddm_event_elapsed_ms")
+        return ms.value
+
+    def __del__(self):
+        for e in getattr(self, "ev", []):
+            if e.value:
+                lib.ddm_event_destroy(e)
+
+
+def _evs(timer):
+    return (None, None) if timer is None else (timer.ev[0], timer.ev[1])
+
+
 def forest_predict(X, y, perm, pos_begin, pos_end, per_batch, forest, err, first_err=None, pred=None,
-                   stream=None):
+                   stream=None, timer=None):
     """X: float32 [F, ld] (columnar), y int32 [ld], perm/err uint8 indexed by DDM position."""
     assert X.dtype == torch.float32 and X.dim() == 2 and X.is_contiguous()
     assert y.dtype == torch.int32 and perm.dtype == torch.uint8 and err.dtype == torch.uint8
@@ -47,25 +70,25 @@ def forest_predict(X, y, perm, pos_begin, pos_end, per_batch, forest, err, first
     F, ld = X.shape
     check(lib.ddm_forest_predict(X.data_ptr(), ld, F, y.data_ptr(), perm.data_ptr(), int(pos_begin), int(pos_end),
                                  int(per_batch), ctypes.byref(forest.desc), err.data_ptr(), _ptr(first_err),
-                                 _ptr(pred), _stream(X, stream)), "ddm_forest_predict")
+                                 _ptr(pred), _stream(X, stream), *_evs(timer)), "ddm_forest_predict")
 
 
 def scan_streams(err, offsets, params, state, batch_base, n_batches_total, ev, first_nz=None, stop=None, nev=None,
-                 mode=0, ps=None, stream=None):
+                 mode=0, ps=None, stream=None, timer=None):
     """err uint8 (padded to a multiple of 16 past the last offset); offsets/batch_base int64;
     state: uint8 tensor holding n_streams ddm_state records; ev int32 [n_batches_total, 2]."""
     check(lib.ddm_scan_streams(err.data_ptr(), _ptr(offsets), offsets.numel() - 1, ctypes.byref(params),
                                _ptr(state), _ptr(first_nz), _ptr(batch_base), int(n_batches_total), _ptr(ev),
-                               _ptr(stop), _ptr(nev), int(mode), _ptr(ps), _stream(err, stream)),
+                               _ptr(stop), _ptr(nev), int(mode), _ptr(ps), _stream(err, stream), *_evs(timer)),
           "ddm_scan_streams")
 
 
 def scan_streams_raw(err_ptr, offsets_ptr, n_streams, params, state_ptr, batch_base_ptr, n_batches_total, ev_ptr,
-                     first_nz_ptr, stop_ptr, nev_ptr, mode, ps_ptr, stream):
+                     first_nz_ptr, stop_ptr, nev_ptr, mode, ps_ptr, stream, timer=None):
     """Pointer-level variant used by the controller (all pointers are device addresses)."""
     check(lib.ddm_scan_streams(err_ptr, offsets_ptr, n_streams, ctypes.byref(params), state_ptr, first_nz_ptr,
                                batch_base_ptr, n_batches_total, ev_ptr, stop_ptr, nev_ptr, mode, ps_ptr,
-                               ctypes.c_void_p(stream.cuda_stream)), "ddm_scan_streams")
+                               ctypes.c_void_p(stream.cuda_stream), *_evs(timer)), "ddm_scan_streams")
 
 
 def synth_block_labels(y, part, n_parts, block_rows, n_classes, stream=None):

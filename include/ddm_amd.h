@@ -16,6 +16,8 @@
  *   ddm_mt_randint31     <- the 100 `randint(2**31-1)` tree seeds RandomForestClassifier
  *                           .fit draws from the same global RNG (:102-103)
  *   ddm_mt_skip          <- re-positioning the global RNG after a speculative window
+ *   ddm_rf_fit           <- train_rf (DDM_Process.py:98-105): RandomForestClassifier.fit
+ *                           restated from scikit-learn 1.7.2 (identical trees), host code
  *   ddm_synth_*          <- synthetic rialto/outdoor-shaped inputs for the benchmark
  *                           (rialto.csv is not shipped, .MISSING_LARGE_BLOBS:1)
  *
@@ -34,12 +36,15 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 1
+#define DDM_AMD_ABI_VERSION 2
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
+#define DDM_E_NAN        1003   /* ddm_rf_fit: NaN in X (use sklearn for missing values) */
+#define DDM_E_IMPURE     1004   /* ddm_rf_fit: impure forest needs a (larger) leaf_value buffer */
 
 typedef struct ihipStream_t* ddm_stream_t;   /* == hipStream_t */
+typedef struct ihipEvent_t* ddm_event_t;     /* == hipEvent_t  */
 
 /* DDM parameters: DDM_Process.py:25,27-29 (PER_BATCH, MIN_NUM_DDM_VALS, WARNING_LEVEL,
  * CHANGE_LEVEL).  Reference values 100 / 3 / 0.5 / 1.5. */
@@ -93,11 +98,14 @@ const char* ddm_last_error(void);
  * (X[f*ld + row], the float32 cast sklearn applies), y int32 labels.
  * err_out[g] = (classes[argmax] != y[row]); first_err (device uint64, may be NULL) is
  * set to the smallest g with an error, UINT64_MAX if none (written by this call);
- * pred_out (may be NULL) receives the predicted label per g. */
+ * pred_out (may be NULL) receives the predicted label per g.
+ * ev_begin / ev_end (may be NULL) are recorded on `stream` immediately before and after
+ * the kernel launch (launch-duration measurement without host gaps). */
 int ddm_forest_predict(const float* X, int64_t ld, int32_t n_features, const int32_t* y,
                        const uint8_t* perm, int64_t pos_begin, int64_t pos_end,
                        int32_t per_batch, const ddm_forest* forest, uint8_t* err_out,
-                       uint64_t* first_err, int32_t* pred_out, ddm_stream_t stream);
+                       uint64_t* first_err, int32_t* pred_out, ddm_stream_t stream,
+                       ddm_event_t ev_begin, ddm_event_t ev_end);
 
 /* run_DDM over every batch of every stream.  Stream s is err[stream_off[s] ..
  * stream_off[s+1]) (device int64 offsets; err readable up to the next multiple of 16
@@ -112,12 +120,19 @@ int ddm_forest_predict(const float* X, int64_t ld, int32_t n_features, const int
  * mode 1: fresh DDM at the next batch after a change (DDM-only streams).
  * stop_out (device int32, may be NULL): batch of the first change or -1 (mode 0).
  * nev_out (device int64, may be NULL): number of batches with an event per stream.
- * ps_out (device double [rows][2], may be NULL): p and s after each processed row. */
+ * ps_out (device double [rows][2], may be NULL): p and s after each processed row.
+ * ev_begin / ev_end (may be NULL): as for ddm_forest_predict. */
 int ddm_scan_streams(const uint8_t* err, const int64_t* stream_off, int64_t n_streams,
                      const ddm_params* prm, ddm_state* state_io, const uint64_t* first_nz,
                      const int64_t* batch_base, int64_t n_batches_total, int32_t* ev_out,
                      int32_t* stop_out, int64_t* nev_out, int32_t mode, double* ps_out,
-                     ddm_stream_t stream);
+                     ddm_stream_t stream, ddm_event_t ev_begin, ddm_event_t ev_end);
+
+/* Timing events for the ev_begin / ev_end arguments (hipEventCreate / Destroy /
+ * ElapsedTime; elapsed needs both events completed, e.g. after a stream sync). */
+int ddm_event_create(ddm_event_t* ev);
+int ddm_event_destroy(ddm_event_t ev);
+int ddm_event_elapsed_ms(ddm_event_t begin, ddm_event_t end, float* ms);
 
 /* ---- host-side MT19937 (numpy legacy RandomState layout: key[624], pos) ---------- */
 
@@ -132,6 +147,20 @@ int ddm_mt_randint31(uint32_t* key, int32_t* pos, int64_t count, int64_t* out);
 
 /* Advance the generator by n_draws 32-bit words. */
 int ddm_mt_skip(uint32_t* key, int32_t* pos, int64_t n_draws);
+
+/* ---- host forest refit ------------------------------------------------------------ */
+
+/* RandomForestClassifier(n_estimators=n_trees).fit(X, y) exactly as scikit-learn 1.7.2
+ * builds it (bootstrap, max_features=sqrt, Gini, fully grown), given the per-tree seeds
+ * the forest draws from the global RNG (ddm_mt_randint31 x n_trees).  X: host float32
+ * [n][n_features] row-major (no NaN), y_idx: class index per row (np.unique inverse).
+ * Writes the packed forest: nodes (capacity >= n_trees*(2n-1)), roots[n_trees];
+ * leaf_value [leaf_rows_cap][n_classes] is only used when some leaf is not one-hot
+ * (DDM_E_IMPURE if it is NULL or too small).  out_info = {n_nodes, pure, n_leaf_rows}. */
+int ddm_rf_fit(const float* X, int32_t n, int32_t n_features, const int32_t* y_idx, int32_t n_classes,
+               const int64_t* seeds, int32_t n_trees, int32_t max_features, ddm_node* nodes,
+               int64_t nodes_cap, int32_t* roots, double* leaf_value, int64_t leaf_rows_cap,
+               int64_t* out_info);
 
 /* ---- synthetic inputs (benchmark configs) ------------------------- */
 

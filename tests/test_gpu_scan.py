@@ -164,7 +164,8 @@ def test_scan_lazy_reset_on_carried_change():
     st["miss_prob"] = 0.3
     st["sample_count"] = 50
     x = np.array([0, 0, 1, 0, 0, 0, 1, 1], np.uint8)
-    _, _, _, out, ps = gpu_scan(x, [0, len(x)], mode=1, state=st, trace=True)
+    # per_batch=1: a fresh DDM at the next batch == skmultiflow's lazy reset at the next element
+    _, _, _, out, ps = gpu_scan(x, [0, len(x)], per_batch=1, mode=1, state=st, trace=True)
     d = OracleDDM()
     d.in_concept_change = True
     for t, v in enumerate(x):
