@@ -11,6 +11,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <immintrin.h>
+
 #include <algorithm>
 
 #include "../../include/ddm_amd.h"
@@ -67,6 +69,52 @@ struct Gen {
     }
 };
 
+
+// Permutation stream, fast path: the current 624-word block is tempered once into a
+// buffer, and each Fisher-Yates interval finds its first accepted draw among the next 8
+// buffered words with one AVX2 compare + movemask (no unpredictable branch on the
+// ~25% rejections).  Draw-for-draw identical to Gen::interval.
+struct PermGen {
+    uint32_t* key;
+    int32_t pos;
+    alignas(32) uint32_t tb[kN];
+    int64_t draws = 0;
+
+    void temper_from(int from) {
+        for (int i = from; i < kN; ++i) {
+            uint32_t y = key[i];
+            y ^= y >> 11;
+            y ^= (y << 7) & 0x9d2c5680u;
+            y ^= (y << 15) & 0xefc60000u;
+            y ^= y >> 18;
+            tb[i] = y;
+        }
+    }
+    PermGen(uint32_t* k, int32_t p) : key(k), pos(p) {
+        if (pos < kN) temper_from(pos);
+    }
+    inline void refill() {
+        regen(key);
+        temper_from(0);
+        pos = 0;
+    }
+};
+
+#define PERM_FN perms_scalar
+#define PERM_AVX2 0
+#include "perm_loop.inc"
+#undef PERM_FN
+#undef PERM_AVX2
+
+#pragma GCC push_options
+#pragma GCC target("avx2")
+#define PERM_FN perms_avx2
+#define PERM_AVX2 1
+#include "perm_loop.inc"
+#undef PERM_FN
+#undef PERM_AVX2
+#pragma GCC pop_options
+
 }  // namespace
 
 extern "C" int ddm_mt_perms(uint32_t* key, int32_t* pos, const int32_t* batch_len, int64_t n_batches,
@@ -74,27 +122,9 @@ extern "C" int ddm_mt_perms(uint32_t* key, int32_t* pos, const int32_t* batch_le
     if (!key || !pos || (!batch_len && n_batches) || (!perm_out && n_batches) || n_batches < 0 || *pos < 0 ||
         *pos > kN)
         return DDM_E_ARG;
-    Gen g{key, *pos};
-    uint8_t* out = perm_out;
-    for (int64_t b = 0; b < n_batches; ++b) {
-        const int32_t n = batch_len[b];
-        if (n < 0 || n > 256) {
-            *pos = g.pos;
-            return DDM_E_ARG;
-        }
-        const int64_t d0 = g.draws;
-        for (int32_t i = 0; i < n; ++i) out[i] = (uint8_t)i;
-        for (int32_t i = n - 1; i >= 1; --i) {
-            const uint32_t j = g.interval((uint32_t)i);
-            const uint8_t t = out[i];
-            out[i] = out[j];
-            out[j] = t;
-        }
-        out += n;
-        if (draws_out) draws_out[b] = g.draws - d0;
-    }
-    *pos = g.pos;
-    return 0;
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    return avx2 ? perms_avx2(key, pos, batch_len, n_batches, perm_out, draws_out)
+                : perms_scalar(key, pos, batch_len, n_batches, perm_out, draws_out);
 }
 
 extern "C" int ddm_mt_randint31(uint32_t* key, int32_t* pos, int64_t count, int64_t* out) {
