@@ -8,7 +8,7 @@ sparse abrupt drifts; rialto.csv is not shipped) partitioned `row % INSTANCES`
 of 10,000,037 global rows (~100 drifts per partition, block edges not batch aligned).
 One step = every partition of this rank through the full reference hot path
 (run_DDM_loop, DDM_Process.py:170-213): batch shuffles from the partition's MT19937,
-forest predict + DDM scan on the GPU, refit on every drift (host sklearn, spawn pool).
+forest predict + DDM scan on the GPU, refit on every drift (native exact RF refit).
 Inputs are resident in HBM before the timed region.  Weak scaling: each rank owns its
 own 8 partitions (global ids rank*8 + p, INSTANCES = 8 * world), no collective on the
 data path; the per-rank event counts are all-reduced once for the self-check.
@@ -41,7 +41,6 @@ def parse():
     ap.add_argument("--features", type=int, default=27)
     ap.add_argument("--refit", default="native", choices=["native", "sklearn"],
                     help="native: ddm_rf_fit (identical trees to sklearn 1.7.2); sklearn: host sklearn")
-    ap.add_argument("--refit-workers", type=int, default=8, help="sklearn refit: spawn-pool size (0 = in-process)")
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-sample-rows", type=int, default=150_000)
@@ -96,13 +95,7 @@ def run_c3(args, world, rank, dev, torch, dist):
     from ddm_amd import kernels
     from ddm_amd.controller import DevicePartition, PartitionRunner
     from ddm_amd.params import DDMSettings
-    from ddm_amd.refit import RefitPool
     from ddm_amd.rng import MTStream
-
-    refit = args._pool
-    if args.refit == "sklearn" and refit is None:
-        from ddm_amd.controller import sklearn_refit
-        refit = sklearn_refit(DDMSettings())
     instances = args.parts * world
     block = args.block_rows if world == 1 else (args.block_rows // 8) * instances + 37
     n = args.rows_per_part
@@ -114,7 +107,7 @@ def run_c3(args, world, rank, dev, torch, dist):
         kernels.synth_block_labels(part.y[:n], gid, instances, block, 10)
         kernels.synth_features(part.X, part.y[:n], gid, instances, args.seed, 0.04)
         parts.append((gid, part))
-        runners.append(PartitionRunner(part, settings, torch.cuda.Stream(dev), refit=refit, timing=True))
+        runners.append(PartitionRunner(part, settings, torch.cuda.Stream(dev), refit=args.refit, timing=True))
     torch.cuda.synchronize()
 
     results = {}
@@ -154,7 +147,8 @@ def run_c3(args, world, rank, dev, torch, dist):
             raise RuntimeError(f"partition {g}: events differ between steps")
     st = [r.stats for r in runners]
     agg = {k: sum(getattr(s, k) for s in st) for k in ("epochs", "refits", "predicted_rows", "refit_s",
-                                                        "predict_ms", "predict_bytes", "scan_ms", "scan_rows")}
+                                                        "predict_ms", "predict_bytes", "scan_ms", "scan_rows",
+                                                        "shuffle_ms")}
     drifts = int(sum((r[:, 1] >= 0).sum() for r in results.values()))
     warns = int(sum((r[:, 0] >= 0).sum() for r in results.values()))
     rows_rank = n * args.parts * args.steps
@@ -172,14 +166,16 @@ def run_c3(args, world, rank, dev, torch, dist):
         "rows_per_gpu_step": n * args.parts, "partitions_per_gpu": args.parts,
         "refit": ("native ddm_rf_fit (sklearn 1.7.2 RandomForestClassifier restated, identical trees), "
                   "one host thread per partition") if args.refit == "native" else
-                 ("host sklearn RandomForestClassifier(100 trees), " + ("spawn pool" if refit else "in-process")),
+                 "host sklearn RandomForestClassifier(100 trees), in-process",
+        "shuffle": "batch shuffles generated on the GPU from the partition's MT19937 stream (ddm_shuffle_*)",
     }
     extra = {"drifts_per_step": drifts, "warnings_per_step": warns,
              "refits_per_step": agg["refits"] / args.steps, "epochs_per_step": agg["epochs"] / args.steps,
              "speculation_overhead": agg["predicted_rows"] / max(1, rows_rank),
              "refit_s_per_step_sum": agg["refit_s"] / args.steps,
              "predict_kernel_ms_per_step": agg["predict_ms"] / args.steps,
-             "scan_kernel_ms_per_step": agg["scan_ms"] / args.steps}
+             "scan_kernel_ms_per_step": agg["scan_ms"] / args.steps,
+             "shuffle_kernels_ms_per_step": agg["shuffle_ms"] / args.steps}
     roofline = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_from_profile("ddm_forest_predict", rows_per_launch),
                 "kernel": "ddm_forest_predict", "alg_bytes_per_row": "4*F_used + 6",
@@ -256,12 +252,6 @@ def run_c4(args, world, rank, dev, torch, dist):
 def main():
     args = parse()
     world, rank, local_rank = dist_env()
-    args._pool = None
-    if args.workload == "c3" and args.refit == "sklearn" and args.refit_workers > 0:
-        # spawn the host refit workers BEFORE anything initialises the GPU
-        # (--refit-workers 0: in-process refits, for runs under a profiler)
-        from ddm_amd.refit import RefitPool
-        args._pool = RefitPool(args.refit_workers)
     import torch
     import torch.distributed as dist
     dev = torch.device("cuda", local_rank)
@@ -288,8 +278,6 @@ def main():
                "config": dict(info, parallelism=f"partitions over {world} GPU(s), no data-path collective"),
                "roofline": roofline, "cpu_baseline": cpu, "breakdown": extra}
         print(json.dumps(out), flush=True)
-    if args._pool is not None:
-        args._pool.close()
     if world > 1:
         dist.destroy_process_group()
 

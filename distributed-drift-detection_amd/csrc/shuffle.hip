@@ -1,0 +1,384 @@
+// Batch shuffles on the GPU: pandas `sample(frac=1)` (DDM_Process.py:187, :190) ==
+// numpy legacy RandomState.permutation on the global MT19937, reproduced draw for draw.
+//
+// The reference consumes one sequential MT19937 stream per partition: for every batch a
+// Fisher-Yates pass whose intervals i = L-1..1 each take the first draw v with
+// (v & mask(i)) <= i (mask(i) = smallest 2^k-1 >= i; rejected draws are skipped).  On
+// the host that chain is latency bound (~10 ns/row).  Here it is made parallel:
+//   1. k_mt_generate   one workgroup per partition emits the raw tempered stream R;
+//                      a 624-word block is regenerated in LDS in three barrier phases.
+//   2. k_fsm_sub       interval acceptance is a finite-state machine whose state is the
+//                      interval index s in [1, L-1] (s == 1 accepted -> batch done,
+//                      s := L-1).  For every 128-draw sub-chunk and EVERY start state a
+//                      lane simulates the sub-chunk: table (end state, batches done).
+//   3. k_fsm_chunk     composes 64 sub-chunk tables into 8192-draw chunk tables.
+//   4. k_fsm_walk      one lane walks chunk tables from a window start (a batch
+//                      boundary at draw P) to find every chunk's start (state, batch).
+//   5. k_fsm_replay    one wave per chunk: lane 0 composes the sub-chunk tables, then
+//                      each lane replays its 128 draws and records, per batch, the j of
+//                      every interval and the draw that completes the batch.
+//   6. k_fsm_perms     one lane per batch applies its L-1 swaps -> perm bytes in HBM.
+// Steps 2-3 depend only on the RNG stream (not on drifts), so they run once per stream
+// segment; 4-6 run per speculative window.  Tempering is invertible, so the host
+// recovers the exact numpy (key, pos) state at any draw from R.
+#include "common.h"
+
+namespace {
+
+constexpr int kN = 624;
+constexpr int kSub = 128;            // draws per sub-chunk
+constexpr int kSubPerChunk = 64;     // sub-chunks per chunk
+constexpr int64_t kChunk = (int64_t)kSub * kSubPerChunk;
+
+__device__ __forceinline__ uint32_t temper(uint32_t y) {
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+__device__ __forceinline__ uint32_t mt_word(uint32_t a, uint32_t b, uint32_t c) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+__device__ __forceinline__ uint32_t imask(uint32_t i) { return 0xffffffffu >> __builtin_clz(i); }
+
+// state word: key[624] (untempered) followed by pos (number of words of key consumed)
+__global__ __launch_bounds__(256) void k_mt_generate(uint32_t* __restrict__ state, uint32_t* __restrict__ R,
+                                                     int64_t n) {
+    __shared__ uint32_t key[kN];
+    __shared__ int s_pos;
+    for (int k = threadIdx.x; k < kN; k += 256) key[k] = state[k];
+    if (threadIdx.x == 0) s_pos = (int)state[kN];
+    __syncthreads();
+    int pos = s_pos;
+    int64_t out = 0;
+    while (out < n) {
+        if (pos >= kN) {
+            // in-place regeneration in three dependency phases (same result as the
+            // sequential loop: word i uses new words only where the loop would)
+            uint32_t v = 0;
+            const int t = threadIdx.x;
+            if (t < 227) v = mt_word(key[t], key[t + 1], key[t + 397]);
+            __syncthreads();
+            if (t < 227) key[t] = v;
+            __syncthreads();
+            if (t < 227) v = mt_word(key[227 + t], key[228 + t], key[t]);
+            __syncthreads();
+            if (t < 227) key[227 + t] = v;
+            __syncthreads();
+            if (t < 169) v = mt_word(key[454 + t], key[455 + t], key[227 + t]);
+            else if (t == 169) v = mt_word(key[623], key[0], key[396]);
+            __syncthreads();
+            if (t < 169) key[454 + t] = v;
+            else if (t == 169) key[623] = v;
+            __syncthreads();
+            pos = 0;
+        }
+        const int take = (int)min((int64_t)(kN - pos), n - out);
+        for (int k = threadIdx.x; k < take; k += 256) R[out + k] = temper(key[pos + k]);
+        out += take;
+        pos += take;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < kN; k += 256) state[k] = key[k];
+    if (threadIdx.x == 0) state[kN] = (uint32_t)pos;
+}
+
+// Tsub[sub][s-1] = end_state | batches_done << 8, for s in [1, L-1].
+__global__ __launch_bounds__(256) void k_fsm_sub(const uint32_t* __restrict__ R, int64_t sub0, int64_t nsub,
+                                                 int L, uint16_t* __restrict__ Tsub) {
+    __shared__ uint32_t draws[kSub];
+    const int S = L - 1;
+    for (int64_t sb = sub0 + blockIdx.x; sb < sub0 + nsub; sb += gridDim.x) {
+        __syncthreads();
+        if (threadIdx.x < kSub) draws[threadIdx.x] = R[sb * kSub + threadIdx.x];
+        __syncthreads();
+        for (int s0 = threadIdx.x + 1; s0 <= S; s0 += 256) {
+            uint32_t s = (uint32_t)s0, done = 0;
+            for (int k = 0; k < kSub; ++k) {
+                const bool acc = (draws[k] & imask(s)) <= s;
+                if (acc) {
+                    if (s == 1) {
+                        s = (uint32_t)S;
+                        ++done;
+                    } else {
+                        --s;
+                    }
+                }
+            }
+            Tsub[sb * S + (s0 - 1)] = (uint16_t)(s | (done << 8));
+        }
+    }
+}
+
+// Tchunk[c][s-1] = end_state | batches_done << 8 over 64 sub-chunks.
+__global__ __launch_bounds__(256) void k_fsm_chunk(const uint16_t* __restrict__ Tsub, int64_t chunk0, int64_t nchunk,
+                                                   int L, uint32_t* __restrict__ Tchunk) {
+    const int S = L - 1;
+    for (int64_t c = chunk0 + blockIdx.x; c < chunk0 + nchunk; c += gridDim.x) {
+        for (int s0 = threadIdx.x + 1; s0 <= S; s0 += 256) {
+            uint32_t s = (uint32_t)s0, done = 0;
+            const uint16_t* t = Tsub + c * kSubPerChunk * S;
+            for (int k = 0; k < kSubPerChunk; ++k) {
+                const uint32_t e = t[(int64_t)k * S + (s - 1)];
+                s = e & 0xffu;
+                done += e >> 8;
+            }
+            Tchunk[c * S + (s0 - 1)] = s | (done << 8);
+        }
+    }
+}
+
+struct ChunkStart {
+    int64_t pos;      // first draw of this window piece
+    int32_t state;    // interval index at pos
+    int32_t batch;    // batches completed (relative to the window) before pos
+};
+
+// From draw P at a batch boundary, walk to the first chunk boundary (draw by draw, then
+// by sub-chunk tables) and then chunk by chunk until W batches are done.  The chunk
+// table rows are staged in LDS 64 chunks at a time (all lanes load, lane 0 walks), so
+// the serial walk does LDS lookups, not dependent HBM loads.
+// out[0] = the piece [P, first chunk boundary); out[k] = chunk starts.
+// info = {pieces, end draw, batches reached}.
+__global__ __launch_bounds__(64) void k_fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restrict__ Tsub,
+                                                 const uint32_t* __restrict__ Tchunk, int64_t P, int64_t W, int L,
+                                                 int64_t avail, ChunkStart* __restrict__ out,
+                                                 int64_t* __restrict__ info) {
+    extern __shared__ uint32_t tab[];   // [64][S]
+    __shared__ int64_t sh_pos, sh_batch, sh_k;
+    __shared__ uint32_t sh_s;
+    const int S = L - 1;
+    if (threadIdx.x == 0) {
+        int64_t pos = P, batch = 0, k = 0;
+        uint32_t s = (uint32_t)S;
+        out[k++] = ChunkStart{pos, (int32_t)s, 0};
+        while (batch < W && pos % kSub != 0 && pos < avail) {
+            const uint32_t v = R[pos++];
+            if ((v & imask(s)) <= s) {
+                if (s == 1) {
+                    s = (uint32_t)S;
+                    ++batch;
+                } else {
+                    --s;
+                }
+            }
+        }
+        while (batch < W && pos % kChunk != 0 && pos + kSub <= avail) {
+            const uint32_t e = Tsub[(pos / kSub) * S + (s - 1)];
+            s = e & 0xffu;
+            batch += e >> 8;
+            pos += kSub;
+        }
+        sh_pos = pos;
+        sh_batch = batch;
+        sh_k = k;
+        sh_s = s;
+    }
+    __syncthreads();
+    for (;;) {
+        const int64_t pos0 = sh_pos;
+        if (sh_batch >= W || pos0 + kChunk > avail) break;
+        const int64_t c0 = pos0 / kChunk;
+        const int nload = (int)min((int64_t)64, (avail - pos0) / kChunk);
+        for (int64_t e = threadIdx.x; e < (int64_t)nload * S; e += 64) tab[e] = Tchunk[c0 * S + e];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t pos = pos0, batch = sh_batch, k = sh_k;
+            uint32_t s = sh_s;
+            for (int c = 0; c < nload && batch < W; ++c) {
+                out[k++] = ChunkStart{pos, (int32_t)s, (int32_t)batch};
+                const uint32_t e = tab[c * S + (s - 1)];
+                s = e & 0xffu;
+                batch += e >> 8;
+                pos += kChunk;
+            }
+            sh_pos = pos;
+            sh_batch = batch;
+            sh_k = k;
+            sh_s = s;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        info[0] = sh_k;
+        info[1] = sh_pos;
+        info[2] = sh_batch;
+    }
+}
+
+// One wave per window piece.  The piece's sub-chunk table rows are staged in LDS, lane 0
+// derives every sub-chunk's start (state, batch); then the lanes replay sub-chunks: for
+// each accepted draw of batch b < W record J[b*L + s] = v & mask(s) and, when s == 1,
+// E[b] = draw index.
+__global__ __launch_bounds__(64) void k_fsm_replay(const uint32_t* __restrict__ R, const uint16_t* __restrict__ Tsub,
+                                                   const ChunkStart* __restrict__ pieces,
+                                                   const int64_t* __restrict__ info, int64_t W, int L,
+                                                   uint8_t* __restrict__ J, int64_t* __restrict__ E) {
+    extern __shared__ uint16_t subtab[];   // [64][S]
+    __shared__ int64_t sub_pos[kSubPerChunk + 2];
+    __shared__ int32_t sub_state[kSubPerChunk + 2], sub_batch[kSubPerChunk + 2];
+    __shared__ int n_subs;
+    const int64_t npieces = info[0], end = info[1];
+    const int S = L - 1;
+    for (int64_t pc = blockIdx.x; pc < npieces; pc += gridDim.x) {
+        const ChunkStart c = pieces[pc];
+        const int64_t stop = (pc + 1 < npieces) ? pieces[pc + 1].pos : end;
+        // stage the table rows of the whole sub-chunks of this piece's chunk
+        const int64_t chunk = c.pos / kChunk;
+        const int64_t first_sub = chunk * kSubPerChunk;
+        for (int64_t e = threadIdx.x; e < (int64_t)kSubPerChunk * S; e += 64) {
+            const int64_t sb = first_sub + e / S;
+            if ((sb + 1) * kSub <= stop) subtab[e] = Tsub[first_sub * S + e];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t pos = c.pos;
+            uint32_t s = (uint32_t)c.state;
+            int32_t b = c.batch;
+            int n = 0;
+            while (pos < stop) {
+                sub_pos[n] = pos;
+                sub_state[n] = (int32_t)s;
+                sub_batch[n] = b;
+                ++n;
+                const int64_t nxt = min(stop, (pos / kSub + 1) * kSub);
+                if (pos % kSub == 0 && nxt - pos == kSub) {
+                    const uint32_t e = subtab[(pos / kSub - first_sub) * S + (s - 1)];
+                    s = e & 0xffu;
+                    b += (int32_t)(e >> 8);
+                } else {
+                    for (int64_t q = pos; q < nxt; ++q) {
+                        const uint32_t v = R[q];
+                        if ((v & imask(s)) <= s) {
+                            if (s == 1) {
+                                s = (uint32_t)S;
+                                ++b;
+                            } else {
+                                --s;
+                            }
+                        }
+                    }
+                }
+                pos = nxt;
+            }
+            sub_pos[n] = stop;
+            n_subs = n;
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < n_subs; t += 64) {
+            uint32_t s = (uint32_t)sub_state[t];
+            int64_t b = sub_batch[t];
+            for (int64_t q = sub_pos[t]; q < sub_pos[t + 1] && b < W; ++q) {
+                const uint32_t v = R[q];
+                const uint32_t m = v & imask(s);
+                if (m <= s) {
+                    J[b * L + s] = (uint8_t)m;
+                    if (s == 1) {
+                        E[b] = q;
+                        s = (uint32_t)S;
+                        ++b;
+                    } else {
+                        --s;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// One lane per batch: Fisher-Yates swaps i = L-1..1 with the recorded j's.
+__global__ __launch_bounds__(256) void k_fsm_perms(const uint8_t* __restrict__ J, int64_t W, int L,
+                                                   uint8_t* __restrict__ perm) {
+    extern __shared__ uint8_t buf[];
+    const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b >= W) return;
+    uint8_t* p = buf + threadIdx.x * L;
+    for (int k = 0; k < L; ++k) p[k] = (uint8_t)k;
+    const uint8_t* j = J + b * L;
+    for (int i = L - 1; i >= 1; --i) {
+        const int jj = j[i];
+        const uint8_t t = p[i];
+        p[i] = p[jj];
+        p[jj] = t;
+    }
+    for (int k = 0; k < L; ++k) perm[b * L + k] = p[k];
+}
+
+__global__ void k_pick(const int32_t* stop, const int64_t* E, int64_t W, int64_t offset, int64_t last, int64_t* out) {
+    const int64_t k = (stop[0] >= 0 ? (int64_t)stop[0] : last) - offset;
+    out[0] = (k >= 0 && k < W) ? E[k] : -1;
+}
+
+}  // namespace
+
+extern "C" int ddm_shuffle_pick(const int32_t* stop, const int64_t* E, int64_t W, int64_t offset, int64_t last,
+                                int64_t* out, ddm_stream_t stream) {
+    if (!stop || !E || !out) {
+        ddm::set_error("ddm_shuffle_pick: invalid argument");
+        return DDM_E_ARG;
+    }
+    hipLaunchKernelGGL(k_pick, dim3(1), dim3(1), 0, ddm::as_hip(stream), stop, E, W, offset, last, out);
+    return ddm::launch_status("ddm_shuffle_pick");
+}
+
+extern "C" int ddm_shuffle_generate(uint32_t* mt_state, uint32_t* R, int64_t n, ddm_stream_t stream) {
+    if (!mt_state || !R || n < 0) {
+        ddm::set_error("ddm_shuffle_generate: invalid argument");
+        return DDM_E_ARG;
+    }
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_mt_generate, dim3(1), dim3(256), 0, ddm::as_hip(stream), mt_state, R, n);
+    return ddm::launch_status("ddm_shuffle_generate");
+}
+
+extern "C" int ddm_shuffle_tables(const uint32_t* R, int64_t chunk0, int64_t nchunk, int32_t batch_len,
+                                  uint16_t* Tsub, uint32_t* Tchunk, ddm_stream_t stream) {
+    if (!R || !Tsub || !Tchunk || chunk0 < 0 || nchunk < 0 || batch_len < 2 || batch_len > 256) {
+        ddm::set_error("ddm_shuffle_tables: invalid argument");
+        return DDM_E_ARG;
+    }
+    if (nchunk == 0) return 0;
+    hipStream_t s = ddm::as_hip(stream);
+    const int64_t nsub = nchunk * kSubPerChunk;
+    hipLaunchKernelGGL(k_fsm_sub, dim3((unsigned)std::min<int64_t>(nsub, 65536)), dim3(256), 0, s, R,
+                       chunk0 * kSubPerChunk, nsub, (int)batch_len, Tsub);
+    if (int rc = ddm::launch_status("ddm_shuffle_tables/sub")) return rc;
+    hipLaunchKernelGGL(k_fsm_chunk, dim3((unsigned)std::min<int64_t>(nchunk, 65536)), dim3(256), 0, s, Tsub, chunk0,
+                       nchunk, (int)batch_len, Tchunk);
+    return ddm::launch_status("ddm_shuffle_tables/chunk");
+}
+
+extern "C" int ddm_shuffle_window(const uint32_t* R, const uint16_t* Tsub, const uint32_t* Tchunk, int64_t avail,
+                                  int64_t P, int64_t W, int32_t batch_len, void* pieces, int64_t max_pieces,
+                                  int64_t* info, uint8_t* J, int64_t* E, uint8_t* perm_out, ddm_stream_t stream,
+                                  ddm_event_t ev_begin, ddm_event_t ev_end) {
+    if (!R || !Tsub || !Tchunk || !pieces || !info || !J || !E || !perm_out || P < 0 || W <= 0 ||
+        batch_len < 2 || batch_len > 256 || max_pieces < 2 + (W * batch_len * 3) / kChunk) {
+        ddm::set_error("ddm_shuffle_window: invalid argument");
+        return DDM_E_ARG;
+    }
+    hipStream_t s = ddm::as_hip(stream);
+    ChunkStart* pc = reinterpret_cast<ChunkStart*>(pieces);
+    if (ev_begin)
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
+    const size_t walk_lds = (size_t)64 * (batch_len - 1) * sizeof(uint32_t);
+    hipLaunchKernelGGL(k_fsm_walk, dim3(1), dim3(64), walk_lds, s, R, Tsub, Tchunk, P, W, (int)batch_len, avail, pc,
+                       info);
+    if (int rc = ddm::launch_status("ddm_shuffle_window/walk")) return rc;
+    const int64_t blocks = std::min<int64_t>(max_pieces, 8192);
+    const size_t rep_lds = (size_t)kSubPerChunk * (batch_len - 1) * sizeof(uint16_t);
+    hipLaunchKernelGGL(k_fsm_replay, dim3((unsigned)blocks), dim3(64), rep_lds, s, R, Tsub, pc, info, W, (int)batch_len,
+                       J, E);
+    if (int rc = ddm::launch_status("ddm_shuffle_window/replay")) return rc;
+    hipLaunchKernelGGL(k_fsm_perms, dim3((unsigned)ddm::ceil_div(W, 256)), dim3(256), (size_t)256 * batch_len, s, J, W,
+                       (int)batch_len, perm_out);
+    if (int rc = ddm::launch_status("ddm_shuffle_window/perms")) return rc;
+    if (ev_end)
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
+    return 0;
+}

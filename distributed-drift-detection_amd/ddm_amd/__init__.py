@@ -5,8 +5,7 @@ Drop-in for the reference's grouped-map partition function `run_DDM_loop`
 (forest predict, DDM scan) behind a C-ABI (include/ddm_amd.h) bound with ctypes;
 PyTorch-ROCm provides device buffers, streams and torch.distributed (RCCL).
 
-The package namespace is lazy: `ddm_amd.treepack` / `ddm_amd.refit` stay importable in
-host-only worker processes without torch; everything else loads libddm_amd.so through
+The package namespace is lazy: `ddm_amd.treepack` stays importable without torch; everything else loads libddm_amd.so through
 `ddm_amd._capi`, which raises if the library is not built (there is no CPU fallback).
 """
 import importlib

@@ -8,15 +8,18 @@ Reference semantics (per partition, one global numpy MT19937):
   is dropped, refit flagged (:207-210); `pd.concat` of the per-batch rows (:212).
 
 MI355X execution: the partition lives in HBM (columnar float32 features, int32
-labels).  Between two refits nothing the host does depends on the rows, so the
-controller speculates: it draws the next W batch shuffles (native MT19937), runs the
-forest-predict kernel over all W batches in DDM order (writing the error bytes and the
-first error position) and the DDM-scan kernel over them (stopping at the first
-change), and reads back one small control block.  No drift: the DDM state carries, W
-doubles.  Drift in batch d: events up to d are final, the RNG is re-positioned right
-after batch d's shuffle (where the reference's next iteration continues), the host
-refits on batch d and the next window starts at d+1.  Work past d is discarded, so
-total predict work stays within ~2x the rows.
+labels) together with its MT19937 stream (shuffle.py: raw draws + interval-FSM tables).
+Between two refits nothing the host does depends on the rows, so the controller
+speculates: for the next W batches it generates the batch shuffles on the device
+(ddm_shuffle_window), runs the forest-predict kernel over all W batches in DDM order
+(writing the error bytes and the first error position) and the DDM-scan kernel over
+them (stopping at the first change, reporting event rows through the shuffle), and
+reads back one 128-byte control block.  No drift: the DDM state carries, W doubles.
+Drift in batch d: events up to d are final, the RNG position becomes the draw after
+batch d's shuffle (where the reference's next iteration continues), the next batch's
+shuffle and the refit's 100 tree seeds are read from the stream on the host, the
+forest is refit natively on batch d, and the next window starts at d+1.  Work past d
+is discarded, so total predict work stays within ~2x the rows.
 """
 import time
 
@@ -25,13 +28,14 @@ import pandas as pd
 import torch
 
 from . import kernels
-from .forest import DeviceForest, pack_sklearn
+from .forest import DeviceForest
 from .params import OUTPUT_COLUMNS, DDMSettings, infer_x_features
 from .rng import MTStream
-from .trainer import native_refit
+from .shuffle import GpuShuffle, expected_draws_per_batch
+from .trainer import NativeForestTrainer
 
 # control block layout (bytes) shared by host (pinned) and device
-_FIRST_ERR, _NEV, _STOP, _OFF, _BASE, _STATE, _CTRL_BYTES = 0, 8, 16, 24, 40, 64, 128
+_FIRST_ERR, _NEV, _STOP, _OFF, _BASE, _PICK, _STATE, _CTRL_BYTES = 0, 8, 16, 24, 40, 48, 64, 128
 
 
 def _round_up(n, m):
@@ -82,15 +86,17 @@ class DevicePartition:
 
 
 def sklearn_refit(settings):
-    """train_rf (DDM_Process.py:98-105) on the host, drawing its 100 tree seeds from the
-    partition's MT19937 stream (== the reference's global RandomState)."""
+    """train_rf (DDM_Process.py:98-105) with sklearn itself: fit(X32, y, np_state) where
+    np_state is numpy's global-RNG state at the refit (its 100 tree seeds come from it)."""
     from sklearn.ensemble import RandomForestClassifier
 
-    def refit(X32, y, rng):
-        rs = rng.to_random_state()
+    from .treepack import pack_sklearn
+
+    def refit(X32, y, np_state):
+        rs = np.random.RandomState()
+        rs.set_state(np_state)
         rf = RandomForestClassifier(n_estimators=settings.n_estimators, n_jobs=settings.cores, random_state=rs)
         rf.fit(X32, y)
-        rng.load_random_state(rs)
         return pack_sklearn(rf)
 
     return refit
@@ -98,148 +104,229 @@ def sklearn_refit(settings):
 
 class RunStats:
     __slots__ = ("epochs", "refits", "predicted_rows", "refit_s", "gpu_s", "host_s", "predict_ms", "predict_bytes",
-                 "scan_ms", "scan_rows")
+                 "scan_ms", "scan_rows", "shuffle_ms", "sklearn_refits")
 
     def __init__(self):
         self.epochs = self.refits = self.predicted_rows = self.predict_bytes = self.scan_rows = 0
-        self.refit_s = self.gpu_s = self.host_s = self.predict_ms = self.scan_ms = 0.0
+        self.sklearn_refits = 0
+        self.refit_s = self.gpu_s = self.host_s = self.predict_ms = self.scan_ms = self.shuffle_ms = 0.0
 
     def as_dict(self):
         return {k: getattr(self, k) for k in self.__slots__}
 
 
 class PartitionRunner:
-    """Runs the speculative predict+scan epochs of one partition on one HIP stream."""
+    """Runs the speculative shuffle+predict+scan epochs of one partition on one HIP stream.
 
-    def __init__(self, part, settings=None, stream=None, refit=None, timing=False):
+    refit: "native" (ddm_rf_fit, identical trees to sklearn 1.7.2; sklearn itself for NaN
+    inputs) or "sklearn"."""
+
+    def __init__(self, part, settings=None, stream=None, refit="native", timing=False):
         self.part = part
+        self.s = settings or DDMSettings()
+        self.stream = stream or torch.cuda.Stream(part.device)
+        self.refit_kind = refit
+        self.trainer = NativeForestTrainer(self.s.n_estimators)
+        self.sk_refit = sklearn_refit(self.s)
         self.timing = timing
         # HIP events recorded by the C-ABI right around each launch on this runner's stream
         self.t_pred = kernels.LaunchTimer() if timing else None
         self.t_scan = kernels.LaunchTimer() if timing else None
-        self.s = settings or DDMSettings()
-        self.stream = stream or torch.cuda.Stream(part.device)
-        self.refit = refit or native_refit(self.s)
+        self.t_shuf = kernels.LaunchTimer() if timing else None
         self.params = kernels.params_struct(self.s.min_num_instances, self.s.per_batch, self.s.warning_level,
                                             self.s.out_control_level)
-        n, dev = part.n, part.device
-        self.perm_h = torch.empty(max(n, 1), dtype=torch.uint8, pin_memory=True)
-        self.perm_np = self.perm_h.numpy()
-        self.perm_d = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        n, dev, pb = part.n, part.device, self.s.per_batch
+        if not 2 <= pb <= 256:
+            raise ValueError("per_batch must be in [2, 256] on the device path")
+        self.perm_d = torch.zeros(max(n, 1) + 256, dtype=torch.uint8, device=dev)
         self.err_d = torch.zeros(_round_up(max(n, 1), 16) + 16, dtype=torch.uint8, device=dev)
         self.ctrl_h = torch.zeros(_CTRL_BYTES, dtype=torch.uint8, pin_memory=True)
         self.ctrl_np = self.ctrl_h.numpy()
         self.ctrl_d = torch.zeros(_CTRL_BYTES, dtype=torch.uint8, device=dev)
-        nb = (n + self.s.per_batch - 1) // self.s.per_batch
+        # pinned staging: [0] batch-j shuffle of a refit epoch, [1] short last batch, [2] D2H
+        self.small_h = [torch.empty(256, dtype=torch.uint8, pin_memory=True) for _ in range(3)]
+        self.neg1_d = torch.full((1,), -1, dtype=torch.int32, device=dev)
+        nb = (n + pb - 1) // pb
         self.max_win = max(1, min(self.s.max_window_batches, nb))
         self.ev_d = torch.empty((self.max_win, 2), dtype=torch.int32, device=dev)
         self.ev_h = torch.empty((self.max_win, 2), dtype=torch.int32, pin_memory=True)
+        cap = int(nb * expected_draws_per_batch(pb) * 1.2) + 64 * 1024
+        self.shuffle = GpuShuffle(dev, pb, cap, self.max_win, self.stream)
         self.stats = RunStats()
 
     # -- host views of the control block
     def _ctrl(self, off, dtype, count=1):
         return self.ctrl_np[off:off + np.dtype(dtype).itemsize * count].view(dtype)
 
+    def _fit(self, rows, P_seeds):
+        """Refit on the rows of the drift batch (shuffled order); returns (forest, draws used)."""
+        X32, y = self.part.rows(rows, self.stream)
+        sh = self.shuffle
+        t0 = time.perf_counter()
+        seeds, P_after = sh.host_seeds(P_seeds, self.s.n_estimators)
+        packed = None
+        if self.refit_kind == "native":
+            packed = self.trainer.fit(X32, y, seeds)
+        if packed is None:                    # sklearn requested, or NaN in X (missing values)
+            packed = self.sk_refit(X32, y, sh.numpy_state(P_seeds))
+            self.stats.sklearn_refits += 1
+        self.stats.refit_s += time.perf_counter() - t0
+        self.stats.refits += 1
+        return DeviceForest(packed, self.part.device), P_after
+
+    def _upload_perm(self, b, perm, slot):
+        pb = self.s.per_batch
+        h = self.small_h[slot]
+        h[:len(perm)].copy_(torch.from_numpy(perm))
+        with torch.cuda.stream(self.stream):
+            self.perm_d[b * pb:b * pb + len(perm)].copy_(h[:len(perm)], non_blocking=True)
+
+    def _perm_rows(self, b, length):
+        """Rows of batch b in its shuffled order (D2H of the batch's perm bytes)."""
+        pb = self.s.per_batch
+        h = self.small_h[2]
+        with torch.cuda.stream(self.stream):
+            h[:length].copy_(self.perm_d[b * pb:b * pb + length], non_blocking=True)
+        self.stream.synchronize()
+        return b * pb + h[:length].numpy().astype(np.int64)
+
     def run(self, rng):
         """Returns int64 [n_batches-1, 2]: partition rows of (first warning, change) per
-        batch 1.. (-1 = none).  Consumes `rng` exactly as the reference consumes np.random."""
+        batch 1.. (-1 = none).  Consumes `rng` (advanced in place) exactly as the reference
+        consumes np.random."""
         s, part, st = self.s, self.part, self.stats
         n, pb = part.n, s.per_batch
         nb = (n + pb - 1) // pb
         if nb == 0:
             raise IndexError("list index out of range")       # batches[0] on an empty frame (:187)
-        blen = np.full(nb, pb, dtype=np.int32)
-        blen[-1] = n - (nb - 1) * pb
-        perm = self.perm_np
+        last_len = n - (nb - 1) * pb
+        n_full = nb if last_len == pb else nb - 1              # batches with exactly pb rows
 
-        def draw(b0, b1):
-            if b1 > b0:
-                rng.perms(blen[b0:b1], out=perm[b0 * pb:b0 * pb + int(blen[b0:b1].sum())])
+        def blen(b):
+            return pb if b < nb - 1 else last_len
 
-        draw(0, 1)                                             # batch_a = batches[0].sample (:187)
-        if nb < 2:
-            raise ValueError("No objects to concatenate")      # pd.concat([]) (:212)
-        train_rows = perm[:blen[0]].astype(np.int64)
-        out = np.full((nb - 1, 2), -1, dtype=np.int64)
-        state = kernels.fresh_states(1)
-        forest = None
-        retrain = True
-        j = 1
-        win = max(1, s.window_batches)
+        sh = self.shuffle
+        sh.reset(rng)
         stream = self.stream
         base = self.ctrl_d.data_ptr()
-        while j < nb:
-            t0 = time.perf_counter()
-            if retrain:
-                draw(j, j + 1)                                 # batch_b.sample before the fit (:190)
-                X32, y = part.rows(train_rows, stream)
-                t1 = time.perf_counter()
-                forest = DeviceForest(self.refit(X32, y, rng), part.device)
-                st.refit_s += time.perf_counter() - t1
-                st.refits += 1
-                retrain = False
-                state = kernels.fresh_states(1)                # ddm = None -> new DDM (:136-139)
-                gen_from = j + 1
-            else:
-                gen_from = j
-            b_end = min(nb, j + min(win, self.max_win))
-            snap = rng.snapshot()
-            draw(gen_from, b_end)
-            p0, p1 = j * pb, (b_end - 1) * pb + int(blen[b_end - 1])
-            self._ctrl(_OFF, np.int64, 2)[:] = (p0, p1)
-            self._ctrl(_BASE, np.int64)[0] = 0
-            self.ctrl_np[_STATE:_STATE + 56] = state.view(np.uint8)
-            st.host_s += time.perf_counter() - t0
-            t0 = time.perf_counter()
-            with torch.cuda.stream(stream):
-                self.ctrl_d.copy_(self.ctrl_h, non_blocking=True)
-                self.perm_d[p0:p1].copy_(self.perm_h[p0:p1], non_blocking=True)
-                kernels.forest_predict(part.X, part.y, self.perm_d, p0, p1, pb, forest, self.err_d,
-                                       first_err=self.ctrl_d[_FIRST_ERR:_FIRST_ERR + 8].view(torch.int64),
-                                       stream=stream, timer=self.t_pred)
-                kernels.scan_streams_raw(self.err_d.data_ptr(), base + _OFF, 1, self.params, base + _STATE,
-                                         base + _BASE, b_end - j, self.ev_d.data_ptr(), base + _FIRST_ERR,
-                                         base + _STOP, base + _NEV, 0, None, stream, self.t_scan)
-                self.ctrl_h.copy_(self.ctrl_d, non_blocking=True)
-            stream.synchronize()
-            stop = int(self._ctrl(_STOP, np.int32)[0])
-            nev = int(self._ctrl(_NEV, np.int64)[0])
-            last = j + stop if stop >= 0 else b_end - 1
-            if self.timing:
-                st.predict_ms += self.t_pred.elapsed_ms()
-                st.scan_ms += self.t_scan.elapsed_ms()
-                st.predict_bytes += (p1 - p0) * (4 * forest.packed.features_used + 6)
-                st.scan_rows += min(p1, (last + 1) * pb) - p0
-            if nev:
-                k = last - j + 1
+        try:
+            perm0, P = sh.host_perm(0, blen(0))                # batch_a = batches[0].sample (:187)
+            if nb < 2:
+                raise ValueError("No objects to concatenate")  # pd.concat([]) (:212)
+            train_rows = perm0.astype(np.int64)
+            out = np.full((nb - 1, 2), -1, dtype=np.int64)
+            state = kernels.fresh_states(1)
+            forest, retrain, j = None, True, 1
+            win = max(1, s.window_batches)
+            while j < nb:
+                t0 = time.perf_counter()
+                P_after_first = None
+                if retrain:
+                    permj, P = sh.host_perm(P, blen(j))        # batch_b.sample before the fit (:190, :194)
+                    self._upload_perm(j, permj, 0)
+                    forest, P = self._fit(train_rows, P)       # 100 tree seeds follow the shuffle
+                    P_after_first = P
+                    retrain = False
+                    state = kernels.fresh_states(1)            # ddm = None -> new DDM (:136-139)
+                    g0 = j + 1
+                else:
+                    g0 = j
+                b_end = min(nb, j + min(win, self.max_win))
+                gpu_end = min(b_end, n_full)
+                Wg = max(0, gpu_end - g0)
+                tail = b_end == nb and last_len != pb and nb - 1 >= g0
+                P_tail_after = None
+                if Wg:
+                    sh.window(P, Wg, self.perm_d[g0 * pb:], timer=self.t_shuf)
+                if tail:
+                    if Wg:
+                        sh.pick(self.neg1_d.data_ptr(), Wg, 0, Wg - 1, base + _PICK)   # end of the GPU batches
+                        P_tail = int(self._read_pick_now()) + 1
+                    else:
+                        P_tail = P
+                    permT, P_tail_after = sh.host_perm(P_tail, last_len)
+                    self._upload_perm(nb - 1, permT, 1)
+                p0, p1 = j * pb, (b_end - 1) * pb + blen(b_end - 1)
+                self._ctrl(_OFF, np.int64, 2)[:] = (p0, p1)
+                self._ctrl(_BASE, np.int64)[0] = 0
+                self.ctrl_np[_STATE:_STATE + 56] = state.view(np.uint8)
+                st.host_s += time.perf_counter() - t0
+                t0 = time.perf_counter()
                 with torch.cuda.stream(stream):
-                    self.ev_h[:k].copy_(self.ev_d[:k], non_blocking=True)
+                    self.ctrl_d[_OFF:_CTRL_BYTES].copy_(self.ctrl_h[_OFF:_CTRL_BYTES], non_blocking=True)
+                    kernels.forest_predict(part.X, part.y, self.perm_d, p0, p1, pb, forest, self.err_d,
+                                           first_err=self.ctrl_d[_FIRST_ERR:_FIRST_ERR + 8].view(torch.int64),
+                                           stream=stream, timer=self.t_pred)
+                    kernels.scan_streams_raw(self.err_d.data_ptr(), base + _OFF, 1, self.params, base + _STATE,
+                                             base + _BASE, b_end - j, self.ev_d.data_ptr(), base + _FIRST_ERR,
+                                             base + _STOP, base + _NEV, 0, None, stream, self.t_scan,
+                                             self.perm_d.data_ptr())
+                    if Wg:
+                        sh.pick(base + _STOP, Wg, g0 - j, b_end - 1 - j, base + _PICK)
+                    self.ctrl_h.copy_(self.ctrl_d, non_blocking=True)
                 stream.synchronize()
-                ev = self.ev_h[:k].numpy()
-                for c in range(2):
-                    q = ev[:, c]
-                    hit = np.nonzero(q >= 0)[0]
-                    b = j + hit
-                    out[b - 1, c] = b * pb + perm[b * pb + q[hit]].astype(np.int64)
-            st.gpu_s += time.perf_counter() - t0
-            st.epochs += 1
-            st.predicted_rows += p1 - p0
-            if stop >= 0:
-                d = j + stop
-                train_rows = d * pb + perm[d * pb:d * pb + blen[d]].astype(np.int64)
-                retrain = True
-                rng.restore(snap)                              # RNG right after batch d's shuffle
-                draw(gen_from, d + 1)
-                j = d + 1
-                win = max(1, s.window_batches)
-            else:
-                state = self._ctrl(_STATE, np.uint8, 56).copy().view(kernels.STATE_DTYPE)
-                j = b_end
-                win *= 2
-        return out
+                stop = int(self._ctrl(_STOP, np.int32)[0])
+                nev = int(self._ctrl(_NEV, np.int64)[0])
+                picked = int(self._ctrl(_PICK, np.int64)[0]) if Wg else -1
+                last = j + stop if stop >= 0 else b_end - 1
+                if self.timing:
+                    st.predict_ms += self.t_pred.elapsed_ms()
+                    st.scan_ms += self.t_scan.elapsed_ms()
+                    if Wg:
+                        st.shuffle_ms += self.t_shuf.elapsed_ms()
+                    st.predict_bytes += (p1 - p0) * (4 * forest.packed.features_used + 6)
+                    st.scan_rows += min(p1, (last + 1) * pb) - p0
+                if nev:
+                    k = last - j + 1
+                    with torch.cuda.stream(stream):
+                        self.ev_h[:k].copy_(self.ev_d[:k], non_blocking=True)
+                    stream.synchronize()
+                    ev = self.ev_h[:k].numpy()
+                    for c in range(2):
+                        hit = np.nonzero(ev[:, c] >= 0)[0]
+                        b = j + hit
+                        out[b - 1, c] = b * pb + ev[hit, c].astype(np.int64)
+                st.gpu_s += time.perf_counter() - t0
+                st.epochs += 1
+                st.predicted_rows += p1 - p0
+                # RNG position right after the last consumed batch shuffle
+                if stop >= 0:
+                    d = j + stop
+                    if d < g0:
+                        P = P_after_first                      # drift in the refit batch: after its seeds
+                    elif tail and d == nb - 1:
+                        P = P_tail_after
+                    else:
+                        P = picked + 1
+                    train_rows = self._perm_rows(d, blen(d))
+                    retrain = True
+                    j = d + 1
+                    win = max(1, s.window_batches)
+                else:
+                    if tail:
+                        P = P_tail_after
+                    elif Wg:
+                        P = picked + 1
+                    elif P_after_first is not None:
+                        P = P_after_first
+                    state = self._ctrl(_STATE, np.uint8, 56).copy().view(kernels.STATE_DTYPE)
+                    j = b_end
+                    win *= 2
+            return out
+        finally:
+            if "P" in locals():
+                ns = sh.numpy_state(P)
+                rng.key[:] = ns[1]
+                rng.pos.value = ns[2]
+
+    def _read_pick_now(self):
+        with torch.cuda.stream(self.stream):
+            self.ctrl_h[_PICK:_PICK + 8].copy_(self.ctrl_d[_PICK:_PICK + 8], non_blocking=True)
+        self.stream.synchronize()
+        return self._ctrl(_PICK, np.int64)[0]
 
 
-def run_partition_frame(pdf, rng, settings=None, device=None, stream=None, refit=None, stats=None):
+def run_partition_frame(pdf, rng, settings=None, device=None, stream=None, refit="native", stats=None):
     """One partition frame through the GPU path with an explicit MT19937 stream `rng`
     (the RNG a Spark Python worker would hold).  Returns the reference's output frame:
     one row per batch after the first, columns warning_flag_local/global and
@@ -269,7 +356,7 @@ def events_frame(rows, local_labels, global_labels):
     return pd.DataFrame(res, columns=OUTPUT_COLUMNS, index=np.zeros(len(res), dtype=np.int64))
 
 
-def run_DDM_loop(pdf, settings=None, device=None, stream=None, refit=None, stats=None):
+def run_DDM_loop(pdf, settings=None, device=None, stream=None, refit="native", stats=None):
     """Drop-in for the grouped-map UDF `run_DDM_loop` (DDM_Process.py:166-213): same input
     frame, same output frame, and it draws from / advances numpy's global RandomState
     exactly as the reference does (so `np.random.seed(k)` before the call reproduces the

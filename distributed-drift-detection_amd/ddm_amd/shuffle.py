@@ -1,0 +1,199 @@
+"""GPU batch shuffles: one partition's numpy MT19937 stream on the device (csrc/shuffle.hip).
+
+The reference shuffles every 100-row batch with pandas `sample(frac=1)` (DDM_Process.py:187,
+:190), i.e. legacy `RandomState.permutation` on numpy's global MT19937, and seeds every
+refit with 100 `randint(2**31-1)` draws of the same stream (:102).  `GpuShuffle` keeps
+that stream as raw tempered words R in HBM (draw 0 = the next draw of the state it was
+reset from) and produces:
+  * window(P, W, out)   shuffles of W full batches starting at draw P, on the device
+  * host_perm(P, L)     one batch's shuffle on the host from a few words of R (the batch
+                        before a refit, the short last batch)
+  * host_seeds(P, T)    the T per-tree seeds of a refit
+  * numpy_state(X)      numpy's exact (key, pos) after X draws (tempering is invertible)
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from ._capi import check, lib
+
+SUB, CHUNK = 128, 8192
+
+
+def expected_draws_per_batch(L):
+    """Mean 32-bit draws of `permutation(L)`: interval i takes (mask(i)+1)/(i+1) draws."""
+    return sum(((1 << int(i).bit_length()) / (i + 1)) for i in range(1, L))
+
+
+def _untemper(y):
+    y = y.astype(np.uint64)
+    y ^= y >> 18
+    y ^= (y << 15) & 0xefc60000
+    t = y.copy()
+    for _ in range(5):
+        t = y ^ ((t << 7) & 0x9d2c5680)
+    t &= 0xffffffff
+    u = t.copy()
+    for _ in range(3):
+        u = t ^ (u >> 11)
+    return (u & 0xffffffff).astype(np.uint32)
+
+
+def _temper(y):
+    y = y.astype(np.uint64)
+    y ^= y >> 11
+    y ^= (y << 7) & 0x9d2c5680
+    y ^= (y << 15) & 0xefc60000
+    y ^= y >> 18
+    return (y & 0xffffffff).astype(np.uint32)
+
+
+def fy_from_words(words, L):
+    """Legacy permutation(L) from tempered draws -> (perm uint8, draws used) or None."""
+    perm = np.arange(L, dtype=np.uint8)
+    k = 0
+    n = len(words)
+    for i in range(L - 1, 0, -1):
+        mask = (1 << int(i).bit_length()) - 1
+        while True:
+            if k >= n:
+                return None
+            v = int(words[k]) & mask
+            k += 1
+            if v <= i:
+                break
+        perm[i], perm[v] = perm[v], perm[i]
+    return perm, k
+
+
+def randint31_from_words(words, T):
+    """T x randint(2**31-1) (mask 0x7fffffff, reject 0x7fffffff) -> (seeds, draws) or None."""
+    out = np.empty(T, dtype=np.int64)
+    k = 0
+    for t in range(T):
+        while True:
+            if k >= len(words):
+                return None
+            v = int(words[k]) & 0x7fffffff
+            k += 1
+            if v <= 0x7ffffffe:
+                break
+        out[t] = v
+    return out, k
+
+
+class GpuShuffle:
+    """One partition's MT19937 stream resident in HBM, with FSM tables for batch length L."""
+
+    def __init__(self, device, L, capacity_draws, max_window, stream):
+        if not 2 <= L <= 256:
+            raise ValueError("GPU shuffles need 2 <= batch length <= 256")
+        self.device, self.L, self.S, self.stream = device, L, L - 1, stream
+        self.max_window = int(max_window)
+        self.mt = torch.zeros(625, dtype=torch.int32, device=device)
+        self._alloc(max(2 * CHUNK, int(capacity_draws)))
+        self.max_pieces = 4 + (self.max_window * L * 3) // CHUNK
+        self.pieces = torch.empty(self.max_pieces * 16, dtype=torch.uint8, device=device)
+        self.info = torch.zeros(3, dtype=torch.int64, device=device)
+        self.J = torch.zeros(self.max_window * L, dtype=torch.uint8, device=device)
+        self.E = torch.zeros(self.max_window, dtype=torch.int64, device=device)
+        self.words_h = torch.empty(4096, dtype=torch.int32, pin_memory=True)
+        self.gen = self.tab = 0
+        self.init_key = None
+        self.init_pos = 624
+
+    def _alloc(self, cap):
+        cap = (cap + CHUNK - 1) // CHUNK * CHUNK
+        R = torch.empty(cap, dtype=torch.int32, device=self.device)
+        Ts = torch.empty(cap // SUB * self.S, dtype=torch.int16, device=self.device)
+        Tc = torch.empty(cap // CHUNK * self.S, dtype=torch.int32, device=self.device)
+        if getattr(self, "R", None) is not None and self.gen:
+            with torch.cuda.stream(self.stream):
+                R[:self.gen].copy_(self.R[:self.gen])
+                Ts[:self.tab * (CHUNK // SUB) * self.S].copy_(self.Tsub[:self.tab * (CHUNK // SUB) * self.S])
+                Tc[:self.tab * self.S].copy_(self.Tchunk[:self.tab * self.S])
+        self.R, self.Tsub, self.Tchunk, self.cap = R, Ts, Tc, cap
+
+    def reset(self, rng):
+        """Draw 0 of the device stream = the next draw of `rng` (an MTStream)."""
+        self.init_key = rng.key.copy()
+        self.init_pos = int(rng.pos.value)
+        st = np.empty(625, dtype=np.uint32)
+        st[:624] = self.init_key
+        st[624] = self.init_pos
+        with torch.cuda.stream(self.stream):
+            self.mt.copy_(torch.from_numpy(st.view(np.int32)))
+        self.gen = self.tab = 0
+
+    def _sp(self):
+        return ctypes.c_void_p(self.stream.cuda_stream)
+
+    def ensure(self, upto):
+        """Generate R and tabulate chunks so that draws [0, upto) are covered."""
+        need_chunks = (int(upto) + CHUNK - 1) // CHUNK + 1
+        target = need_chunks * CHUNK
+        if target > self.cap:
+            self._alloc(max(target, int(self.cap * 1.5)))
+        if target > self.gen:
+            check(lib.ddm_shuffle_generate(self.mt.data_ptr(), self.R.data_ptr() + 4 * self.gen, target - self.gen,
+                                           self._sp()), "ddm_shuffle_generate")
+            self.gen = target
+        if need_chunks > self.tab:
+            check(lib.ddm_shuffle_tables(self.R.data_ptr(), self.tab, need_chunks - self.tab, self.L,
+                                         self.Tsub.data_ptr(), self.Tchunk.data_ptr(), self._sp()),
+                  "ddm_shuffle_tables")
+            self.tab = need_chunks
+
+    def window(self, P, W, perm_out, timer=None):
+        """Shuffles of W batches from draw P into perm_out (device uint8, W*L bytes); E[b] =
+        last draw of batch b (device)."""
+        assert 0 < W <= self.max_window and perm_out.numel() >= W * self.L
+        est = int(W * expected_draws_per_batch(self.L) * 1.15) + 4 * CHUNK
+        self.ensure(P + est)
+        ev = (None, None) if timer is None else (timer.ev[0], timer.ev[1])
+        check(lib.ddm_shuffle_window(self.R.data_ptr(), self.Tsub.data_ptr(), self.Tchunk.data_ptr(),
+                                     self.tab * CHUNK, int(P), int(W), self.L, self.pieces.data_ptr(),
+                                     self.max_pieces, self.info.data_ptr(), self.J.data_ptr(), self.E.data_ptr(),
+                                     perm_out.data_ptr(), self._sp(), *ev), "ddm_shuffle_window")
+
+    def pick(self, stop_ptr, W, offset, last, out_ptr):
+        check(lib.ddm_shuffle_pick(stop_ptr, self.E.data_ptr(), int(W), int(offset), int(last), out_ptr, self._sp()),
+              "ddm_shuffle_pick")
+
+    def words(self, P, n):
+        """Host copy of R[P:P+n] (synchronises the stream)."""
+        self.ensure(P + n)
+        if n > self.words_h.numel():
+            self.words_h = torch.empty(n, dtype=torch.int32, pin_memory=True)
+        with torch.cuda.stream(self.stream):
+            self.words_h[:n].copy_(self.R[P:P + n], non_blocking=True)
+        self.stream.synchronize()
+        return self.words_h[:n].numpy().view(np.uint32)
+
+    def host_perm(self, P, L):
+        n = max(64, 3 * L)
+        while True:
+            r = fy_from_words(self.words(P, n), L)
+            if r is not None:
+                return r[0], P + r[1]
+            n *= 2
+
+    def host_seeds(self, P, T):
+        n = T + 16
+        while True:
+            r = randint31_from_words(self.words(P, n), T)
+            if r is not None:
+                return r[0], P + r[1]
+            n *= 2
+
+    def numpy_state(self, X):
+        """numpy's ('MT19937', key, pos) after X draws of this stream."""
+        first = 624 - self.init_pos
+        if X <= first:
+            return ("MT19937", self.init_key.copy(), self.init_pos + int(X), 0, 0.0)
+        r = int(X) - first
+        q = (r - 1) // 624
+        start = first + q * 624
+        key = _untemper(self.words(start, 624))
+        return ("MT19937", key, r - q * 624, 0, 0.0)

@@ -2,10 +2,11 @@
 an exact restatement of scikit-learn 1.7.2's RandomForestClassifier.fit.
 
 The reference fits `RandomForestClassifier(n_jobs=CORES)` with random_state=None, i.e. it
-draws the 100 per-tree seeds from numpy's global RandomState; here they come from the
-partition's MT19937 stream (ddm_mt_randint31), then the trees are grown natively (the call
-releases the GIL, so partition threads refit in parallel) and come back already packed
-for ddm_forest_predict.  Inputs containing NaN (missing values) go to sklearn itself.
+draws the 100 per-tree seeds from numpy's global RandomState; the controller reads them
+from the partition's MT19937 stream, then the trees are grown natively (the call releases
+the GIL, so partition threads refit in parallel) and come back already packed for
+ddm_forest_predict.  Inputs containing NaN (missing values) return None: the controller
+then refits with sklearn itself.
 """
 import ctypes
 
@@ -61,24 +62,3 @@ class NativeForestTrainer:
         return PackedForest(self.nodes[:n_nodes].copy(), self.roots.copy(), leaf, classes.astype(np.int32),
                             bool(pure))
 
-
-def native_refit(settings):
-    """refit(X32, y, rng) for PartitionRunner: seeds from the partition RNG, native fit."""
-    import threading
-    local = threading.local()
-
-    def refit(X32, y, rng):
-        tr = getattr(local, "trainer", None)
-        if tr is None:
-            tr = local.trainer = NativeForestTrainer(settings.n_estimators)
-        snap = rng.snapshot()
-        seeds = rng.randint31(settings.n_estimators)
-        packed = tr.fit(X32, y, seeds)
-        if packed is None:                        # NaN in X: sklearn handles missing values
-            rng.restore(snap)
-            from .controller import sklearn_refit
-            tr.sklearn_fallbacks += 1
-            return sklearn_refit(settings)(X32, y, rng)
-        return packed
-
-    return refit

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 2
+#define DDM_AMD_ABI_VERSION 3
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -121,12 +121,16 @@ int ddm_forest_predict(const float* X, int64_t ld, int32_t n_features, const int
  * stop_out (device int32, may be NULL): batch of the first change or -1 (mode 0).
  * nev_out (device int64, may be NULL): number of batches with an event per stream.
  * ps_out (device double [rows][2], may be NULL): p and s after each processed row.
+ * perm_map (device uint8, may be NULL): when given, events are reported as the ROW
+ * offset inside the batch, perm_map[batch start + position] (the label the reference
+ * records at DDM_Process.py:148,151), instead of the DDM position.
  * ev_begin / ev_end (may be NULL): as for ddm_forest_predict. */
 int ddm_scan_streams(const uint8_t* err, const int64_t* stream_off, int64_t n_streams,
                      const ddm_params* prm, ddm_state* state_io, const uint64_t* first_nz,
                      const int64_t* batch_base, int64_t n_batches_total, int32_t* ev_out,
                      int32_t* stop_out, int64_t* nev_out, int32_t mode, double* ps_out,
-                     ddm_stream_t stream, ddm_event_t ev_begin, ddm_event_t ev_end);
+                     const uint8_t* perm_map, ddm_stream_t stream, ddm_event_t ev_begin,
+                     ddm_event_t ev_end);
 
 /* Timing events for the ev_begin / ev_end arguments (hipEventCreate / Destroy /
  * ElapsedTime; elapsed needs both events completed, e.g. after a stream sync). */
@@ -147,6 +151,39 @@ int ddm_mt_randint31(uint32_t* key, int32_t* pos, int64_t count, int64_t* out);
 
 /* Advance the generator by n_draws 32-bit words. */
 int ddm_mt_skip(uint32_t* key, int32_t* pos, int64_t n_draws);
+
+/* ---- batch shuffles on the GPU (csrc/shuffle.hip) -------------------------------- */
+/* The partition's MT19937 stream as raw tempered words R[0..), generated on the device,
+ * plus interval-FSM tables that make the Fisher-Yates draws of many batches parallel.
+ * Batches handled here all have batch_len rows (2..256); draws are indexed from the
+ * stream start (the state uploaded into mt_state). */
+#define DDM_SHUFFLE_SUB   128    /* draws per sub-chunk table   */
+#define DDM_SHUFFLE_CHUNK 8192   /* draws per chunk table       */
+
+/* Append n tempered words to R (device).  mt_state (device uint32[625]) = numpy key[624]
+ * followed by pos; it is advanced in place (one workgroup, 624-word blocks in LDS). */
+int ddm_shuffle_generate(uint32_t* mt_state, uint32_t* R, int64_t n, ddm_stream_t stream);
+
+/* FSM tables for chunks [chunk0, chunk0+nchunk) of R: Tsub uint16 [sub][batch_len-1],
+ * Tchunk uint32 [chunk][batch_len-1] (end interval | batches completed << 8). */
+int ddm_shuffle_tables(const uint32_t* R, int64_t chunk0, int64_t nchunk, int32_t batch_len,
+                       uint16_t* Tsub, uint32_t* Tchunk, ddm_stream_t stream);
+
+/* Shuffles of W consecutive batches whose first draw is R[P] (a batch boundary):
+ * perm_out[b*batch_len + k] (uint8) and E[b] = index of the draw completing batch b.
+ * avail = draws covered by tables (multiple of DDM_SHUFFLE_CHUNK); pieces (device,
+ * >= max_pieces * 16 bytes) and J (device, W*batch_len bytes) are scratch; info
+ * (device int64[3]) = {pieces, end draw, batches reached} (batches reached < W means
+ * avail was too small). */
+int ddm_shuffle_window(const uint32_t* R, const uint16_t* Tsub, const uint32_t* Tchunk, int64_t avail,
+                       int64_t P, int64_t W, int32_t batch_len, void* pieces, int64_t max_pieces,
+                       int64_t* info, uint8_t* J, int64_t* E, uint8_t* perm_out, ddm_stream_t stream,
+                       ddm_event_t ev_begin, ddm_event_t ev_end);
+
+/* out[0] = E[k] with k = (stop[0] >= 0 ? stop[0] : last) - offset if 0 <= k < W, else -1
+ * (device scalars; lets the controller read the RNG position with the control block). */
+int ddm_shuffle_pick(const int32_t* stop, const int64_t* E, int64_t W, int64_t offset, int64_t last,
+                     int64_t* out, ddm_stream_t stream);
 
 /* ---- host forest refit ------------------------------------------------------------ */
 

@@ -17,7 +17,8 @@ def test_header_lists_expected_entry_points():
     names = header_functions()
     for want in ("ddm_abi_version", "ddm_last_error", "ddm_forest_predict", "ddm_scan_streams", "ddm_mt_perms",
                  "ddm_mt_randint31", "ddm_mt_skip", "ddm_synth_block_labels", "ddm_synth_features",
-                 "ddm_synth_bernoulli_streams"):
+                 "ddm_synth_bernoulli_streams", "ddm_rf_fit", "ddm_shuffle_generate", "ddm_shuffle_tables",
+                 "ddm_shuffle_window", "ddm_shuffle_pick", "ddm_event_create"):
         assert want in names
 
 
@@ -44,6 +45,6 @@ def test_invalid_args_report_errors():
     rc = _capi.lib.ddm_mt_perms(None, None, None, 0, None, None)
     assert rc == _capi.DDM_E_ARG
     rc = _capi.lib.ddm_scan_streams(None, None, 1, None, None, None, None, 0, None, None, None, 0, None, None,
-                                    None, None)
+                                    None, None, None)
     assert rc == _capi.DDM_E_ARG
     assert b"invalid argument" in _capi.lib.ddm_last_error()

@@ -72,20 +72,3 @@ def test_too_many_classes_rejected():
     with pytest.raises(ValueError):
         pack(tree_arrays(rf), rf.classes_)
 
-
-def test_refit_worker_equals_global_rng_fit():
-    """ddm_amd.refit.fit_packed (the host refit backend) draws the same 100 tree seeds from the
-    passed MT19937 state as RandomForestClassifier(random_state=None) from np.random."""
-    from ddm_amd.refit import fit_packed
-    rs = np.random.RandomState(8)
-    X = rs.rand(100, 5).astype(np.float32)
-    y = (np.arange(100) // 40).astype(np.int64)
-    np.random.seed(123)
-    st = np.random.get_state()
-    rf = RandomForestClassifier().fit(X.astype(np.float64), y)
-    want = pack_sklearn(rf)
-    after = np.random.get_state()
-    got, key, pos = fit_packed(X, y, st[1], st[2])
-    assert np.array_equal(got.nodes, want.nodes) and np.array_equal(got.roots, want.roots)
-    assert np.array_equal(key, after[1]) and pos == after[2]
-    assert got.features_used == want.features_used > 0

@@ -1,0 +1,96 @@
+"""GPU batch shuffles (csrc/shuffle.hip) == numpy's legacy permutation stream, draw for draw."""
+import numpy as np
+import pytest
+import torch
+
+from ddm_amd.rng import MTStream
+
+pytestmark = pytest.mark.gpu
+
+
+def _mk(L, cap=1 << 20, max_window=70000):
+    from ddm_amd.shuffle import GpuShuffle
+    dev = torch.device("cuda", 0)
+    return GpuShuffle(dev, L, cap, max_window, torch.cuda.current_stream(dev))
+
+
+def test_raw_stream_equals_numpy():
+    sh = _mk(100)
+    for seed, pre in ((1, 0), (2, 5), (3, 623), (4, 624 * 3 + 17)):
+        mt = MTStream.from_seed(seed)
+        mt.skip(pre)
+        sh.reset(mt)
+        got = sh.words(0, 50000).copy()
+        rs = np.random.RandomState(seed)
+        if pre:
+            rs.randint(0, 2**32, pre, dtype=np.uint64)
+        want = rs.randint(0, 2**32, 50000, dtype=np.uint64).astype(np.uint32)
+        assert np.array_equal(got, want), (seed, pre)
+
+
+@pytest.mark.parametrize("L", [100, 2, 7, 256])
+def test_windows_equal_host_permutations(L):
+    sh = _mk(L)
+    for seed, pre in ((11, 0), (12, 333)):
+        mt = MTStream.from_seed(seed)
+        mt.skip(pre)
+        host = mt.copy()
+        sh.reset(mt)
+        dev = torch.device("cuda", 0)
+        P = 0
+        for W in (1, 3, 64, 1000, 9000):
+            out = torch.zeros(W * L, dtype=torch.uint8, device=dev)
+            sh.window(P, W, out)
+            torch.cuda.synchronize()
+            draws = np.zeros(W, dtype=np.int64)
+            want = host.perms(np.full(W, L, np.int32), draws=draws)
+            assert np.array_equal(out.cpu().numpy(), want), (seed, W)
+            E = sh.E[:W].cpu().numpy()
+            assert np.array_equal(E, P + np.cumsum(draws) - 1)
+            info = sh.info.cpu().numpy()
+            assert info[2] >= W
+            P = int(E[-1]) + 1
+            ns = sh.numpy_state(P)
+            assert np.array_equal(ns[1], host.key) and ns[2] == host.pos.value
+
+
+def test_host_helpers_interleave_with_windows():
+    """The controller's sequence: window, host perm, seeds, window — same as numpy."""
+    sh = _mk(100)
+    mt = MTStream.from_seed(99)
+    sh.reset(mt)
+    rs = np.random.RandomState(99)
+    dev = torch.device("cuda", 0)
+    out = torch.zeros(500 * 100, dtype=torch.uint8, device=dev)
+    sh.window(0, 500, out)
+    torch.cuda.synchronize()
+    want = np.concatenate([rs.permutation(100) for _ in range(500)])
+    assert np.array_equal(out.cpu().numpy(), want)
+    P = int(sh.E[499].item()) + 1
+    perm, P = sh.host_perm(P, 100)
+    assert np.array_equal(perm, rs.permutation(100))
+    seeds, P = sh.host_seeds(P, 100)
+    assert np.array_equal(seeds, [rs.randint(2147483647) for _ in range(100)])
+    perm, P = sh.host_perm(P, 37)
+    assert np.array_equal(perm, rs.permutation(37))
+    sh.window(P, 200, out)
+    torch.cuda.synchronize()
+    want = np.concatenate([rs.permutation(100) for _ in range(200)])
+    assert np.array_equal(out[:20000].cpu().numpy(), want)
+    P = int(sh.E[199].item()) + 1
+    ns = sh.numpy_state(P)
+    st = rs.get_state()
+    assert np.array_equal(ns[1], st[1]) and ns[2] == st[2]
+
+
+def test_stream_growth():
+    """Capacity grows (R and tables copied) when a window needs more draws."""
+    sh = _mk(100, cap=20000, max_window=5000)
+    mt = MTStream.from_seed(5)
+    host = mt.copy()
+    sh.reset(mt)
+    dev = torch.device("cuda", 0)
+    out = torch.zeros(5000 * 100, dtype=torch.uint8, device=dev)
+    sh.window(0, 5000, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), host.perms(np.full(5000, 100, np.int32)))
