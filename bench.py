@@ -22,6 +22,10 @@ import sys
 import threading
 import time
 
+# one HIP stream per partition: give HIP enough hardware queues to run them concurrently
+# (HIP's default is 4 per process; must be set before the runtime initialises)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "distributed-drift-detection_amd"))
 sys.path.insert(0, ROOT)

@@ -75,10 +75,11 @@ __global__ __launch_bounds__(256) void k_scan_streams(
     const uint8_t* __restrict__ err, const int64_t* __restrict__ off, int64_t n_streams,
     ddm_params P, ddm_state* __restrict__ state, const uint64_t* __restrict__ first_nz,
     const int64_t* __restrict__ batch_base, int32_t* __restrict__ ev, int32_t* __restrict__ stop_out,
-    int64_t* __restrict__ nev_out, int mode, double* __restrict__ ps_out, const uint8_t* __restrict__ pmap) {
+    int64_t* __restrict__ nev_out, int mode, double* __restrict__ ps_out, const uint8_t* __restrict__ pmap,
+    const int64_t* __restrict__ stream_end) {
     const int64_t sid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (sid >= n_streams) return;
-    const int64_t lo = off[sid], hi = off[sid + 1];
+    const int64_t lo = off[sid], hi = stream_end ? stream_end[sid] : off[sid + 1];
     const int64_t pb = P.per_batch;
     const int min_inst = P.min_num_instances;
     const double wl = P.warning_level, cl = P.out_control_level;
@@ -197,8 +198,8 @@ extern "C" int ddm_scan_streams(const uint8_t* err, const int64_t* stream_off, i
                                 const ddm_params* prm, ddm_state* state_io, const uint64_t* first_nz,
                                 const int64_t* batch_base, int64_t n_batches_total, int32_t* ev_out,
                                 int32_t* stop_out, int64_t* nev_out, int32_t mode, double* ps_out,
-                                const uint8_t* perm_map, ddm_stream_t stream, ddm_event_t ev_begin,
-                                ddm_event_t ev_end) {
+                                const uint8_t* perm_map, const int64_t* stream_end, ddm_stream_t stream,
+                                ddm_event_t ev_begin, ddm_event_t ev_end) {
     if (!err || !stream_off || !prm || !state_io || !batch_base || !ev_out || n_streams < 0 ||
         n_batches_total < 0 || prm->per_batch <= 0 || (mode != 0 && mode != 1)) {
         ddm::set_error("ddm_scan_streams: invalid argument");
@@ -214,7 +215,8 @@ extern "C" int ddm_scan_streams(const uint8_t* err, const int64_t* stream_off, i
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
     hipLaunchKernelGGL(k_scan_streams, dim3((unsigned)blocks), dim3(threads), 0, s, err, stream_off, n_streams, *prm,
-                       state_io, first_nz, batch_base, ev_out, stop_out, nev_out, (int)mode, ps_out, perm_map);
+                       state_io, first_nz, batch_base, ev_out, stop_out, nev_out, (int)mode, ps_out, perm_map,
+                       stream_end);
     if (ev_end)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
     return ddm::launch_status("ddm_scan_streams");

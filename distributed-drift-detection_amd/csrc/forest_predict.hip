@@ -16,6 +16,8 @@
 // error vector comes out already in DDM order.  The forest (16-byte nodes) sits in
 // LDS when it fits, shared by the workgroup's rows for its whole grid-stride loop.
 // The first error position is reduced per wave with a ballot and one atomicMin.
+#include <vector>
+
 #include "common.h"
 
 namespace {
@@ -36,35 +38,52 @@ __device__ __forceinline__ int leaf_of(const ddm_node* __restrict__ nodes, int n
     }
 }
 
+// One segment of predict work: DDM positions [pos_begin, pos_end) of one partition with
+// its forest.  The batch entry point takes a device array of these (one per partition).
+struct Seg {
+    const float* X;
+    int64_t ld;
+    const int32_t* y;
+    const uint8_t* perm;
+    uint8_t* err;
+    int32_t* pred;
+    unsigned long long* first_err;
+    int64_t pos_begin, pos_end;
+    const ddm_node* nodes;
+    const int32_t* roots;
+    const double* leaf_value;
+    const int32_t* classes;
+    int32_t n_trees, n_classes, n_nodes, pure;
+    int64_t row_base;            // rows are (g / per_batch) * per_batch + perm[g] - row_base
+    int64_t block0, nblocks;     // this segment's blocks in the launch grid
+};
+
 template <bool kPure, int kK, bool kLdsForest>
-__global__ __launch_bounds__(kThreads) void k_forest_predict(
-    const float* __restrict__ X, int64_t ld, const int32_t* __restrict__ y, const uint8_t* __restrict__ perm,
-    int64_t pos_begin, int64_t pos_end, int64_t per_batch, const ddm_node* __restrict__ g_nodes,
-    const int32_t* __restrict__ g_roots, const double* __restrict__ leaf_value, const int32_t* __restrict__ classes,
-    int n_trees, int n_classes, int n_nodes, uint8_t* __restrict__ err_out, unsigned long long* __restrict__ first_err,
-    int32_t* __restrict__ pred_out) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const ddm_node* nodes = g_nodes;
-    const int32_t* roots = g_roots;
+__device__ __forceinline__ void predict_segment(const Seg& sg, int64_t blk, int64_t nblk, int64_t per_batch,
+                                                unsigned char* smem) {
+    const ddm_node* nodes = sg.nodes;
+    const int32_t* roots = sg.roots;
+    const float* __restrict__ X = sg.X;
+    const int64_t ld = sg.ld;
+    const int n_trees = sg.n_trees, n_classes = sg.n_classes;
     if constexpr (kLdsForest) {
         uint4* dst = reinterpret_cast<uint4*>(smem);
-        const uint4* src = reinterpret_cast<const uint4*>(g_nodes);
-        for (int k = threadIdx.x; k < n_nodes; k += kThreads) dst[k] = src[k];
-        int32_t* r = reinterpret_cast<int32_t*>(smem + (size_t)n_nodes * sizeof(ddm_node));
-        for (int k = threadIdx.x; k < n_trees; k += kThreads) r[k] = g_roots[k];
+        const uint4* src = reinterpret_cast<const uint4*>(sg.nodes);
+        for (int k = threadIdx.x; k < sg.n_nodes; k += kThreads) dst[k] = src[k];
+        int32_t* r = reinterpret_cast<int32_t*>(smem + (size_t)sg.n_nodes * sizeof(ddm_node));
+        for (int k = threadIdx.x; k < n_trees; k += kThreads) r[k] = sg.roots[k];
         __syncthreads();
         nodes = reinterpret_cast<const ddm_node*>(smem);
         roots = r;
     }
     const int lane = threadIdx.x & 63;
-    const int64_t stride = (int64_t)gridDim.x * kThreads;
-    for (int64_t base = pos_begin + (int64_t)blockIdx.x * kThreads + (threadIdx.x & ~63); base < pos_end;
-         base += stride) {
+    const int64_t stride = nblk * kThreads;
+    for (int64_t base = sg.pos_begin + blk * kThreads + (threadIdx.x & ~63); base < sg.pos_end; base += stride) {
         const int64_t g = base + lane;
-        const bool valid = g < pos_end;
+        const bool valid = g < sg.pos_end;
         int e = 0;
         if (valid) {
-            const int64_t row = (g / per_batch) * per_batch + perm[g];
+            const int64_t row = (g / per_batch) * per_batch + sg.perm[g] - sg.row_base;
             int best_k = 0;
             if constexpr (kPure) {
                 constexpr int kRegs = (kK + 3) / 4;
@@ -92,7 +111,7 @@ __global__ __launch_bounds__(kThreads) void k_forest_predict(
                 for (int k = 0; k < kK; ++k) acc[k] = 0.0;
                 for (int t = 0; t < n_trees; ++t) {
                     const int lr = leaf_of<kLdsForest>(nodes, roots[t], X, ld, row);
-                    const double* lv = leaf_value + (int64_t)lr * n_classes;
+                    const double* lv = sg.leaf_value + (int64_t)lr * n_classes;
 #pragma unroll
                     for (int k = 0; k < kK; ++k)
                         if (k < n_classes) acc[k] += lv[k];
@@ -108,21 +127,40 @@ __global__ __launch_bounds__(kThreads) void k_forest_predict(
                     }
                 }
             }
-            const int32_t label = classes[best_k];
-            e = label != y[row];
-            err_out[g] = (uint8_t)e;
-            if (pred_out) pred_out[g] = label;
+            const int32_t label = sg.classes[best_k];
+            e = label != sg.y[row];
+            sg.err[g] = (uint8_t)e;
+            if (sg.pred) sg.pred[g] = label;
         }
-        if (first_err) {
+        if (sg.first_err) {
             const unsigned long long m = __ballot(e);
-            if (m && lane == __ffsll((long long)m) - 1) atomicMin(first_err, (unsigned long long)g);
+            if (m && lane == __ffsll((long long)m) - 1) atomicMin(sg.first_err, (unsigned long long)g);
         }
     }
 }
 
-using predict_fn = void (*)(const float*, int64_t, const int32_t*, const uint8_t*, int64_t, int64_t, int64_t,
-                            const ddm_node*, const int32_t*, const double*, const int32_t*, int, int, int, uint8_t*,
-                            unsigned long long*, int32_t*);
+template <bool kPure, int kK, bool kLdsForest>
+__global__ __launch_bounds__(kThreads) void k_forest_predict(Seg sg, int64_t per_batch) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    predict_segment<kPure, kK, kLdsForest>(sg, blockIdx.x, gridDim.x, per_batch, smem);
+}
+
+// Batched: every block finds its segment (one per partition) and works on it.  Segments
+// are ordered by their global block range; this launch covers blocks [block_base, ...).
+template <bool kPure, int kK, bool kLdsForest>
+__global__ __launch_bounds__(kThreads) void k_forest_predict_batch(const Seg* __restrict__ segs, int n_segs,
+                                                                   int64_t block_base, int64_t per_batch) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int64_t gb = block_base + blockIdx.x;
+    int s = 0;
+    while (s < n_segs && !(segs[s].block0 <= gb && gb < segs[s].block0 + segs[s].nblocks)) ++s;
+    if (s == n_segs) return;
+    const Seg sg = segs[s];
+    predict_segment<kPure, kK, kLdsForest>(sg, gb - sg.block0, sg.nblocks, per_batch, smem);
+}
+
+using predict_fn = void (*)(Seg, int64_t);
+using predict_batch_fn = void (*)(const Seg*, int, int64_t, int64_t);
 
 template <bool kLds>
 predict_fn pick(bool pure, int k) {
@@ -135,6 +173,23 @@ predict_fn pick(bool pure, int k) {
     if (k <= 4) return k_forest_predict<false, 4, kLds>;
     if (k <= 16) return k_forest_predict<false, 16, kLds>;
     return k_forest_predict<false, 64, kLds>;
+}
+
+template <bool kLds>
+predict_batch_fn pick_batch(bool pure, int k) {
+    if (pure) {
+        if (k <= 4) return k_forest_predict_batch<true, 4, kLds>;
+        if (k <= 8) return k_forest_predict_batch<true, 8, kLds>;
+        if (k <= 16) return k_forest_predict_batch<true, 16, kLds>;
+        return k_forest_predict_batch<true, 64, kLds>;
+    }
+    if (k <= 4) return k_forest_predict_batch<false, 4, kLds>;
+    if (k <= 16) return k_forest_predict_batch<false, 16, kLds>;
+    return k_forest_predict_batch<false, 64, kLds>;
+}
+
+size_t forest_lds_bytes(int n_nodes, int n_trees) {
+    return ((size_t)n_nodes * sizeof(ddm_node) + (size_t)n_trees * 4 + 15) & ~(size_t)15;
 }
 
 }  // namespace
@@ -162,18 +217,99 @@ extern "C" int ddm_forest_predict(const float* X, int64_t ld, int32_t n_features
     }
     const int64_t n = pos_end - pos_begin;
     if (n == 0) return 0;
-    const size_t lds = ((size_t)forest->n_nodes * sizeof(ddm_node) + (size_t)forest->n_trees * 4 + 15) & ~(size_t)15;
+    const size_t lds = forest_lds_bytes(forest->n_nodes, forest->n_trees);
     const bool use_lds = lds <= (size_t)kMaxLdsForest;
     const predict_fn fn = use_lds ? pick<true>(forest->pure, forest->n_classes)
                                   : pick<false>(forest->pure, forest->n_classes);
     const int64_t blocks = std::min<int64_t>(ddm::ceil_div(n, kThreads), 256 * 8);
+    Seg sg{X, ld, y, perm, err_out, pred_out, reinterpret_cast<unsigned long long*>(first_err), pos_begin, pos_end,
+           forest->nodes, forest->roots, forest->leaf_value, forest->classes, forest->n_trees, forest->n_classes,
+           forest->n_nodes, forest->pure, 0, 0, blocks};
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
-    hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kThreads), use_lds ? lds : 0, s, X, ld, y, perm, pos_begin,
-                       pos_end, (int64_t)per_batch, forest->nodes, forest->roots, forest->leaf_value,
-                       forest->classes, forest->n_trees, forest->n_classes, forest->n_nodes, err_out,
-                       reinterpret_cast<unsigned long long*>(first_err), pred_out);
+    hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kThreads), use_lds ? lds : 0, s, sg, (int64_t)per_batch);
     if (ev_end)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
     return ddm::launch_status("ddm_forest_predict");
+}
+
+static_assert(sizeof(Seg) == sizeof(ddm_predict_segment), "ddm_predict_segment layout");
+
+extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, ddm_predict_segment* segs_dev,
+                                        int32_t n_segs, int32_t per_batch, ddm_stream_t stream, ddm_event_t ev_begin,
+                                        ddm_event_t ev_end) {
+    if (!segs_host || !segs_dev || n_segs <= 0 || per_batch <= 0 || per_batch > 256) {
+        ddm::set_error("ddm_forest_predict_batch: invalid argument");
+        return DDM_E_ARG;
+    }
+    hipStream_t s = ddm::as_hip(stream);
+    // One launch per kernel variant (pure/impure x classes x LDS-resident forest); every
+    // launch walks the whole device table and only the blocks assigned to its segments
+    // work.  Block counts are proportional to rows, 2048 blocks in total per variant.
+    Seg* hs = reinterpret_cast<Seg*>(const_cast<ddm_predict_segment*>(segs_host));
+    for (int i = 0; i < n_segs; ++i) {
+        const Seg& g = hs[i];
+        if (!g.X || !g.y || !g.perm || !g.err || !g.nodes || !g.roots || !g.classes || g.pos_end < g.pos_begin ||
+            g.n_classes <= 0 || g.n_classes > 64 || g.n_trees <= 0 || (g.pure && g.n_trees > 255) ||
+            (!g.pure && !g.leaf_value)) {
+            ddm::set_error("ddm_forest_predict_batch: invalid segment %d", i);
+            return DDM_E_ARG;
+        }
+        if (g.first_err)
+            if (int rc = ddm::hip_status(hipMemsetAsync(g.first_err, 0xff, sizeof(uint64_t), s), "predict_batch memset"))
+                return rc;
+    }
+    if (ev_begin)
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
+    // Variants (pure/impure x classes x LDS-resident forest) get disjoint global block
+    // ranges, so ONE copy of the table serves one launch per variant present.
+    std::vector<int> variant(n_segs);
+    for (int i = 0; i < n_segs; ++i) {
+        const Seg& g = hs[i];
+        const bool lds = forest_lds_bytes(g.n_nodes, g.n_trees) <= (size_t)kMaxLdsForest;
+        const int kc = g.n_classes <= 4 ? 0 : g.n_classes <= 8 ? 1 : g.n_classes <= 16 ? 2 : 3;
+        variant[i] = (g.pure ? 1 : 0) * 8 + (lds ? 4 : 0) + kc;
+    }
+    int64_t vbase[17] = {0};
+    size_t vlds[16] = {0};
+    int64_t b0 = 0;
+    for (int v = 0; v < 16; ++v) {
+        vbase[v] = b0;
+        int64_t rows = 0;
+        for (int i = 0; i < n_segs; ++i)
+            if (variant[i] == v) {
+                rows += hs[i].pos_end - hs[i].pos_begin;
+                vlds[v] = std::max(vlds[v], forest_lds_bytes(hs[i].n_nodes, hs[i].n_trees));
+            }
+        const int64_t total_blocks = rows ? std::min<int64_t>(ddm::ceil_div(rows, kThreads), 256 * 8) : 0;
+        for (int i = 0; i < n_segs; ++i) {
+            if (variant[i] != v) continue;
+            Seg& g = hs[i];
+            const int64_t r = g.pos_end - g.pos_begin;
+            g.block0 = b0;
+            g.nblocks = r == 0 ? 0 : std::max<int64_t>(1, (total_blocks * r + rows - 1) / rows);
+            b0 += g.nblocks;
+        }
+    }
+    vbase[16] = b0;
+    if (b0 > 0) {
+        if (int rc = ddm::hip_status(hipMemcpyAsync(segs_dev, hs, sizeof(Seg) * n_segs, hipMemcpyHostToDevice, s),
+                                     "predict_batch table"))
+            return rc;
+    }
+    for (int v = 0; v < 16; ++v) {
+        const int64_t nb = vbase[v + 1] - vbase[v];
+        if (nb == 0) continue;
+        const bool lds = (v & 4) != 0;
+        const bool pure = (v & 8) != 0;
+        const int kmax = (v & 3) == 0 ? 4 : (v & 3) == 1 ? 8 : (v & 3) == 2 ? 16 : 64;
+        const predict_batch_fn fn = lds ? pick_batch<true>(pure, kmax) : pick_batch<false>(pure, kmax);
+        hipLaunchKernelGGL(fn, dim3((unsigned)nb), dim3(kThreads), lds ? vlds[v] : 0, s,
+                           reinterpret_cast<const Seg*>(segs_dev), n_segs, vbase[v],
+                           (int64_t)per_batch);
+        if (int rc = ddm::launch_status("ddm_forest_predict_batch")) return rc;
+    }
+    if (ev_end)
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
+    return 0;
 }

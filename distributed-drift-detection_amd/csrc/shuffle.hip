@@ -45,46 +45,74 @@ __device__ __forceinline__ uint32_t mt_word(uint32_t a, uint32_t b, uint32_t c) 
 
 __device__ __forceinline__ uint32_t imask(uint32_t i) { return 0xffffffffu >> __builtin_clz(i); }
 
-// state word: key[624] (untempered) followed by pos (number of words of key consumed)
+// state word: key[624] (untempered) followed by pos (number of words of key consumed).
+// Double-buffered regeneration: the new block is computed from the old one in three
+// dependency phases (words 0..226 need only old words; 227..453 need new 0..226;
+// 454..623 need new 227..396 and new 0), each thread tempering and storing the words it
+// produced, so a 624-word block costs three barriers.
+__device__ void mt_generate(uint32_t* __restrict__ state, uint32_t* __restrict__ R, int64_t n) {
+    __shared__ uint32_t buf[2][kN];
+    for (int k = threadIdx.x; k < kN; k += 256) buf[0][k] = state[k];
+    const int pos0 = (int)state[kN];
+    __syncthreads();
+    int cur = 0;
+    int64_t out = 0;
+    const int t = threadIdx.x;
+    // the rest of the current block
+    if (pos0 < kN) {
+        const int take = (int)min((int64_t)(kN - pos0), n);
+        for (int k = t; k < take; k += 256) R[k] = temper(buf[0][pos0 + k]);
+        out = take;
+    }
+    int pos = pos0 < kN ? pos0 + (int)out : kN;
+    while (out < n) {
+        const uint32_t* o = buf[cur];
+        uint32_t* w = buf[cur ^ 1];
+        const int64_t base = out;
+        const int64_t lim = n - base;   // words of this block to emit
+        if (t < 227) {
+            const uint32_t v = mt_word(o[t], o[t + 1], o[t + 397]);
+            w[t] = v;
+            if (t < lim) R[base + t] = temper(v);
+        }
+        __syncthreads();
+        if (t < 227) {
+            const int i = 227 + t;
+            const uint32_t v = mt_word(o[i], o[i + 1], w[t]);
+            w[i] = v;
+            if (i < lim) R[base + i] = temper(v);
+        }
+        __syncthreads();
+        if (t < 170) {
+            const int i = 454 + t;
+            const uint32_t v = (i < kN - 1) ? mt_word(o[i], o[i + 1], w[i - 227]) : mt_word(o[kN - 1], w[0], w[396]);
+            w[i] = v;
+            if (i < lim) R[base + i] = temper(v);
+        }
+        __syncthreads();
+        cur ^= 1;
+        const int take = (int)min((int64_t)kN, lim);
+        out += take;
+        pos = take;
+    }
+    for (int k = t; k < kN; k += 256) state[k] = buf[cur][k];
+    if (t == 0) state[kN] = (uint32_t)pos;
+}
+
 __global__ __launch_bounds__(256) void k_mt_generate(uint32_t* __restrict__ state, uint32_t* __restrict__ R,
                                                      int64_t n) {
-    __shared__ uint32_t key[kN];
-    __shared__ int s_pos;
-    for (int k = threadIdx.x; k < kN; k += 256) key[k] = state[k];
-    if (threadIdx.x == 0) s_pos = (int)state[kN];
-    __syncthreads();
-    int pos = s_pos;
-    int64_t out = 0;
-    while (out < n) {
-        if (pos >= kN) {
-            // in-place regeneration in three dependency phases (same result as the
-            // sequential loop: word i uses new words only where the loop would)
-            uint32_t v = 0;
-            const int t = threadIdx.x;
-            if (t < 227) v = mt_word(key[t], key[t + 1], key[t + 397]);
-            __syncthreads();
-            if (t < 227) key[t] = v;
-            __syncthreads();
-            if (t < 227) v = mt_word(key[227 + t], key[228 + t], key[t]);
-            __syncthreads();
-            if (t < 227) key[227 + t] = v;
-            __syncthreads();
-            if (t < 169) v = mt_word(key[454 + t], key[455 + t], key[227 + t]);
-            else if (t == 169) v = mt_word(key[623], key[0], key[396]);
-            __syncthreads();
-            if (t < 169) key[454 + t] = v;
-            else if (t == 169) key[623] = v;
-            __syncthreads();
-            pos = 0;
-        }
-        const int take = (int)min((int64_t)(kN - pos), n - out);
-        for (int k = threadIdx.x; k < take; k += 256) R[out + k] = temper(key[pos + k]);
-        out += take;
-        pos += take;
-    }
-    __syncthreads();
-    for (int k = threadIdx.x; k < kN; k += 256) state[k] = key[k];
-    if (threadIdx.x == 0) state[kN] = (uint32_t)pos;
+    mt_generate(state, R, n);
+}
+
+struct GenJob {
+    uint32_t* state;
+    uint32_t* R;
+    int64_t n;
+};
+
+__global__ __launch_bounds__(256) void k_mt_generate_batch(const GenJob* __restrict__ jobs) {
+    const GenJob j = jobs[blockIdx.x];
+    mt_generate(j.state, j.R, j.n);
 }
 
 // Tsub[sub][s-1] = end_state | batches_done << 8, for s in [1, L-1].
@@ -132,6 +160,21 @@ __global__ __launch_bounds__(256) void k_fsm_chunk(const uint16_t* __restrict__ 
     }
 }
 
+struct Job {
+    const uint32_t* R;
+    const uint16_t* Tsub;
+    const uint32_t* Tchunk;
+    int64_t avail, P, W;
+    void* pieces;
+    int64_t* info;
+    uint8_t* J;
+    int64_t* E;
+    uint8_t* perm_out;
+    const int32_t* stop;
+    int64_t pick_offset, pick_last;
+    int64_t* pick_out;
+};
+
 struct ChunkStart {
     int64_t pos;      // first draw of this window piece
     int32_t state;    // interval index at pos
@@ -144,20 +187,32 @@ struct ChunkStart {
 // the serial walk does LDS lookups, not dependent HBM loads.
 // out[0] = the piece [P, first chunk boundary); out[k] = chunk starts.
 // info = {pieces, end draw, batches reached}.
-__global__ __launch_bounds__(64) void k_fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restrict__ Tsub,
-                                                 const uint32_t* __restrict__ Tchunk, int64_t P, int64_t W, int L,
-                                                 int64_t avail, ChunkStart* __restrict__ out,
-                                                 int64_t* __restrict__ info) {
-    extern __shared__ uint32_t tab[];   // [64][S]
+__device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restrict__ Tsub,
+                         const uint32_t* __restrict__ Tchunk, int64_t P, int64_t W, int L, int64_t avail,
+                         ChunkStart* __restrict__ out, int64_t* __restrict__ info) {
+    extern __shared__ uint32_t tab[];   // [64][S] chunk rows; phase A: draws + sub-chunk rows
     __shared__ int64_t sh_pos, sh_batch, sh_k;
     __shared__ uint32_t sh_s;
     const int S = L - 1;
+    // phase A inputs: the draws up to the next sub-chunk boundary and the sub-chunk rows up
+    // to the next chunk boundary, staged in LDS by all lanes
+    const int64_t sub_end = min(avail, (P / kSub + 1) * kSub);
+    const int64_t chunk_end = min(avail, (P / kChunk + 1) * kChunk);
+    const int n_draws = (int)max((int64_t)0, sub_end - P);
+    const int64_t first_sub = sub_end / kSub;
+    const int n_subrows = (int)max((int64_t)0, (chunk_end - sub_end) / kSub);
+    uint32_t* a_draws = tab;
+    uint16_t* a_sub = reinterpret_cast<uint16_t*>(tab + kSub);
+    for (int k = threadIdx.x; k < n_draws; k += 64) a_draws[k] = R[P + k];
+    for (int64_t e = threadIdx.x; e < (int64_t)n_subrows * S; e += 64) a_sub[e] = Tsub[first_sub * S + e];
+    __syncthreads();
     if (threadIdx.x == 0) {
         int64_t pos = P, batch = 0, k = 0;
         uint32_t s = (uint32_t)S;
         out[k++] = ChunkStart{pos, (int32_t)s, 0};
-        while (batch < W && pos % kSub != 0 && pos < avail) {
-            const uint32_t v = R[pos++];
+        while (batch < W && pos < sub_end) {
+            const uint32_t v = a_draws[pos - P];
+            ++pos;
             if ((v & imask(s)) <= s) {
                 if (s == 1) {
                     s = (uint32_t)S;
@@ -168,7 +223,7 @@ __global__ __launch_bounds__(64) void k_fsm_walk(const uint32_t* __restrict__ R,
             }
         }
         while (batch < W && pos % kChunk != 0 && pos + kSub <= avail) {
-            const uint32_t e = Tsub[(pos / kSub) * S + (s - 1)];
+            const uint32_t e = a_sub[(pos / kSub - first_sub) * S + (s - 1)];
             s = e & 0xffu;
             batch += e >> 8;
             pos += kSub;
@@ -184,6 +239,7 @@ __global__ __launch_bounds__(64) void k_fsm_walk(const uint32_t* __restrict__ R,
         if (sh_batch >= W || pos0 + kChunk > avail) break;
         const int64_t c0 = pos0 / kChunk;
         const int nload = (int)min((int64_t)64, (avail - pos0) / kChunk);
+        __syncthreads();
         for (int64_t e = threadIdx.x; e < (int64_t)nload * S; e += 64) tab[e] = Tchunk[c0 * S + e];
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -210,21 +266,32 @@ __global__ __launch_bounds__(64) void k_fsm_walk(const uint32_t* __restrict__ R,
     }
 }
 
+__global__ __launch_bounds__(64) void k_fsm_walk(Job j, int L) {
+    fsm_walk(j.R, j.Tsub, j.Tchunk, j.P, j.W, L, j.avail, reinterpret_cast<ChunkStart*>(j.pieces), j.info);
+}
+
+__global__ __launch_bounds__(64) void k_fsm_walk_batch(const Job* __restrict__ jobs, int L) {
+    const Job j = jobs[blockIdx.x];
+    if (j.W <= 0) return;
+    fsm_walk(j.R, j.Tsub, j.Tchunk, j.P, j.W, L, j.avail, reinterpret_cast<ChunkStart*>(j.pieces), j.info);
+}
+
 // One wave per window piece.  The piece's sub-chunk table rows are staged in LDS, lane 0
 // derives every sub-chunk's start (state, batch); then the lanes replay sub-chunks: for
 // each accepted draw of batch b < W record J[b*L + s] = v & mask(s) and, when s == 1,
 // E[b] = draw index.
-__global__ __launch_bounds__(64) void k_fsm_replay(const uint32_t* __restrict__ R, const uint16_t* __restrict__ Tsub,
-                                                   const ChunkStart* __restrict__ pieces,
-                                                   const int64_t* __restrict__ info, int64_t W, int L,
-                                                   uint8_t* __restrict__ J, int64_t* __restrict__ E) {
-    extern __shared__ uint16_t subtab[];   // [64][S]
+__device__ void fsm_replay(const uint32_t* __restrict__ R, const uint16_t* __restrict__ Tsub,
+                           const ChunkStart* __restrict__ pieces, const int64_t* __restrict__ info, int64_t W, int L,
+                           uint8_t* __restrict__ J, int64_t* __restrict__ E, int64_t blk, int64_t nblk) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t rep_lds[];   // [kChunk] draws, then [64][S] rows
+    uint32_t* draws = rep_lds;
+    uint16_t* subtab = reinterpret_cast<uint16_t*>(rep_lds + kChunk);
     __shared__ int64_t sub_pos[kSubPerChunk + 2];
     __shared__ int32_t sub_state[kSubPerChunk + 2], sub_batch[kSubPerChunk + 2];
     __shared__ int n_subs;
     const int64_t npieces = info[0], end = info[1];
     const int S = L - 1;
-    for (int64_t pc = blockIdx.x; pc < npieces; pc += gridDim.x) {
+    for (int64_t pc = blk; pc < npieces; pc += nblk) {
         const ChunkStart c = pieces[pc];
         const int64_t stop = (pc + 1 < npieces) ? pieces[pc + 1].pos : end;
         // stage the table rows of the whole sub-chunks of this piece's chunk
@@ -234,6 +301,9 @@ __global__ __launch_bounds__(64) void k_fsm_replay(const uint32_t* __restrict__ 
             const int64_t sb = first_sub + e / S;
             if ((sb + 1) * kSub <= stop) subtab[e] = Tsub[first_sub * S + e];
         }
+        // the piece's draws (a piece lies inside one chunk)
+        const int64_t dbase = chunk * kChunk;
+        for (int64_t q = c.pos + threadIdx.x; q < stop; q += 64) draws[q - dbase] = R[q];
         __syncthreads();
         if (threadIdx.x == 0) {
             int64_t pos = c.pos;
@@ -252,7 +322,7 @@ __global__ __launch_bounds__(64) void k_fsm_replay(const uint32_t* __restrict__ 
                     b += (int32_t)(e >> 8);
                 } else {
                     for (int64_t q = pos; q < nxt; ++q) {
-                        const uint32_t v = R[q];
+                        const uint32_t v = draws[q - dbase];
                         if ((v & imask(s)) <= s) {
                             if (s == 1) {
                                 s = (uint32_t)S;
@@ -273,7 +343,7 @@ __global__ __launch_bounds__(64) void k_fsm_replay(const uint32_t* __restrict__ 
             uint32_t s = (uint32_t)sub_state[t];
             int64_t b = sub_batch[t];
             for (int64_t q = sub_pos[t]; q < sub_pos[t + 1] && b < W; ++q) {
-                const uint32_t v = R[q];
+                const uint32_t v = draws[q - dbase];
                 const uint32_t m = v & imask(s);
                 if (m <= s) {
                     J[b * L + s] = (uint8_t)m;
@@ -291,11 +361,22 @@ __global__ __launch_bounds__(64) void k_fsm_replay(const uint32_t* __restrict__ 
     }
 }
 
+__global__ __launch_bounds__(64) void k_fsm_replay(Job j, int L) {
+    fsm_replay(j.R, j.Tsub, reinterpret_cast<const ChunkStart*>(j.pieces), j.info, j.W, L, j.J, j.E, blockIdx.x,
+               gridDim.x);
+}
+
+__global__ __launch_bounds__(64) void k_fsm_replay_batch(const Job* __restrict__ jobs, int L) {
+    const Job j = jobs[blockIdx.y];
+    if (j.W <= 0) return;
+    fsm_replay(j.R, j.Tsub, reinterpret_cast<const ChunkStart*>(j.pieces), j.info, j.W, L, j.J, j.E, blockIdx.x,
+               gridDim.x);
+}
+
 // One lane per batch: Fisher-Yates swaps i = L-1..1 with the recorded j's.
-__global__ __launch_bounds__(256) void k_fsm_perms(const uint8_t* __restrict__ J, int64_t W, int L,
-                                                   uint8_t* __restrict__ perm) {
+__device__ void fsm_perms(const uint8_t* __restrict__ J, int64_t W, int L, uint8_t* __restrict__ perm, int64_t b0) {
     extern __shared__ uint8_t buf[];
-    const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t b = b0 + threadIdx.x;
     if (b >= W) return;
     uint8_t* p = buf + threadIdx.x * L;
     for (int k = 0; k < L; ++k) p[k] = (uint8_t)k;
@@ -309,12 +390,91 @@ __global__ __launch_bounds__(256) void k_fsm_perms(const uint8_t* __restrict__ J
     for (int k = 0; k < L; ++k) perm[b * L + k] = p[k];
 }
 
+__global__ __launch_bounds__(256) void k_fsm_perms(Job j, int L) {
+    fsm_perms(j.J, j.W, L, j.perm_out, (int64_t)blockIdx.x * 256);
+}
+
+__global__ __launch_bounds__(256) void k_fsm_perms_batch(const Job* __restrict__ jobs, int L) {
+    const Job j = jobs[blockIdx.y];
+    for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < j.W; b0 += (int64_t)gridDim.x * 256)
+        fsm_perms(j.J, j.W, L, j.perm_out, b0);
+}
+
 __global__ void k_pick(const int32_t* stop, const int64_t* E, int64_t W, int64_t offset, int64_t last, int64_t* out) {
     const int64_t k = (stop[0] >= 0 ? (int64_t)stop[0] : last) - offset;
     out[0] = (k >= 0 && k < W) ? E[k] : -1;
 }
 
+__global__ void k_pick_batch(const Job* __restrict__ jobs, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Job j = jobs[i];
+    if (!j.pick_out) return;
+    const int64_t k = (j.stop && j.stop[0] >= 0 ? (int64_t)j.stop[0] : j.pick_last) - j.pick_offset;
+    j.pick_out[0] = (j.W > 0 && k >= 0 && k < j.W) ? j.E[k] : -1;
+}
+
+size_t walk_lds_bytes(int L) {
+    return std::max((size_t)64 * (L - 1) * sizeof(uint32_t),
+                    kSub * sizeof(uint32_t) + (size_t)kSubPerChunk * (L - 1) * sizeof(uint16_t));
+}
+
+size_t replay_lds_bytes(int L) { return kChunk * sizeof(uint32_t) + (size_t)kSubPerChunk * (L - 1) * sizeof(uint16_t); }
+
 }  // namespace
+
+static_assert(sizeof(Job) == sizeof(ddm_shuffle_job), "ddm_shuffle_job layout");
+static_assert(sizeof(GenJob) == sizeof(ddm_gen_job), "ddm_gen_job layout");
+
+extern "C" int ddm_shuffle_generate_batch(const ddm_gen_job* jobs_dev, int32_t n_jobs, ddm_stream_t stream) {
+    if (!jobs_dev || n_jobs < 0) {
+        ddm::set_error("ddm_shuffle_generate_batch: invalid argument");
+        return DDM_E_ARG;
+    }
+    if (n_jobs == 0) return 0;
+    hipLaunchKernelGGL(k_mt_generate_batch, dim3((unsigned)n_jobs), dim3(256), 0, ddm::as_hip(stream),
+                       reinterpret_cast<const GenJob*>(jobs_dev));
+    return ddm::launch_status("ddm_shuffle_generate_batch");
+}
+
+extern "C" int ddm_shuffle_window_batch(const ddm_shuffle_job* jobs_dev, int32_t n_jobs, int64_t max_W,
+                                        int64_t max_pieces, int32_t batch_len, ddm_stream_t stream,
+                                        ddm_event_t ev_begin, ddm_event_t ev_end) {
+    if (!jobs_dev || n_jobs < 0 || max_W < 0 || batch_len < 2 || batch_len > 256) {
+        ddm::set_error("ddm_shuffle_window_batch: invalid argument");
+        return DDM_E_ARG;
+    }
+    if (n_jobs == 0 || max_W == 0) return 0;
+    hipStream_t s = ddm::as_hip(stream);
+    const Job* jobs = reinterpret_cast<const Job*>(jobs_dev);
+    if (ev_begin)
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
+    hipLaunchKernelGGL(k_fsm_walk_batch, dim3((unsigned)n_jobs), dim3(64), walk_lds_bytes(batch_len), s, jobs,
+                       (int)batch_len);
+    if (int rc = ddm::launch_status("ddm_shuffle_window_batch/walk")) return rc;
+    const int64_t pblocks = std::max<int64_t>(1, std::min<int64_t>(max_pieces, 2048));
+    hipLaunchKernelGGL(k_fsm_replay_batch, dim3((unsigned)pblocks, (unsigned)n_jobs), dim3(64),
+                       replay_lds_bytes(batch_len), s, jobs, (int)batch_len);
+    if (int rc = ddm::launch_status("ddm_shuffle_window_batch/replay")) return rc;
+    const int64_t bblocks = std::min<int64_t>(ddm::ceil_div(max_W, 256), 1024);
+    hipLaunchKernelGGL(k_fsm_perms_batch, dim3((unsigned)bblocks, (unsigned)n_jobs), dim3(256),
+                       (size_t)256 * batch_len, s, jobs, (int)batch_len);
+    if (int rc = ddm::launch_status("ddm_shuffle_window_batch/perms")) return rc;
+    if (ev_end)
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
+    return 0;
+}
+
+extern "C" int ddm_shuffle_pick_batch(const ddm_shuffle_job* jobs_dev, int32_t n_jobs, ddm_stream_t stream) {
+    if (!jobs_dev || n_jobs < 0) {
+        ddm::set_error("ddm_shuffle_pick_batch: invalid argument");
+        return DDM_E_ARG;
+    }
+    if (n_jobs == 0) return 0;
+    hipLaunchKernelGGL(k_pick_batch, dim3((unsigned)ddm::ceil_div(n_jobs, 64)), dim3(64), 0, ddm::as_hip(stream),
+                       reinterpret_cast<const Job*>(jobs_dev), (int)n_jobs);
+    return ddm::launch_status("ddm_shuffle_pick_batch");
+}
 
 extern "C" int ddm_shuffle_pick(const int32_t* stop, const int64_t* E, int64_t W, int64_t offset, int64_t last,
                                 int64_t* out, ddm_stream_t stream) {
@@ -363,20 +523,17 @@ extern "C" int ddm_shuffle_window(const uint32_t* R, const uint16_t* Tsub, const
         return DDM_E_ARG;
     }
     hipStream_t s = ddm::as_hip(stream);
-    ChunkStart* pc = reinterpret_cast<ChunkStart*>(pieces);
+    Job j{R, Tsub, Tchunk, avail, P, W, pieces, info, J, E, perm_out, nullptr, 0, 0, nullptr};
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
-    const size_t walk_lds = (size_t)64 * (batch_len - 1) * sizeof(uint32_t);
-    hipLaunchKernelGGL(k_fsm_walk, dim3(1), dim3(64), walk_lds, s, R, Tsub, Tchunk, P, W, (int)batch_len, avail, pc,
-                       info);
+    hipLaunchKernelGGL(k_fsm_walk, dim3(1), dim3(64), walk_lds_bytes(batch_len), s, j, (int)batch_len);
     if (int rc = ddm::launch_status("ddm_shuffle_window/walk")) return rc;
     const int64_t blocks = std::min<int64_t>(max_pieces, 8192);
-    const size_t rep_lds = (size_t)kSubPerChunk * (batch_len - 1) * sizeof(uint16_t);
-    hipLaunchKernelGGL(k_fsm_replay, dim3((unsigned)blocks), dim3(64), rep_lds, s, R, Tsub, pc, info, W, (int)batch_len,
-                       J, E);
+    hipLaunchKernelGGL(k_fsm_replay, dim3((unsigned)blocks), dim3(64), replay_lds_bytes(batch_len), s, j,
+                       (int)batch_len);
     if (int rc = ddm::launch_status("ddm_shuffle_window/replay")) return rc;
-    hipLaunchKernelGGL(k_fsm_perms, dim3((unsigned)ddm::ceil_div(W, 256)), dim3(256), (size_t)256 * batch_len, s, J, W,
-                       (int)batch_len, perm_out);
+    hipLaunchKernelGGL(k_fsm_perms, dim3((unsigned)ddm::ceil_div(W, 256)), dim3(256), (size_t)256 * batch_len, s, j,
+                       (int)batch_len);
     if (int rc = ddm::launch_status("ddm_shuffle_window/perms")) return rc;
     if (ev_end)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;

@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
@@ -49,7 +49,11 @@ SIGNATURES = {
     "ddm_forest_predict": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _i64, _i64, _i32, ctypes.POINTER(DdmForest),
                                           _vp, _vp, _vp, _vp, _vp, _vp]),
     "ddm_scan_streams": (ctypes.c_int, [_vp, _vp, _i64, ctypes.POINTER(DdmParams), _vp, _vp, _vp, _i64, _vp, _vp,
-                                        _vp, _i32, _vp, _vp, _vp, _vp, _vp]),
+                                        _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "ddm_forest_predict_batch": (ctypes.c_int, [_vp, _vp, _i32, _i32, _vp, _vp, _vp]),
+    "ddm_shuffle_generate_batch": (ctypes.c_int, [_vp, _i32, _vp]),
+    "ddm_shuffle_window_batch": (ctypes.c_int, [_vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp]),
+    "ddm_shuffle_pick_batch": (ctypes.c_int, [_vp, _i32, _vp]),
     "ddm_shuffle_generate": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
     "ddm_shuffle_tables": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp]),
     "ddm_shuffle_window": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp,

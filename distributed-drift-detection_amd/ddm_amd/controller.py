@@ -207,6 +207,9 @@ class PartitionRunner:
 
         sh = self.shuffle
         sh.reset(rng)
+        # the whole partition's stream up front (one generate + table pass); windows
+        # extend it if drifts (100 seed draws each) push it further
+        sh.ensure(int(nb * expected_draws_per_batch(pb) * 1.02))
         stream = self.stream
         base = self.ctrl_d.data_ptr()
         try:

@@ -79,16 +79,17 @@ def scan_streams(err, offsets, params, state, batch_base, n_batches_total, ev, f
     state: uint8 tensor holding n_streams ddm_state records; ev int32 [n_batches_total, 2]."""
     check(lib.ddm_scan_streams(err.data_ptr(), _ptr(offsets), offsets.numel() - 1, ctypes.byref(params),
                                _ptr(state), _ptr(first_nz), _ptr(batch_base), int(n_batches_total), _ptr(ev),
-                               _ptr(stop), _ptr(nev), int(mode), _ptr(ps), _ptr(perm_map), _stream(err, stream),
-                               *_evs(timer)), "ddm_scan_streams")
+                               _ptr(stop), _ptr(nev), int(mode), _ptr(ps), _ptr(perm_map), None,
+                               _stream(err, stream), *_evs(timer)), "ddm_scan_streams")
 
 
 def scan_streams_raw(err_ptr, offsets_ptr, n_streams, params, state_ptr, batch_base_ptr, n_batches_total, ev_ptr,
-                     first_nz_ptr, stop_ptr, nev_ptr, mode, ps_ptr, stream, timer=None, perm_map_ptr=None):
+                     first_nz_ptr, stop_ptr, nev_ptr, mode, ps_ptr, stream, timer=None, perm_map_ptr=None,
+                     end_ptr=None):
     """Pointer-level variant used by the controller (all pointers are device addresses)."""
     check(lib.ddm_scan_streams(err_ptr, offsets_ptr, n_streams, ctypes.byref(params), state_ptr, first_nz_ptr,
                                batch_base_ptr, n_batches_total, ev_ptr, stop_ptr, nev_ptr, mode, ps_ptr, perm_map_ptr,
-                               ctypes.c_void_p(stream.cuda_stream), *_evs(timer)), "ddm_scan_streams")
+                               end_ptr, ctypes.c_void_p(stream.cuda_stream), *_evs(timer)), "ddm_scan_streams")
 
 
 def synth_block_labels(y, part, n_parts, block_rows, n_classes, stream=None):

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 3
+#define DDM_AMD_ABI_VERSION 4
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -107,6 +107,24 @@ int ddm_forest_predict(const float* X, int64_t ld, int32_t n_features, const int
                        uint64_t* first_err, int32_t* pred_out, ddm_stream_t stream,
                        ddm_event_t ev_begin, ddm_event_t ev_end);
 
+/* Batched predict: one segment per partition window (the same work as one
+ * ddm_forest_predict call each), all in one launch per kernel variant.  segs_host must
+ * stay valid (e.g. pinned) until the stream has consumed the table copy; block0/nblocks
+ * are filled in by the call; segs_dev (device) receives the table.  first_err of every
+ * segment (if non-NULL) is reset by the call. */
+typedef struct ddm_predict_segment {
+    const float* X; int64_t ld; const int32_t* y; const uint8_t* perm; uint8_t* err;
+    int32_t* pred; uint64_t* first_err; int64_t pos_begin, pos_end;
+    const ddm_node* nodes; const int32_t* roots; const double* leaf_value; const int32_t* classes;
+    int32_t n_trees, n_classes, n_nodes, pure;
+    int64_t row_base;       /* row = (g / per_batch) * per_batch + perm[g] - row_base (g: position) */
+    int64_t block0, nblocks;
+} ddm_predict_segment;
+
+int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, ddm_predict_segment* segs_dev,
+                             int32_t n_segs, int32_t per_batch, ddm_stream_t stream,
+                             ddm_event_t ev_begin, ddm_event_t ev_end);
+
 /* run_DDM over every batch of every stream.  Stream s is err[stream_off[s] ..
  * stream_off[s+1]) (device int64 offsets; err readable up to the next multiple of 16
  * bytes past the last offset), cut into batches of per_batch rows (last one short).
@@ -121,6 +139,8 @@ int ddm_forest_predict(const float* X, int64_t ld, int32_t n_features, const int
  * stop_out (device int32, may be NULL): batch of the first change or -1 (mode 0).
  * nev_out (device int64, may be NULL): number of batches with an event per stream.
  * ps_out (device double [rows][2], may be NULL): p and s after each processed row.
+ * stream_end (device int64, may be NULL): when given, stream s is [stream_off[s],
+ * stream_end[s]) (streams need not be adjacent), else [stream_off[s], stream_off[s+1]).
  * perm_map (device uint8, may be NULL): when given, events are reported as the ROW
  * offset inside the batch, perm_map[batch start + position] (the label the reference
  * records at DDM_Process.py:148,151), instead of the DDM position.
@@ -129,8 +149,8 @@ int ddm_scan_streams(const uint8_t* err, const int64_t* stream_off, int64_t n_st
                      const ddm_params* prm, ddm_state* state_io, const uint64_t* first_nz,
                      const int64_t* batch_base, int64_t n_batches_total, int32_t* ev_out,
                      int32_t* stop_out, int64_t* nev_out, int32_t mode, double* ps_out,
-                     const uint8_t* perm_map, ddm_stream_t stream, ddm_event_t ev_begin,
-                     ddm_event_t ev_end);
+                     const uint8_t* perm_map, const int64_t* stream_end, ddm_stream_t stream,
+                     ddm_event_t ev_begin, ddm_event_t ev_end);
 
 /* Timing events for the ev_begin / ev_end arguments (hipEventCreate / Destroy /
  * ElapsedTime; elapsed needs both events completed, e.g. after a stream sync). */
@@ -179,6 +199,23 @@ int ddm_shuffle_window(const uint32_t* R, const uint16_t* Tsub, const uint32_t* 
                        int64_t P, int64_t W, int32_t batch_len, void* pieces, int64_t max_pieces,
                        int64_t* info, uint8_t* J, int64_t* E, uint8_t* perm_out, ddm_stream_t stream,
                        ddm_event_t ev_begin, ddm_event_t ev_end);
+
+/* Batched forms (one job per partition, device array of jobs; W = 0 skips a job). */
+typedef struct ddm_gen_job { uint32_t* mt_state; uint32_t* R; int64_t n; } ddm_gen_job;
+typedef struct ddm_shuffle_job {
+    const uint32_t* R; const uint16_t* Tsub; const uint32_t* Tchunk;
+    int64_t avail, P, W;
+    void* pieces; int64_t* info; uint8_t* J; int64_t* E; uint8_t* perm_out;
+    const int32_t* stop;            /* ddm_shuffle_pick_batch: scan stop flag (may be NULL) */
+    int64_t pick_offset, pick_last; /* pick E[(stop >= 0 ? stop : pick_last) - pick_offset] */
+    int64_t* pick_out;              /* may be NULL: no pick for this job                   */
+} ddm_shuffle_job;
+
+int ddm_shuffle_generate_batch(const ddm_gen_job* jobs_dev, int32_t n_jobs, ddm_stream_t stream);
+int ddm_shuffle_window_batch(const ddm_shuffle_job* jobs_dev, int32_t n_jobs, int64_t max_W,
+                             int64_t max_pieces, int32_t batch_len, ddm_stream_t stream,
+                             ddm_event_t ev_begin, ddm_event_t ev_end);
+int ddm_shuffle_pick_batch(const ddm_shuffle_job* jobs_dev, int32_t n_jobs, ddm_stream_t stream);
 
 /* out[0] = E[k] with k = (stop[0] >= 0 ? stop[0] : last) - offset if 0 <= k < W, else -1
  * (device scalars; lets the controller read the RNG position with the control block). */

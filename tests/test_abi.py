@@ -45,6 +45,6 @@ def test_invalid_args_report_errors():
     rc = _capi.lib.ddm_mt_perms(None, None, None, 0, None, None)
     assert rc == _capi.DDM_E_ARG
     rc = _capi.lib.ddm_scan_streams(None, None, 1, None, None, None, None, 0, None, None, None, 0, None, None,
-                                    None, None, None)
+                                    None, None, None, None)
     assert rc == _capi.DDM_E_ARG
     assert b"invalid argument" in _capi.lib.ddm_last_error()
