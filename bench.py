@@ -19,7 +19,6 @@ import argparse
 import json
 import os
 import sys
-import threading
 import time
 
 # one HIP stream per partition: give HIP enough hardware queues to run them concurrently
@@ -45,6 +44,7 @@ def parse():
     ap.add_argument("--features", type=int, default=27)
     ap.add_argument("--refit", default="native", choices=["native", "sklearn"],
                     help="native: ddm_rf_fit (identical trees to sklearn 1.7.2); sklearn: host sklearn")
+    ap.add_argument("--fit-threads", type=int, default=8, help="host threads for parallel native refits")
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-sample-rows", type=int, default=150_000)
@@ -97,13 +97,13 @@ def cpu_baseline_c3(part, n_rows, seed):
 def run_c3(args, world, rank, dev, torch, dist):
     import numpy as np
     from ddm_amd import kernels
-    from ddm_amd.controller import DevicePartition, PartitionRunner
+    from ddm_amd.controller import BatchRunner, DevicePartition
     from ddm_amd.params import DDMSettings
     from ddm_amd.rng import MTStream
     instances = args.parts * world
     block = args.block_rows if world == 1 else (args.block_rows // 8) * instances + 37
     n = args.rows_per_part
-    parts, runners = [], []
+    parts = []
     settings = DDMSettings()
     for p in range(args.parts):
         gid = rank * args.parts + p
@@ -111,30 +111,23 @@ def run_c3(args, world, rank, dev, torch, dist):
         kernels.synth_block_labels(part.y[:n], gid, instances, block, 10)
         kernels.synth_features(part.X, part.y[:n], gid, instances, args.seed, 0.04)
         parts.append((gid, part))
-        runners.append(PartitionRunner(part, settings, torch.cuda.Stream(dev), refit=args.refit, timing=True))
+    # all partitions of this GPU in lockstep: one batched launch per kernel per epoch
+    runner = BatchRunner([p for _, p in parts], settings, torch.cuda.Stream(dev), refit=args.refit, timing=True,
+                         fit_threads=args.fit_threads)
     torch.cuda.synchronize()
 
     results = {}
 
-    def one(i):
-        gid, _ = parts[i]
-        results[gid] = runners[i].run(MTStream.from_seed(args.seed + gid))
-
     def step():
-        ths = [threading.Thread(target=one, args=(i,)) for i in range(len(parts))]
-        for t in ths:
-            t.start()
-        for t in ths:
-            t.join()
-        if len(results) != len(parts):
-            raise RuntimeError("a partition runner failed")
+        outs = runner.run([MTStream.from_seed(args.seed + gid) for gid, _ in parts])
+        for (gid, _), o in zip(parts, outs):
+            results[gid] = o
 
     for _ in range(args.warmup):
         step()
     ref_events = {g: r.copy() for g, r in results.items()}
     from ddm_amd.controller import RunStats
-    for r in runners:
-        r.stats = RunStats()
+    runner.stats = RunStats()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -149,10 +142,10 @@ def run_c3(args, world, rank, dev, torch, dist):
     for g, r in results.items():          # every step reproduces the same events
         if args.warmup and not np.array_equal(r, ref_events[g]):
             raise RuntimeError(f"partition {g}: events differ between steps")
-    st = [r.stats for r in runners]
+    st = [runner.stats]
     agg = {k: sum(getattr(s, k) for s in st) for k in ("epochs", "refits", "predicted_rows", "refit_s",
                                                         "predict_ms", "predict_bytes", "scan_ms", "scan_rows",
-                                                        "shuffle_ms")}
+                                                        "shuffle_ms", "host_s", "gpu_s")}
     drifts = int(sum((r[:, 1] >= 0).sum() for r in results.values()))
     warns = int(sum((r[:, 0] >= 0).sum() for r in results.values()))
     rows_rank = n * args.parts * args.steps
@@ -169,9 +162,11 @@ def run_c3(args, world, rank, dev, torch, dist):
                     f"{args.parts} partitions x {n} rows per GPU",
         "rows_per_gpu_step": n * args.parts, "partitions_per_gpu": args.parts,
         "refit": ("native ddm_rf_fit (sklearn 1.7.2 RandomForestClassifier restated, identical trees), "
-                  "one host thread per partition") if args.refit == "native" else
+                  "refits of different partitions in parallel host threads") if args.refit == "native" else
                  "host sklearn RandomForestClassifier(100 trees), in-process",
         "shuffle": "batch shuffles generated on the GPU from the partition's MT19937 stream (ddm_shuffle_*)",
+        "execution": "all partitions of the GPU in lockstep epochs: one batched shuffle, predict and scan "
+                     "launch per epoch (BatchRunner)",
     }
     extra = {"drifts_per_step": drifts, "warnings_per_step": warns,
              "refits_per_step": agg["refits"] / args.steps, "epochs_per_step": agg["epochs"] / args.steps,
@@ -179,7 +174,8 @@ def run_c3(args, world, rank, dev, torch, dist):
              "refit_s_per_step_sum": agg["refit_s"] / args.steps,
              "predict_kernel_ms_per_step": agg["predict_ms"] / args.steps,
              "scan_kernel_ms_per_step": agg["scan_ms"] / args.steps,
-             "shuffle_kernels_ms_per_step": agg["shuffle_ms"] / args.steps}
+             "shuffle_kernels_ms_per_step": agg["shuffle_ms"] / args.steps,
+             "host_s_per_step": agg["host_s"] / args.steps, "gpu_wait_s_per_step": agg["gpu_s"] / args.steps}
     roofline = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_from_profile("ddm_forest_predict", rows_per_launch),
                 "kernel": "ddm_forest_predict", "alg_bytes_per_row": "4*F_used + 6",

@@ -57,6 +57,7 @@ struct Seg {
     int64_t row_base;            // rows are (g / per_batch) * per_batch + perm[g] - row_base
     int64_t block0, nblocks;     // this segment's blocks in the launch grid
 };
+static_assert(sizeof(Seg) == sizeof(ddm_predict_segment) && sizeof(Seg) == 144, "Seg must mirror ddm_predict_segment");
 
 template <bool kPure, int kK, bool kLdsForest>
 __device__ __forceinline__ void predict_segment(const Seg& sg, int64_t blk, int64_t nblk, int64_t per_batch,

@@ -34,10 +34,6 @@ from .rng import MTStream
 from .shuffle import GpuShuffle, expected_draws_per_batch
 from .trainer import NativeForestTrainer
 
-# control block layout (bytes) shared by host (pinned) and device
-_FIRST_ERR, _NEV, _STOP, _OFF, _BASE, _PICK, _STATE, _CTRL_BYTES = 0, 8, 16, 24, 40, 48, 64, 128
-
-
 def _round_up(n, m):
     return (n + m - 1) // m * m
 
@@ -115,218 +111,400 @@ class RunStats:
         return {k: getattr(self, k) for k in self.__slots__}
 
 
-class PartitionRunner:
-    """Runs the speculative shuffle+predict+scan epochs of one partition on one HIP stream.
+class _Part:
+    """Host-side epoch state of one partition in a BatchRunner."""
+    __slots__ = ("i", "nb", "last_len", "n_full", "max_win", "base", "ev_base", "j", "P", "retrain", "train_rows",
+                 "state", "win", "forest", "out", "done", "P_after_first", "g0", "b_end", "Wg", "tail",
+                 "P_tail_after", "seg_start", "pb")
+
+    def blen(self, b):
+        return self.last_len if b == self.nb - 1 else self.pb
+
+
+class BatchRunner:
+    """Runs the speculative shuffle+predict+scan epochs of many partitions in lockstep on
+    one HIP stream: each epoch is ONE batched shuffle launch (csrc/shuffle.hip job table),
+    ONE batched forest-predict launch per kernel variant (segment table), ONE scan launch
+    (a lane per partition) and ONE control-block read-back, whatever the partition count.
+    Partitions are independent (DDM_Process.py:226 groups by device_id), so a partition
+    that is done simply drops out of the tables.
 
     refit: "native" (ddm_rf_fit, identical trees to sklearn 1.7.2; sklearn itself for NaN
-    inputs) or "sklearn"."""
+    inputs) or "sklearn".  Refits of different partitions run in parallel threads (the
+    native fit releases the GIL)."""
 
-    def __init__(self, part, settings=None, stream=None, refit="native", timing=False):
-        self.part = part
+    def __init__(self, parts, settings=None, stream=None, refit="native", timing=False, fit_threads=8):
+        self.parts = list(parts)
+        if not self.parts:
+            raise ValueError("no partitions")
+        dev = self.parts[0].device
+        if any(p.device != dev for p in self.parts):
+            raise ValueError("a BatchRunner drives the partitions of one device")
+        self.device = dev
         self.s = settings or DDMSettings()
-        self.stream = stream or torch.cuda.Stream(part.device)
+        self.stream = stream or torch.cuda.Stream(dev)
         self.refit_kind = refit
-        self.trainer = NativeForestTrainer(self.s.n_estimators)
+        self.fit_threads = max(1, int(fit_threads))
+        pb = self.s.per_batch
+        if not 2 <= pb <= 256:
+            raise ValueError("per_batch must be in [2, 256] on the device path")
+        self.trainers = [NativeForestTrainer(self.s.n_estimators) for _ in self.parts]
         self.sk_refit = sklearn_refit(self.s)
         self.timing = timing
-        # HIP events recorded by the C-ABI right around each launch on this runner's stream
+        # HIP events recorded by the C-ABI right around each batched launch
         self.t_pred = kernels.LaunchTimer() if timing else None
         self.t_scan = kernels.LaunchTimer() if timing else None
         self.t_shuf = kernels.LaunchTimer() if timing else None
-        self.params = kernels.params_struct(self.s.min_num_instances, self.s.per_batch, self.s.warning_level,
+        self.params = kernels.params_struct(self.s.min_num_instances, pb, self.s.warning_level,
                                             self.s.out_control_level)
-        n, dev, pb = part.n, part.device, self.s.per_batch
-        if not 2 <= pb <= 256:
-            raise ValueError("per_batch must be in [2, 256] on the device path")
-        self.perm_d = torch.zeros(max(n, 1) + 256, dtype=torch.uint8, device=dev)
-        self.err_d = torch.zeros(_round_up(max(n, 1), 16) + 16, dtype=torch.uint8, device=dev)
-        self.ctrl_h = torch.zeros(_CTRL_BYTES, dtype=torch.uint8, pin_memory=True)
-        self.ctrl_np = self.ctrl_h.numpy()
-        self.ctrl_d = torch.zeros(_CTRL_BYTES, dtype=torch.uint8, device=dev)
-        # pinned staging: [0] batch-j shuffle of a refit epoch, [1] short last batch, [2] D2H
-        self.small_h = [torch.empty(256, dtype=torch.uint8, pin_memory=True) for _ in range(3)]
-        self.neg1_d = torch.full((1,), -1, dtype=torch.int32, device=dev)
-        nb = (n + pb - 1) // pb
-        self.max_win = max(1, min(self.s.max_window_batches, nb))
-        self.ev_d = torch.empty((self.max_win, 2), dtype=torch.int32, device=dev)
-        self.ev_h = torch.empty((self.max_win, 2), dtype=torch.int32, pin_memory=True)
-        cap = int(nb * expected_draws_per_batch(pb) * 1.2) + 64 * 1024
-        self.shuffle = GpuShuffle(dev, pb, cap, self.max_win, self.stream)
+        n = len(self.parts)
+        # partition p's DDM positions live at [base_p, base_p + n_p) of the shared perm/err
+        # buffers (base_p a multiple of 16*pb, so batches and 16-byte scan chunks align)
+        align = 16 * pb
+        self.bases, self.ev_bases, self.max_wins, self.nbs = [], [], [], []
+        pos = evp = 0
+        for part in self.parts:
+            nb = (part.n + pb - 1) // pb
+            mw = max(1, min(self.s.max_window_batches, nb))
+            self.bases.append(pos)
+            self.ev_bases.append(evp)
+            self.max_wins.append(mw)
+            self.nbs.append(nb)
+            pos = _round_up(pos + part.n, align) + align
+            evp += mw
+        self.perm_all = torch.zeros(pos + 256, dtype=torch.uint8, device=dev)
+        self.err_all = torch.zeros(pos + 32, dtype=torch.uint8, device=dev)
+        self.ev_total = evp
+        self.ev_d = torch.empty((evp, 2), dtype=torch.int32, device=dev)
+        self.ev_h = torch.empty((evp, 2), dtype=torch.int32, pin_memory=True)
+        # control block, struct-of-arrays over partitions: outputs first, then inputs
+        k = _round_up(n, 2)
+        self.o_first, self.o_nev, self.o_stop, self.o_pick = 0, 8 * k, 16 * k, 20 * k
+        self.o_off, self.o_end, self.o_bbase, self.o_state = 28 * k, 36 * k, 44 * k, 52 * k
+        self.ctrl_bytes = _round_up(self.o_state + 56 * k, 64)
+        self.ctrl_h = torch.zeros(self.ctrl_bytes, dtype=torch.uint8, pin_memory=True)
+        self.ctrl_d = torch.zeros(self.ctrl_bytes, dtype=torch.uint8, device=dev)
+        c = self.ctrl_h.numpy()
+        self.first_h = c[self.o_first:self.o_first + 8 * n].view(np.int64)
+        self.nev_h = c[self.o_nev:self.o_nev + 8 * n].view(np.int64)
+        self.stop_h = c[self.o_stop:self.o_stop + 4 * n].view(np.int32)
+        self.pick_h = c[self.o_pick:self.o_pick + 8 * n].view(np.int64)
+        self.off_h = c[self.o_off:self.o_off + 8 * n].view(np.int64)
+        self.end_h = c[self.o_end:self.o_end + 8 * n].view(np.int64)
+        self.bbase_h = c[self.o_bbase:self.o_bbase + 8 * n].view(np.int64)
+        self.state_h = c[self.o_state:self.o_state + 56 * n].view(kernels.STATE_DTYPE)
+        self.bbase_h[:] = self.ev_bases
+        self.segs = kernels.PinnedTable(kernels.SEG_DTYPE, n, dev)
+        self.jobs = kernels.PinnedTable(kernels.JOB_DTYPE, n, dev)
+        self.gens = kernels.PinnedTable(kernels.GEN_DTYPE, n, dev)
+        # pinned staging per partition: [0] batch-j shuffle of a refit epoch, [1] short last
+        # batch, [2] drift batch's shuffle read back
+        self.small_h = [[torch.empty(256, dtype=torch.uint8, pin_memory=True) for _ in range(3)] for _ in self.parts]
+        self.shuffles = []
+        for part, nb, mw in zip(self.parts, self.nbs, self.max_wins):
+            cap = int(nb * expected_draws_per_batch(pb) * 1.2) + 64 * 1024
+            self.shuffles.append(GpuShuffle(dev, pb, cap, mw, self.stream))
         self.stats = RunStats()
 
-    # -- host views of the control block
-    def _ctrl(self, off, dtype, count=1):
-        return self.ctrl_np[off:off + np.dtype(dtype).itemsize * count].view(dtype)
+    # -- helpers
+    def _dptr(self, off, i, size):
+        return self.ctrl_d.data_ptr() + off + size * i
 
-    def _fit(self, rows, P_seeds):
-        """Refit on the rows of the drift batch (shuffled order); returns (forest, draws used)."""
-        X32, y = self.part.rows(rows, self.stream)
-        sh = self.shuffle
-        t0 = time.perf_counter()
-        seeds, P_after = sh.host_seeds(P_seeds, self.s.n_estimators)
+    def _ensure_all(self, wants):
+        """wants: [(partition index, draws needed)] -> one batched generate launch + tables."""
+        reqs, tabs = [], []
+        for i, upto in wants:
+            req, need = self.shuffles[i].gen_request(upto)
+            if req is not None:
+                reqs.append(req)
+            tabs.append((i, need))
+        if reqs:
+            rec = self.gens.rec
+            for k, (st, R, cnt) in enumerate(reqs):
+                rec[k] = (st, R, cnt)
+            kernels.shuffle_generate_batch(self.gens, len(reqs), self.stream)
+        for i, need in tabs:
+            self.shuffles[i].tables_to(need)
+
+    def _upload_perm(self, i, b, perm, slot):
+        pb = self.s.per_batch
+        h = self.small_h[i][slot]
+        h[:len(perm)].copy_(torch.from_numpy(perm))
+        at = self.bases[i] + b * pb
+        with torch.cuda.stream(self.stream):
+            self.perm_all[at:at + len(perm)].copy_(h[:len(perm)], non_blocking=True)
+
+    def _fit_one(self, i, X32, y, seeds, P_seeds):
         packed = None
         if self.refit_kind == "native":
-            packed = self.trainer.fit(X32, y, seeds)
+            packed = self.trainers[i].fit(X32, y, seeds)
         if packed is None:                    # sklearn requested, or NaN in X (missing values)
-            packed = self.sk_refit(X32, y, sh.numpy_state(P_seeds))
-            self.stats.sklearn_refits += 1
-        self.stats.refit_s += time.perf_counter() - t0
-        self.stats.refits += 1
-        return DeviceForest(packed, self.part.device), P_after
+            packed = self.sk_refit(X32, y, self.shuffles[i].numpy_state(P_seeds))
+            return packed, True
+        return packed, False
 
-    def _upload_perm(self, b, perm, slot):
-        pb = self.s.per_batch
-        h = self.small_h[slot]
-        h[:len(perm)].copy_(torch.from_numpy(perm))
-        with torch.cuda.stream(self.stream):
-            self.perm_d[b * pb:b * pb + len(perm)].copy_(h[:len(perm)], non_blocking=True)
+    def _refits(self, need):
+        """Refit every partition in `need` on its drift batch (train_rows, shuffled order)."""
+        st, T = self.stats, self.s.n_estimators
+        t0 = time.perf_counter()
+        work = []
+        for ps in need:
+            sh = self.shuffles[ps.i]
+            permj, ps.P = sh.host_perm(ps.P, ps.blen(ps.j))     # batch_b.sample before the fit (:190, :194)
+            self._upload_perm(ps.i, ps.j, permj, 0)
+            P_seeds = ps.P
+            seeds, ps.P = sh.host_seeds(P_seeds, T)              # 100 tree seeds follow the shuffle
+            ps.P_after_first = ps.P
+            X32, y = self.parts[ps.i].rows(ps.train_rows, self.stream)
+            work.append((ps, X32, y, seeds, P_seeds))
+        if self.refit_kind == "native" and len(work) > 1 and self.fit_threads > 1:
+            pool = self._pool()
+            res = list(pool.map(lambda w: self._fit_one(w[0].i, *w[1:]), work))
+        else:
+            res = [self._fit_one(w[0].i, *w[1:]) for w in work]
+        for (ps, *_), (packed, used_sk) in zip(work, res):
+            ps.forest = DeviceForest(packed, self.device)
+            ps.retrain = False
+            ps.state = kernels.fresh_states(1)                  # ddm = None -> new DDM (:136-139)
+            ps.g0 = ps.j + 1
+            ps.seg_start = ps.j
+            st.sklearn_refits += int(used_sk)
+        st.refits += len(work)
+        st.refit_s += time.perf_counter() - t0
 
-    def _perm_rows(self, b, length):
-        """Rows of batch b in its shuffled order (D2H of the batch's perm bytes)."""
-        pb = self.s.per_batch
-        h = self.small_h[2]
-        with torch.cuda.stream(self.stream):
-            h[:length].copy_(self.perm_d[b * pb:b * pb + length], non_blocking=True)
-        self.stream.synchronize()
-        return b * pb + h[:length].numpy().astype(np.int64)
+    def _pool(self):
+        if getattr(self, "_executor", None) is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._executor = ThreadPoolExecutor(self.fit_threads)
+        return self._executor
+
+    def close(self):
+        ex = getattr(self, "_executor", None)
+        if ex is not None:
+            ex.shutdown(wait=True)
+            self._executor = None
+
+    def _jobs_for(self, live, with_stop):
+        """Fill the job table for partitions with device shuffles this epoch."""
+        rec = self.jobs.rec
+        for k, ps in enumerate(live):
+            pb = self.s.per_batch
+            out_ptr = self.perm_all.data_ptr() + self.bases[ps.i] + ps.g0 * pb
+            if with_stop:
+                self.shuffles[ps.i].fill_job(rec[k], ps.P, ps.Wg, out_ptr, self._dptr(self.o_stop, ps.i, 4),
+                                             ps.g0 - ps.j, ps.b_end - 1 - ps.j, self._dptr(self.o_pick, ps.i, 8))
+            else:                                # end of the window's GPU batches (tail epochs)
+                self.shuffles[ps.i].fill_job(rec[k], ps.P, ps.Wg, out_ptr, 0, 0, ps.Wg - 1,
+                                             self._dptr(self.o_pick, ps.i, 8))
+        self.jobs.upload(len(live), self.stream)
+
+    def run(self, rngs):
+        """Returns, per partition, int64 [n_batches-1, 2]: partition rows of (first warning,
+        change) per batch 1.. (-1 = none).  Consumes each `rngs[p]` (an MTStream, advanced
+        in place) exactly as the reference consumes np.random in that partition's worker."""
+        s, st, pb = self.s, self.stats, self.s.per_batch
+        if len(rngs) != len(self.parts):
+            raise ValueError("one MT19937 stream per partition")
+        pss = []
+        for i, part in enumerate(self.parts):
+            ps = _Part()
+            ps.pb = pb
+            ps.i, ps.nb, ps.base, ps.ev_base, ps.max_win = i, self.nbs[i], self.bases[i], self.ev_bases[i], \
+                self.max_wins[i]
+            if ps.nb == 0:
+                raise IndexError("list index out of range")       # batches[0] on an empty frame (:187)
+            ps.last_len = part.n - (ps.nb - 1) * pb
+            ps.n_full = ps.nb if ps.last_len == pb else ps.nb - 1
+            pss.append(ps)
+        for ps, rng in zip(pss, rngs):
+            self.shuffles[ps.i].reset(rng)
+        started = []
+        try:
+            # each partition's whole stream up front (one batched generate + tables);
+            # windows extend it if drifts (100 seed draws each) push it further
+            self._ensure_all([(ps.i, int(ps.nb * expected_draws_per_batch(pb) * 1.02)) for ps in pss])
+            for ps in pss:
+                perm0, ps.P = self.shuffles[ps.i].host_perm(0, ps.blen(0))   # batches[0].sample (:187)
+                started.append(ps)
+                if ps.nb < 2:
+                    raise ValueError("No objects to concatenate")  # pd.concat([]) (:212)
+                ps.train_rows = perm0.astype(np.int64)
+                ps.out = np.full((ps.nb - 1, 2), -1, dtype=np.int64)
+                ps.state = kernels.fresh_states(1)
+                ps.forest, ps.retrain, ps.j, ps.done = None, True, 1, False
+                ps.win = max(1, s.window_batches)
+                ps.seg_start = 1
+            while True:
+                live = [ps for ps in pss if not ps.done]
+                if not live:
+                    break
+                self._epoch(live)
+            return [ps.out for ps in pss]
+        finally:
+            for ps in started:
+                ns = self.shuffles[ps.i].numpy_state(ps.P)
+                rngs[ps.i].key[:] = ns[1]
+                rngs[ps.i].pos.value = ns[2]
+
+    def _epoch(self, live):
+        s, st, pb, stream = self.s, self.stats, self.s.per_batch, self.stream
+        t0 = time.perf_counter()
+        refit_before = self.stats.refit_s
+        need = [ps for ps in live if ps.retrain]
+        for ps in live:
+            ps.P_after_first = None
+        if need:
+            self._refits(need)
+        t1 = time.perf_counter()
+        host = t1 - t0 - (self.stats.refit_s - refit_before)
+        for ps in live:
+            if ps not in need:
+                ps.g0 = ps.j
+            ps.b_end = min(ps.nb, ps.j + min(ps.win, ps.max_win))
+            ps.Wg = max(0, min(ps.b_end, ps.n_full) - ps.g0)
+            ps.tail = ps.b_end == ps.nb and ps.last_len != pb and ps.nb - 1 >= ps.g0
+            ps.P_tail_after = None
+        shuf = [ps for ps in live if ps.Wg]
+        if shuf:
+            self._ensure_all([(ps.i, ps.P + self.shuffles[ps.i].window_draws(ps.Wg)) for ps in shuf])
+            max_W = max(ps.Wg for ps in shuf)
+            max_pieces = max(2 + self.shuffles[ps.i].window_draws(ps.Wg) // 8192 for ps in shuf)
+        tails = [ps for ps in live if ps.tail]
+        shuffled = False
+        if tails:
+            # the short last batch is shuffled on the host after the GPU batches before it
+            if shuf:
+                self._jobs_for(shuf, with_stop=False)
+                kernels.shuffle_window_batch(self.jobs, len(shuf), max_W, max_pieces, pb, stream, self.t_shuf)
+                kernels.shuffle_pick_batch(self.jobs, len(shuf), stream)
+                with torch.cuda.stream(stream):
+                    self.ctrl_h[self.o_pick:self.o_off].copy_(self.ctrl_d[self.o_pick:self.o_off], non_blocking=True)
+                stream.synchronize()
+                shuffled = True
+            for ps in tails:
+                P_tail = int(self.pick_h[ps.i]) + 1 if ps.Wg else ps.P
+                permT, ps.P_tail_after = self.shuffles[ps.i].host_perm(P_tail, ps.last_len)
+                self._upload_perm(ps.i, ps.nb - 1, permT, 1)
+        # segment table (predict), scan ranges and carried DDM states
+        segs = self.segs.rec
+        self.off_h[:] = 0
+        self.end_h[:] = 0
+        for k, ps in enumerate(live):
+            part, f = self.parts[ps.i], ps.forest
+            p0 = ps.base + ps.j * pb
+            p1 = ps.base + (ps.b_end - 1) * pb + ps.blen(ps.b_end - 1)
+            self.off_h[ps.i], self.end_h[ps.i] = p0, p1
+            self.state_h[ps.i] = ps.state[0]
+            sg = segs[k]
+            sg["X"], sg["ld"], sg["y"] = part.X.data_ptr(), part.X.shape[1], part.y.data_ptr()
+            sg["perm"], sg["err"], sg["pred"] = self.perm_all.data_ptr(), self.err_all.data_ptr(), 0
+            sg["first_err"] = self._dptr(self.o_first, ps.i, 8)
+            sg["pos_begin"], sg["pos_end"], sg["row_base"] = p0, p1, ps.base
+            d = f.desc
+            sg["nodes"], sg["roots"], sg["leaf_value"], sg["classes"] = d.nodes, d.roots, d.leaf_value or 0, d.classes
+            sg["n_trees"], sg["n_classes"], sg["n_nodes"], sg["pure"] = d.n_trees, d.n_classes, d.n_nodes, d.pure
+        t2 = time.perf_counter()
+        host += t2 - t1
+        t1 = t2
+        n = len(self.parts)
+        base = self.ctrl_d.data_ptr()
+        with torch.cuda.stream(stream):
+            self.ctrl_d[self.o_off:].copy_(self.ctrl_h[self.o_off:], non_blocking=True)
+        if shuf:
+            self._jobs_for(shuf, with_stop=True)
+            if not shuffled:
+                kernels.shuffle_window_batch(self.jobs, len(shuf), max_W, max_pieces, pb, stream, self.t_shuf)
+        kernels.forest_predict_batch(self.segs, len(live), pb, stream, self.t_pred)
+        kernels.scan_streams_raw(self.err_all.data_ptr(), base + self.o_off, n, self.params, base + self.o_state,
+                                 base + self.o_bbase, self.ev_total, self.ev_d.data_ptr(), base + self.o_first,
+                                 base + self.o_stop, base + self.o_nev, 0, None, stream, self.t_scan,
+                                 self.perm_all.data_ptr(), base + self.o_end)
+        if shuf:
+            kernels.shuffle_pick_batch(self.jobs, len(shuf), stream)
+        with torch.cuda.stream(stream):
+            self.ctrl_h[:self.o_off].copy_(self.ctrl_d[:self.o_off], non_blocking=True)
+            self.ctrl_h[self.o_state:].copy_(self.ctrl_d[self.o_state:], non_blocking=True)
+        stream.synchronize()
+        if self.timing:
+            st.predict_ms += self.t_pred.elapsed_ms()
+            st.scan_ms += self.t_scan.elapsed_ms()
+            if shuf:
+                st.shuffle_ms += self.t_shuf.elapsed_ms()
+        # read-backs that depend on the results: event rows and drift batches' shuffles
+        pending = False
+        for ps in live:
+            stop, nev = int(self.stop_h[ps.i]), int(self.nev_h[ps.i])
+            ps_last = ps.j + stop if stop >= 0 else ps.b_end - 1
+            p0, p1 = int(self.off_h[ps.i]), int(self.end_h[ps.i])
+            st.predicted_rows += p1 - p0
+            if self.timing:
+                st.predict_bytes += (p1 - p0) * (4 * ps.forest.packed.features_used + 6)
+                st.scan_rows += min(p1, ps.base + (ps_last + 1) * pb) - p0
+            with torch.cuda.stream(stream):
+                if nev:
+                    k, e0 = ps_last - ps.j + 1, ps.ev_base
+                    self.ev_h[e0:e0 + k].copy_(self.ev_d[e0:e0 + k], non_blocking=True)
+                    pending = True
+                if stop >= 0:
+                    d = ps.j + stop
+                    at = ps.base + d * pb
+                    self.small_h[ps.i][2][:ps.blen(d)].copy_(self.perm_all[at:at + ps.blen(d)], non_blocking=True)
+                    pending = True
+        if pending:
+            stream.synchronize()
+        t2 = time.perf_counter()
+        st.gpu_s += t2 - t1
+        st.epochs += 1
+        for ps in live:
+            stop, nev = int(self.stop_h[ps.i]), int(self.nev_h[ps.i])
+            last = ps.j + stop if stop >= 0 else ps.b_end - 1
+            if nev:
+                k, e0 = last - ps.j + 1, ps.ev_base
+                ev = self.ev_h[e0:e0 + k].numpy()
+                for c in range(2):
+                    hit = np.nonzero(ev[:, c] >= 0)[0]
+                    b = ps.j + hit
+                    ps.out[b - 1, c] = b * pb + ev[hit, c].astype(np.int64)
+            picked = int(self.pick_h[ps.i]) if ps.Wg else -1
+            # RNG position right after the last consumed batch shuffle
+            if stop >= 0:
+                d = ps.j + stop
+                if d < ps.g0:
+                    ps.P = ps.P_after_first              # drift in the refit batch: after its seeds
+                elif ps.tail and d == ps.nb - 1:
+                    ps.P = ps.P_tail_after
+                else:
+                    ps.P = picked + 1
+                ps.train_rows = d * pb + self.small_h[ps.i][2][:ps.blen(d)].numpy().astype(np.int64)
+                ps.retrain = True
+                # adaptive speculation: the next concept likely lasts about as long as this one
+                seg = d - ps.seg_start + 1
+                ps.win = max(max(1, s.window_batches), seg // 2)
+                ps.j = d + 1
+            else:
+                if ps.tail:
+                    ps.P = ps.P_tail_after
+                elif ps.Wg:
+                    ps.P = picked + 1
+                elif ps.P_after_first is not None:
+                    ps.P = ps.P_after_first
+                ps.state = self.state_h[ps.i:ps.i + 1].copy()
+                ps.j = ps.b_end
+                ps.win *= 2
+            if ps.j >= ps.nb:
+                ps.done = True
+        st.host_s += host + time.perf_counter() - t2
+
+
+class PartitionRunner(BatchRunner):
+    """One partition (the reference's per-UDF-call unit) on one HIP stream."""
+
+    def __init__(self, part, settings=None, stream=None, refit="native", timing=False):
+        super().__init__([part], settings, stream, refit, timing, fit_threads=1)
+        self.part = part
 
     def run(self, rng):
-        """Returns int64 [n_batches-1, 2]: partition rows of (first warning, change) per
-        batch 1.. (-1 = none).  Consumes `rng` (advanced in place) exactly as the reference
-        consumes np.random."""
-        s, part, st = self.s, self.part, self.stats
-        n, pb = part.n, s.per_batch
-        nb = (n + pb - 1) // pb
-        if nb == 0:
-            raise IndexError("list index out of range")       # batches[0] on an empty frame (:187)
-        last_len = n - (nb - 1) * pb
-        n_full = nb if last_len == pb else nb - 1              # batches with exactly pb rows
-
-        def blen(b):
-            return pb if b < nb - 1 else last_len
-
-        sh = self.shuffle
-        sh.reset(rng)
-        # the whole partition's stream up front (one generate + table pass); windows
-        # extend it if drifts (100 seed draws each) push it further
-        sh.ensure(int(nb * expected_draws_per_batch(pb) * 1.02))
-        stream = self.stream
-        base = self.ctrl_d.data_ptr()
-        try:
-            perm0, P = sh.host_perm(0, blen(0))                # batch_a = batches[0].sample (:187)
-            if nb < 2:
-                raise ValueError("No objects to concatenate")  # pd.concat([]) (:212)
-            train_rows = perm0.astype(np.int64)
-            out = np.full((nb - 1, 2), -1, dtype=np.int64)
-            state = kernels.fresh_states(1)
-            forest, retrain, j = None, True, 1
-            win = max(1, s.window_batches)
-            while j < nb:
-                t0 = time.perf_counter()
-                P_after_first = None
-                if retrain:
-                    permj, P = sh.host_perm(P, blen(j))        # batch_b.sample before the fit (:190, :194)
-                    self._upload_perm(j, permj, 0)
-                    forest, P = self._fit(train_rows, P)       # 100 tree seeds follow the shuffle
-                    P_after_first = P
-                    retrain = False
-                    state = kernels.fresh_states(1)            # ddm = None -> new DDM (:136-139)
-                    g0 = j + 1
-                else:
-                    g0 = j
-                b_end = min(nb, j + min(win, self.max_win))
-                gpu_end = min(b_end, n_full)
-                Wg = max(0, gpu_end - g0)
-                tail = b_end == nb and last_len != pb and nb - 1 >= g0
-                P_tail_after = None
-                if Wg:
-                    sh.window(P, Wg, self.perm_d[g0 * pb:], timer=self.t_shuf)
-                if tail:
-                    if Wg:
-                        sh.pick(self.neg1_d.data_ptr(), Wg, 0, Wg - 1, base + _PICK)   # end of the GPU batches
-                        P_tail = int(self._read_pick_now()) + 1
-                    else:
-                        P_tail = P
-                    permT, P_tail_after = sh.host_perm(P_tail, last_len)
-                    self._upload_perm(nb - 1, permT, 1)
-                p0, p1 = j * pb, (b_end - 1) * pb + blen(b_end - 1)
-                self._ctrl(_OFF, np.int64, 2)[:] = (p0, p1)
-                self._ctrl(_BASE, np.int64)[0] = 0
-                self.ctrl_np[_STATE:_STATE + 56] = state.view(np.uint8)
-                st.host_s += time.perf_counter() - t0
-                t0 = time.perf_counter()
-                with torch.cuda.stream(stream):
-                    self.ctrl_d[_OFF:_CTRL_BYTES].copy_(self.ctrl_h[_OFF:_CTRL_BYTES], non_blocking=True)
-                    kernels.forest_predict(part.X, part.y, self.perm_d, p0, p1, pb, forest, self.err_d,
-                                           first_err=self.ctrl_d[_FIRST_ERR:_FIRST_ERR + 8].view(torch.int64),
-                                           stream=stream, timer=self.t_pred)
-                    kernels.scan_streams_raw(self.err_d.data_ptr(), base + _OFF, 1, self.params, base + _STATE,
-                                             base + _BASE, b_end - j, self.ev_d.data_ptr(), base + _FIRST_ERR,
-                                             base + _STOP, base + _NEV, 0, None, stream, self.t_scan,
-                                             self.perm_d.data_ptr())
-                    if Wg:
-                        sh.pick(base + _STOP, Wg, g0 - j, b_end - 1 - j, base + _PICK)
-                    self.ctrl_h.copy_(self.ctrl_d, non_blocking=True)
-                stream.synchronize()
-                stop = int(self._ctrl(_STOP, np.int32)[0])
-                nev = int(self._ctrl(_NEV, np.int64)[0])
-                picked = int(self._ctrl(_PICK, np.int64)[0]) if Wg else -1
-                last = j + stop if stop >= 0 else b_end - 1
-                if self.timing:
-                    st.predict_ms += self.t_pred.elapsed_ms()
-                    st.scan_ms += self.t_scan.elapsed_ms()
-                    if Wg:
-                        st.shuffle_ms += self.t_shuf.elapsed_ms()
-                    st.predict_bytes += (p1 - p0) * (4 * forest.packed.features_used + 6)
-                    st.scan_rows += min(p1, (last + 1) * pb) - p0
-                if nev:
-                    k = last - j + 1
-                    with torch.cuda.stream(stream):
-                        self.ev_h[:k].copy_(self.ev_d[:k], non_blocking=True)
-                    stream.synchronize()
-                    ev = self.ev_h[:k].numpy()
-                    for c in range(2):
-                        hit = np.nonzero(ev[:, c] >= 0)[0]
-                        b = j + hit
-                        out[b - 1, c] = b * pb + ev[hit, c].astype(np.int64)
-                st.gpu_s += time.perf_counter() - t0
-                st.epochs += 1
-                st.predicted_rows += p1 - p0
-                # RNG position right after the last consumed batch shuffle
-                if stop >= 0:
-                    d = j + stop
-                    if d < g0:
-                        P = P_after_first                      # drift in the refit batch: after its seeds
-                    elif tail and d == nb - 1:
-                        P = P_tail_after
-                    else:
-                        P = picked + 1
-                    train_rows = self._perm_rows(d, blen(d))
-                    retrain = True
-                    j = d + 1
-                    win = max(1, s.window_batches)
-                else:
-                    if tail:
-                        P = P_tail_after
-                    elif Wg:
-                        P = picked + 1
-                    elif P_after_first is not None:
-                        P = P_after_first
-                    state = self._ctrl(_STATE, np.uint8, 56).copy().view(kernels.STATE_DTYPE)
-                    j = b_end
-                    win *= 2
-            return out
-        finally:
-            if "P" in locals():
-                ns = sh.numpy_state(P)
-                rng.key[:] = ns[1]
-                rng.pos.value = ns[2]
-
-    def _read_pick_now(self):
-        with torch.cuda.stream(self.stream):
-            self.ctrl_h[_PICK:_PICK + 8].copy_(self.ctrl_d[_PICK:_PICK + 8], non_blocking=True)
-        self.stream.synchronize()
-        return self._ctrl(_PICK, np.int64)[0]
+        return super().run([rng])[0]
 
 
 def run_partition_frame(pdf, rng, settings=None, device=None, stream=None, refit="native", stats=None):
@@ -348,6 +526,28 @@ def run_partition_frame(pdf, rng, settings=None, device=None, stream=None, refit
     if stats is not None:
         stats.update(runner.stats.as_dict())
     return events_frame(rows, pdf.index.to_numpy(), pdf[s.row_number].to_numpy())
+
+
+def run_partition_frames(frames, rngs, settings=None, device=None, stream=None, refit="native", stats=None):
+    """Many partition frames of ONE device in lockstep (BatchRunner): the output frame of
+    each, as run_partition_frame would return it, with rngs[k] consumed by frames[k]."""
+    s = settings or DDMSettings()
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    parts, labels = [], []
+    for pdf in frames:
+        feats = s.x_features or infer_x_features(pdf.columns)
+        X32 = pdf[feats].to_numpy(dtype=np.float64).astype(np.float32)
+        parts.append(DevicePartition.from_arrays(X32, pdf[s.target].to_numpy(), device, stream))
+        labels.append((pdf.index.to_numpy(), pdf[s.row_number].to_numpy()))
+    runner = BatchRunner(parts, s, stream, refit)
+    try:
+        rows = runner.run(rngs)
+    finally:
+        runner.close()
+    if stats is not None:
+        stats.update(runner.stats.as_dict())
+    return [events_frame(r, *lab) for r, lab in zip(rows, labels)]
 
 
 def events_frame(rows, local_labels, global_labels):

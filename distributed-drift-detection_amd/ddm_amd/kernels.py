@@ -16,6 +16,61 @@ STATE_DTYPE = np.dtype([("miss_prob", "<f8"), ("miss_std", "<f8"), ("miss_prob_m
 assert STATE_DTYPE.itemsize == 56
 
 
+# Batch tables (include/ddm_amd.h: ddm_predict_segment, ddm_shuffle_job, ddm_gen_job)
+SEG_DTYPE = np.dtype([("X", "<u8"), ("ld", "<i8"), ("y", "<u8"), ("perm", "<u8"), ("err", "<u8"), ("pred", "<u8"),
+                      ("first_err", "<u8"), ("pos_begin", "<i8"), ("pos_end", "<i8"), ("nodes", "<u8"),
+                      ("roots", "<u8"), ("leaf_value", "<u8"), ("classes", "<u8"), ("n_trees", "<i4"),
+                      ("n_classes", "<i4"), ("n_nodes", "<i4"), ("pure", "<i4"), ("row_base", "<i8"),
+                      ("block0", "<i8"), ("nblocks", "<i8")])
+assert SEG_DTYPE.itemsize == 144
+JOB_DTYPE = np.dtype([("R", "<u8"), ("Tsub", "<u8"), ("Tchunk", "<u8"), ("avail", "<i8"), ("P", "<i8"), ("W", "<i8"),
+                      ("pieces", "<u8"), ("info", "<u8"), ("J", "<u8"), ("E", "<u8"), ("perm_out", "<u8"),
+                      ("stop", "<u8"), ("pick_offset", "<i8"), ("pick_last", "<i8"), ("pick_out", "<u8")])
+assert JOB_DTYPE.itemsize == 120
+GEN_DTYPE = np.dtype([("state", "<u8"), ("R", "<u8"), ("n", "<i8")])
+
+
+class PinnedTable:
+    """A pinned host table of `dtype` records mirrored by a device buffer."""
+
+    def __init__(self, dtype, n, device):
+        self.dtype, self.n = dtype, int(n)
+        nbytes = max(1, self.n) * dtype.itemsize
+        self.h = torch.zeros(nbytes, dtype=torch.uint8, pin_memory=True)
+        self.d = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+        self.rec = self.h.numpy().view(dtype)
+
+    def upload(self, count, stream):
+        nb = int(count) * self.dtype.itemsize
+        if nb:
+            with torch.cuda.stream(stream):
+                self.d[:nb].copy_(self.h[:nb], non_blocking=True)
+
+
+def forest_predict_batch(table, n_segs, per_batch, stream, timer=None):
+    """All segments of `table` (a PinnedTable of SEG_DTYPE) in one launch per kernel variant;
+    the C-ABI assigns blocks and copies the table itself."""
+    check(lib.ddm_forest_predict_batch(table.h.data_ptr(), table.d.data_ptr(), int(n_segs), int(per_batch),
+                                       ctypes.c_void_p(stream.cuda_stream), *_evs(timer)), "ddm_forest_predict_batch")
+
+
+def shuffle_generate_batch(table, n_jobs, stream):
+    table.upload(n_jobs, stream)
+    check(lib.ddm_shuffle_generate_batch(table.d.data_ptr(), int(n_jobs), ctypes.c_void_p(stream.cuda_stream)),
+          "ddm_shuffle_generate_batch")
+
+
+def shuffle_window_batch(table, n_jobs, max_W, max_pieces, batch_len, stream, timer=None):
+    """Window shuffles of every job in the (already uploaded) job table."""
+    check(lib.ddm_shuffle_window_batch(table.d.data_ptr(), int(n_jobs), int(max_W), int(max_pieces), int(batch_len),
+                                       ctypes.c_void_p(stream.cuda_stream), *_evs(timer)), "ddm_shuffle_window_batch")
+
+
+def shuffle_pick_batch(table, n_jobs, stream):
+    check(lib.ddm_shuffle_pick_batch(table.d.data_ptr(), int(n_jobs), ctypes.c_void_p(stream.cuda_stream)),
+          "ddm_shuffle_pick_batch")
+
+
 def fresh_states(n):
     """`DDM(...)` as constructed at DDM_Process.py:139 (skmultiflow reset())."""
     st = np.zeros(n, dtype=STATE_DTYPE)

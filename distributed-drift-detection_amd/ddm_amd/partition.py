@@ -6,7 +6,8 @@ INSTANCES` (:225, a row-at-a-time Python UDF), `repartition("device_id")
 pandas frame with a RangeIndex, and the UDF outputs are concatenated.
 
 Here the groups are strided subsets computed with one vectorised modulo, each group's
-rows go to HBM of GPU `device_id % n_gpus` and run on their own HIP stream, and the
+rows go to HBM of GPU `device_id % n_gpus`, all partitions of one GPU run in lockstep in
+one BatchRunner (one batched launch per kernel per epoch, controller.py), and the
 per-partition outputs are concatenated in device_id order.  Partitions are
 independent (the reference shares nothing between them), so there is no collective on
 the data path; `dist.py` adds the one gather of events across processes.
@@ -17,7 +18,7 @@ import numpy as np
 import pandas as pd
 import torch
 
-from .controller import run_partition_frame
+from .controller import run_partition_frames
 from .params import OUTPUT_COLUMNS, DDMSettings
 from .rng import MTStream
 
@@ -46,36 +47,53 @@ def placement(device_id, n_gpus):
 
 
 def run_partitions(parts, seeds, settings=None, devices=None, max_workers=None, fn=None, stats=None):
-    """Run [(device_id, frame)] concurrently, one HIP stream (and host thread) per partition.
+    """Run [(device_id, frame)]: the partitions placed on each GPU run in lockstep in one
+    BatchRunner, one host thread per GPU.
 
     seeds: device_id -> MT19937 seed, the RNG each partition's Spark worker would hold
-    (`np.random.seed(base + device_id)` in the oracle).  fn(frame, rng, device) replaces
-    the GPU partition function (tests only).  Returns {device_id: output frame}."""
+    (`np.random.seed(base + device_id)` in the oracle).  fn(frame, rng, device, stats)
+    replaces the GPU path with a per-partition function (tests only; run in a thread
+    pool).  Returns {device_id: output frame}."""
     s = settings or DDMSettings()
     if devices is None:
         devices = [torch.device("cuda", i) for i in range(torch.cuda.device_count())]
-    if fn is None:
-        if not devices:
-            raise RuntimeError("no GPU visible: the MI355X partition path needs a HIP device")
+    if fn is not None:
+        def one(item):
+            d, frame = item
+            dev = devices[placement(d, len(devices))] if devices else None
+            st = {}
+            return d, fn(frame, MTStream.from_seed(seeds[d]), dev, st), st
 
-        def fn(frame, rng, device, st):
-            stream = torch.cuda.Stream(device)
-            return run_partition_frame(frame, rng, s, device, stream, stats=st)
+        workers = max_workers or max(1, min(len(parts), 16))
+        with ThreadPoolExecutor(workers) as ex:
+            res = list(ex.map(one, parts))
+        if stats is not None:
+            for d, _, st in res:
+                stats[d] = st
+        return {d: out for d, out, _ in res}
+    if not devices:
+        raise RuntimeError("no GPU visible: the MI355X partition path needs a HIP device")
+    groups = {}
+    for d, frame in parts:
+        groups.setdefault(placement(d, len(devices)), []).append((d, frame))
 
-    def one(item):
-        d, frame = item
-        dev = devices[placement(d, len(devices))] if devices else None
+    def on_gpu(item):
+        g, items = item
+        dev = devices[g]
         st = {}
-        out = fn(frame, MTStream.from_seed(seeds[d]), dev, st)
-        return d, out, st
+        outs = run_partition_frames([f for _, f in items], [MTStream.from_seed(seeds[d]) for d, _ in items], s,
+                                    dev, torch.cuda.Stream(dev), stats=st)
+        return [(d, o) for (d, _), o in zip(items, outs)], st
 
-    workers = max_workers or max(1, min(len(parts), 16))
-    with ThreadPoolExecutor(workers) as ex:
-        res = list(ex.map(one, parts))
-    if stats is not None:
-        for d, _, st in res:
-            stats[d] = st
-    return {d: out for d, out, _ in res}
+    with ThreadPoolExecutor(max(1, len(groups))) as ex:
+        res = list(ex.map(on_gpu, sorted(groups.items())))
+    out = {}
+    for pairs, st in res:
+        for d, o in pairs:
+            out[d] = o
+            if stats is not None:
+                stats[d] = st
+    return out
 
 
 def apply_in_pandas(df, instances, base_seed, settings=None, devices=None, max_workers=None):

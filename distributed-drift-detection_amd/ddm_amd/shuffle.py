@@ -129,28 +129,53 @@ class GpuShuffle:
     def _sp(self):
         return ctypes.c_void_p(self.stream.cuda_stream)
 
-    def ensure(self, upto):
-        """Generate R and tabulate chunks so that draws [0, upto) are covered."""
+    def window_draws(self, W):
+        """Draws a window of W batches may need (mean + 15% + slack; windows grow R on demand)."""
+        return int(W * expected_draws_per_batch(self.L) * 1.15) + 4 * CHUNK
+
+    def gen_request(self, upto):
+        """Grow R to cover draws [0, upto) plus one chunk; returns the (state, R, n) generate
+        job still to launch (or None) and the chunk count the tables must reach."""
         need_chunks = (int(upto) + CHUNK - 1) // CHUNK + 1
         target = need_chunks * CHUNK
         if target > self.cap:
             self._alloc(max(target, int(self.cap * 1.5)))
+        req = None
         if target > self.gen:
-            check(lib.ddm_shuffle_generate(self.mt.data_ptr(), self.R.data_ptr() + 4 * self.gen, target - self.gen,
-                                           self._sp()), "ddm_shuffle_generate")
+            req = (self.mt.data_ptr(), self.R.data_ptr() + 4 * self.gen, target - self.gen)
             self.gen = target
+        return req, need_chunks
+
+    def tables_to(self, need_chunks):
         if need_chunks > self.tab:
             check(lib.ddm_shuffle_tables(self.R.data_ptr(), self.tab, need_chunks - self.tab, self.L,
                                          self.Tsub.data_ptr(), self.Tchunk.data_ptr(), self._sp()),
                   "ddm_shuffle_tables")
             self.tab = need_chunks
 
+    def ensure(self, upto):
+        """Generate R and tabulate chunks so that draws [0, upto) are covered."""
+        req, need_chunks = self.gen_request(upto)
+        if req is not None:
+            check(lib.ddm_shuffle_generate(req[0], req[1], req[2], self._sp()), "ddm_shuffle_generate")
+        self.tables_to(need_chunks)
+
+    def fill_job(self, rec, P, W, perm_out_ptr, stop_ptr=0, pick_offset=0, pick_last=0, pick_out_ptr=0):
+        """One ddm_shuffle_job record (kernels.JOB_DTYPE) for a window of W batches from draw P;
+        R must already cover it (window_draws)."""
+        assert 0 <= W <= self.max_window
+        rec["R"], rec["Tsub"], rec["Tchunk"] = self.R.data_ptr(), self.Tsub.data_ptr(), self.Tchunk.data_ptr()
+        rec["avail"], rec["P"], rec["W"] = self.tab * CHUNK, int(P), int(W)
+        rec["pieces"], rec["info"] = self.pieces.data_ptr(), self.info.data_ptr()
+        rec["J"], rec["E"], rec["perm_out"] = self.J.data_ptr(), self.E.data_ptr(), int(perm_out_ptr)
+        rec["stop"], rec["pick_offset"], rec["pick_last"] = int(stop_ptr), int(pick_offset), int(pick_last)
+        rec["pick_out"] = int(pick_out_ptr)
+
     def window(self, P, W, perm_out, timer=None):
         """Shuffles of W batches from draw P into perm_out (device uint8, W*L bytes); E[b] =
         last draw of batch b (device)."""
         assert 0 < W <= self.max_window and perm_out.numel() >= W * self.L
-        est = int(W * expected_draws_per_batch(self.L) * 1.15) + 4 * CHUNK
-        self.ensure(P + est)
+        self.ensure(P + self.window_draws(W))
         ev = (None, None) if timer is None else (timer.ev[0], timer.ev[1])
         check(lib.ddm_shuffle_window(self.R.data_ptr(), self.Tsub.data_ptr(), self.Tchunk.data_ptr(),
                                      self.tab * CHUNK, int(P), int(W), self.L, self.pieces.data_ptr(),

@@ -91,3 +91,39 @@ def test_synthetic_rialto_stream_vs_oracle():
     want = run_partition(X.astype(np.float64), y, np.arange(n), np.arange(n))
     assert np.array_equal(got[:, 0], want[:, 0]) and np.array_equal(got[:, 1], want[:, 2])
     assert (want[:, 2] >= 0).sum() >= 3
+
+
+@pytest.mark.parametrize("win,maxwin", [(256, 1 << 16), (1, 8), (7, 64)])
+def test_lockstep_batch_of_unequal_partitions_vs_oracle(win, maxwin):
+    """Partitions of different lengths (short tails, one finishing epochs before the
+    others) in ONE BatchRunner == the oracle run on each partition alone."""
+    from ddm_amd import kernels
+    from ddm_amd.controller import BatchRunner, DevicePartition
+    from ddm_amd.params import DDMSettings
+    from ddm_amd.rng import MTStream
+    from oracle.controller import run_partition
+    dev = torch.device("cuda", 0)
+    sizes, F = (24_000, 17_055, 4_321, 250, 9_999), 27
+    parts, host = [], []
+    for k, n in enumerate(sizes):
+        part = DevicePartition.allocate(n, F, dev)
+        kernels.synth_block_labels(part.y[:n], part=k, n_parts=len(sizes), block_rows=6_007, n_classes=10)
+        kernels.synth_features(part.X, part.y[:n], row0=k, row_stride=len(sizes), seed=7, noise=0.04)
+        parts.append(part)
+    torch.cuda.synchronize()
+    for part in parts:
+        host.append((part.X[:, :part.n].t().contiguous().cpu().numpy().astype(np.float64),
+                     part.y[:part.n].cpu().numpy().astype(np.int64)))
+    runner = BatchRunner(parts, DDMSettings(window_batches=win, max_window_batches=maxwin))
+    rngs = [MTStream.from_seed(50 + k) for k in range(len(parts))]
+    got = runner.run(rngs)
+    runner.close()
+    drifts = 0
+    for k, (X, y) in enumerate(host):
+        np.random.seed(50 + k)
+        want = run_partition(X, y, np.arange(len(y)), np.arange(len(y)))
+        assert np.array_equal(got[k][:, 0], want[:, 0]) and np.array_equal(got[k][:, 1], want[:, 2]), k
+        after = np.random.get_state()
+        assert np.array_equal(rngs[k].key, after[1]) and rngs[k].pos.value == after[2], k
+        drifts += int((want[:, 2] >= 0).sum())
+    assert drifts >= 5
