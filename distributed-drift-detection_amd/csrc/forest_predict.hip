@@ -15,7 +15,11 @@
 // addressed through the batch shuffle (row = batch*per_batch + perm[g]) so the
 // error vector comes out already in DDM order.  The forest (16-byte nodes) sits in
 // LDS when it fits, shared by the workgroup's rows for its whole grid-stride loop.
-// The first error position is reduced per wave with a ballot and one atomicMin.
+// The first error position is reduced per wave with a ballot; a wave's positions only
+// grow along its grid-stride loop, so it issues at most one atomicMin (and none when the
+// global minimum is already smaller): hot single-address atomics would otherwise
+// serialise every wave that sees an error.
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -24,6 +28,18 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kMaxLdsForest = 64 * 1024;
+
+// first_err reduction: at most one atomicMin per wave (see the file comment).
+__device__ __forceinline__ void note_first_error(unsigned long long* first_err, int e, int64_t g, int lane,
+                                                 bool& wave_done) {
+    const unsigned long long m = __ballot(e);
+    if (m && !wave_done) {
+        wave_done = true;
+        if (lane == __ffsll((long long)m) - 1 &&
+            (unsigned long long)g < __hip_atomic_load(first_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicMin(first_err, (unsigned long long)g);
+    }
+}
 
 template <bool kLdsForest>
 __device__ __forceinline__ int leaf_of(const ddm_node* __restrict__ nodes, int nd, const float* __restrict__ X,
@@ -56,8 +72,10 @@ struct Seg {
     int32_t n_trees, n_classes, n_nodes, pure;
     int64_t row_base;            // rows are (g / per_batch) * per_batch + perm[g] - row_base
     int64_t block0, nblocks;     // this segment's blocks in the launch grid
+    const uint8_t* cforest;      // compiled forest or NULL
+    int32_t cf_slots, cf_vote_regs, cf_leaves, cf_pad;
 };
-static_assert(sizeof(Seg) == sizeof(ddm_predict_segment) && sizeof(Seg) == 144, "Seg must mirror ddm_predict_segment");
+static_assert(sizeof(Seg) == sizeof(ddm_predict_segment) && sizeof(Seg) == 168, "Seg must mirror ddm_predict_segment");
 
 template <bool kPure, int kK, bool kLdsForest>
 __device__ __forceinline__ void predict_segment(const Seg& sg, int64_t blk, int64_t nblk, int64_t per_batch,
@@ -78,6 +96,7 @@ __device__ __forceinline__ void predict_segment(const Seg& sg, int64_t blk, int6
         roots = r;
     }
     const int lane = threadIdx.x & 63;
+    bool wave_done = false;
     const int64_t stride = nblk * kThreads;
     for (int64_t base = sg.pos_begin + blk * kThreads + (threadIdx.x & ~63); base < sg.pos_end; base += stride) {
         const int64_t g = base + lane;
@@ -133,10 +152,7 @@ __device__ __forceinline__ void predict_segment(const Seg& sg, int64_t blk, int6
             sg.err[g] = (uint8_t)e;
             if (sg.pred) sg.pred[g] = label;
         }
-        if (sg.first_err) {
-            const unsigned long long m = __ballot(e);
-            if (m && lane == __ffsll((long long)m) - 1) atomicMin(sg.first_err, (unsigned long long)g);
-        }
+        if (sg.first_err) note_first_error(sg.first_err, e, g, lane, wave_done);
     }
 }
 
@@ -160,6 +176,261 @@ __global__ __launch_bounds__(kThreads) void k_forest_predict_batch(const Seg* __
     predict_segment<kPure, kK, kLdsForest>(sg, gb - sg.block0, sg.nblocks, per_batch, smem);
 }
 
+// ---------------------------------------------------------------------------------
+// Compiled-forest path (ddm_forest_compile, csrc/forest_compile.cpp).
+//
+// A workgroup of 512 threads owns a tile of whole batches (tile = floor(512/pb)*pb
+// positions, so a tile's DDM positions and its rows are the same set):
+//   1. row phase: thread t owns ROW g0+t of the tile.  It loads only the forest's
+//      feature columns (slot s <- X[cols[s]*ld + row], 4-byte coalesced loads), runs the
+//      compiled forest out of registers (node data arrive through uniform/scalar loads)
+//      and keeps err/label in LDS at t;
+//   2. position phase: thread t owns DDM POSITION g0+t and picks the error of row
+//      tb + perm[g] from LDS, so err (and pred) are written in DDM order, coalesced.
+// Bytes per row from HBM: 4*n_slots (X) + 4 (y) + 1 (perm) + 1 (err).
+constexpr int kCfThreads = 512;
+
+// Uniform loads: the blob and the segment table are read-only for the kernel's lifetime,
+// so they are read through the constant address space (scalar s_load into SGPRs).
+#define DDM_CONST __attribute__((address_space(4)))
+template <class T>
+__device__ __forceinline__ T ldu(const T* p) {
+    if constexpr (std::is_arithmetic<T>::value) {
+        return *(const DDM_CONST T*)(p);
+    } else {
+        static_assert(sizeof(T) % 4 == 0, "records are dword multiples");
+        T out;
+        uint32_t* o = reinterpret_cast<uint32_t*>(&out);
+        const DDM_CONST uint32_t* q = (const DDM_CONST uint32_t*)(p);
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof(T) / 4); ++i) o[i] = q[i];
+        return out;
+    }
+}
+
+// Stump record {float32 threshold, slot, delta[kVR]} padded to 16 / 32 bytes
+// (ddm_forest_compile: stump_words).
+template <int kVR>
+struct StumpRec {
+    float thr;
+    int32_t slot;
+    uint32_t delta[kVR];
+    uint32_t pad[(kVR <= 2 ? 4 : 8) - 2 - kVR];
+};
+template <>
+struct StumpRec<2> {
+    float thr;
+    int32_t slot;
+    uint32_t delta[2];
+};
+template <int kVR>
+struct StumpChunk {
+    StumpRec<kVR> r[8];
+};
+
+template <bool kNanLeft, int kVR>
+__device__ __forceinline__ void stump_one(const StumpRec<kVR>& rec, const float* xl, uint32_t (&votes)[kVR]) {
+    const float v = xl[rec.slot * kCfThreads];
+    const bool right = kNanLeft ? (v > rec.thr) : !(v <= rec.thr);
+#pragma unroll
+    for (int j = 0; j < kVR; ++j) votes[j] += right ? rec.delta[j] : 0u;
+}
+
+// vote += right ? delta : 0 over stumps [k0, k1); right = !(x <= thr) (kNanLeft false:
+// NaN goes right) or x > thr.  x comes from the thread's LDS column (xl[slot * 512]).
+// Records are uniform scalar loads, eight per trip.
+template <bool kNanLeft, int kVR>
+__device__ __forceinline__ void stump_range(const StumpRec<kVR>* recs, int k0, int k1, const float* xl,
+                                            uint32_t (&votes)[kVR]) {
+    const StumpRec<kVR>* p = recs + k0;
+    const StumpRec<kVR>* e = recs + k1;
+    for (; p + 8 <= e; p += 8) {                // 8 records per trip: wide scalar loads
+        const StumpChunk<kVR> c = ldu(reinterpret_cast<const StumpChunk<kVR>*>(p));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) stump_one<kNanLeft, kVR>(c.r[i], xl, votes);
+    }
+    for (; p < e; ++p) stump_one<kNanLeft, kVR>(ldu(p), xl, votes);
+}
+
+template <int kU, int kVR>
+__device__ __forceinline__ void cf_segment(const Seg& sg, int64_t blk, int64_t nblk, int pb, unsigned char* smem) {
+    const uint8_t* blob = sg.cforest;
+    const ddm_cforest_head* H = reinterpret_cast<const ddm_cforest_head*>(blob);
+    const int U = ldu(&H->n_slots), K = ldu(&H->n_classes), n_general = ldu(&H->n_general);
+    const int n_leaves = ldu(&H->n_leaves), S = ldu(&H->n_stumps), n_right = ldu(&H->n_stumps_right);
+    const StumpRec<kVR>* recs = reinterpret_cast<const StumpRec<kVR>*>(blob + ldu(&H->stumps_off));
+    const ddm_cforest_tree* trees = reinterpret_cast<const ddm_cforest_tree*>(blob + ldu(&H->trees_off));
+    const ddm_cforest_node* gnodes = reinterpret_cast<const ddm_cforest_node*>(blob + ldu(&H->nodes_off));
+    const uint8_t* leafcls = blob + ldu(&H->leafcls_off);
+
+    const int tid = threadIdx.x;
+    // LDS: row slots [U][512] | err [512] | label [512] | classes [16] | leaf classes
+    float* s_x = reinterpret_cast<float*>(smem);
+    uint8_t* s_e = reinterpret_cast<uint8_t*>(s_x + (size_t)U * kCfThreads);
+    int32_t* s_pred = reinterpret_cast<int32_t*>(s_e + kCfThreads);
+    int32_t* s_cls = s_pred + kCfThreads;
+    uint8_t* s_leaf = reinterpret_cast<uint8_t*>(s_cls + 16);
+    for (int k = tid; k < n_leaves; k += kCfThreads) s_leaf[k] = leafcls[k];
+    if (tid < 16) s_cls[tid] = H->classes[tid];
+    uint32_t base_votes[kVR];
+#pragma unroll
+    for (int j = 0; j < kVR; ++j) base_votes[j] = ldu(&H->base_votes[j]);
+
+    const int tile = (kCfThreads / pb) * pb;
+    const int tb = (tid / pb) * pb;
+    const float* __restrict__ X = sg.X;
+    const int64_t ld = sg.ld;
+    int64_t colbase[kU];
+#pragma unroll
+    for (int s = 0; s < kU; ++s) colbase[s] = U > 0 ? (int64_t)ldu(&H->cols[s < U ? s : U - 1]) * ld : 0;
+    const float* xl = s_x + tid;
+    float* xw = s_x + tid;
+    const int lane = tid & 63;
+    bool wave_done = false;
+    // Register double buffering: the next tile's slots and label are loaded while the
+    // current tile is evaluated out of LDS.
+    const int64_t step = nblk * tile;
+    auto row_of = [&](int64_t gt0) -> int64_t {
+        const int64_t gg = gt0 + tid;
+        return ((tid < tile && gg < sg.pos_end) ? gg : min(gt0, sg.pos_end - 1)) - sg.row_base;
+    };
+    float vnext[kU];
+    int32_t ynext = 0;
+    int64_t g0 = sg.pos_begin + blk * tile;
+    if (g0 < sg.pos_end) {
+        const int64_t row = row_of(g0);
+        if (U > 0) {
+#pragma unroll
+            for (int s = 0; s < kU; ++s) vnext[s] = X[colbase[s] + row];
+        }
+        ynext = sg.y[row];
+    }
+    for (; g0 < sg.pos_end; g0 += step) {
+        __syncthreads();                        // LDS tables ready / previous tile consumed
+        const int64_t g = g0 + tid;
+        const bool valid = tid < tile && g < sg.pos_end;
+        // ---- row phase (every lane runs it, on a clamped row, so that the forest loops
+        // stay wave-uniform and their records stay in SGPRs).  Each thread only reads the
+        // LDS column it wrote itself, so no barrier is needed before the forest.
+        {
+            if (U > 0) {
+#pragma unroll
+                for (int s = 0; s < kU; ++s)
+                    if (s < U) xw[s * kCfThreads] = vnext[s];
+            }
+            const int32_t yv = ynext;
+            if (g0 + step < sg.pos_end) {       // prefetch (slots past U re-read the last column)
+                const int64_t row = row_of(g0 + step);
+                if (U > 0) {
+#pragma unroll
+                    for (int s = 0; s < kU; ++s) vnext[s] = X[colbase[s] + row];
+                }
+                ynext = sg.y[row];
+            }
+            uint32_t votes[kVR];
+#pragma unroll
+            for (int j = 0; j < kVR; ++j) votes[j] = base_votes[j];
+            stump_range<false, kVR>(recs, 0, n_right, xl, votes);
+            if (n_right < S) stump_range<true, kVR>(recs, n_right, S, xl, votes);
+            // deeper trees: QuickScorer exit-leaf masks
+            for (int t = 0; t < n_general; ++t) {
+                const ddm_cforest_tree T = ldu(trees + t);
+                uint32_t mlo = 0xffffffffu, mhi = 0xffffffffu;
+                for (int k = T.node_begin; k < T.node_begin + T.n_nodes; ++k) {
+                    const ddm_cforest_node nd = ldu(gnodes + k);
+                    const float v = xl[(nd.slot_nanleft & 0xff) * kCfThreads];
+                    const bool right = (nd.slot_nanleft >> 8) ? (v > nd.threshold) : !(v <= nd.threshold);
+                    mlo = right ? (mlo & ~nd.left_lo) : mlo;
+                    mhi = right ? (mhi & ~nd.left_hi) : mhi;
+                }
+                const int leaf = mlo ? __builtin_ctz(mlo) : 32 + __builtin_ctz(mhi);
+                const int c = s_leaf[T.leaf_begin + leaf];
+                const uint32_t inc = 1u << (8 * (c & 3));
+#pragma unroll
+                for (int j = 0; j < kVR; ++j) votes[j] += (c >> 2) == j ? inc : 0u;
+            }
+            // first argmax over the vote counters
+            int best = 0, bestv = -1;
+#pragma unroll
+            for (int c = 0; c < 4 * kVR; ++c) {
+                const int v = (int)((votes[c >> 2] >> (8 * (c & 3))) & 0xffu);
+                if (c < K && v > bestv) {
+                    bestv = v;
+                    best = c;
+                }
+            }
+            const int32_t label = s_cls[best];
+            if (valid) {
+                s_e[tid] = (uint8_t)(label != yv);
+                if (sg.pred) s_pred[tid] = label;
+            }
+        }
+        __syncthreads();
+        // ---- position phase
+        int e = 0;
+        if (valid) {
+            const int k = tb + (int)sg.perm[g];
+            e = s_e[k];
+            sg.err[g] = (uint8_t)e;
+            if (sg.pred) sg.pred[g] = s_pred[k];
+        }
+        if (sg.first_err) note_first_error(sg.first_err, e, g, lane, wave_done);
+    }
+}
+
+template <int kU, int kVR>
+__global__ __launch_bounds__(kCfThreads) void k_cforest_predict(Seg sg, int pb) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    cf_segment<kU, kVR>(sg, blockIdx.x, gridDim.x, pb, smem);
+}
+
+template <int kU, int kVR>
+__global__ __launch_bounds__(kCfThreads) void k_cforest_predict_batch(const Seg* __restrict__ segs, int n_segs,
+                                                                      int64_t block_base, int pb) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int64_t gb = block_base + blockIdx.x;
+    int s = 0;
+    while (s < n_segs && !(ldu(&segs[s].block0) <= gb && gb < ldu(&segs[s].block0) + ldu(&segs[s].nblocks))) ++s;
+    if (s == n_segs) return;
+    const Seg sg = ldu(segs + s);
+    cf_segment<kU, kVR>(sg, gb - sg.block0, sg.nblocks, pb, smem);
+}
+
+using cf_fn = void (*)(Seg, int);
+using cf_batch_fn = void (*)(const Seg*, int, int64_t, int);
+
+int cf_ukind(int slots) { return slots <= 8 ? 0 : slots <= 16 ? 1 : 2; }
+int cf_vkind(int vr) { return vr <= 1 ? 0 : vr <= 2 ? 1 : 2; }
+
+template <int kU>
+cf_fn pick_cf_u(int vk) {
+    return vk == 0 ? k_cforest_predict<kU, 1> : vk == 1 ? k_cforest_predict<kU, 2> : k_cforest_predict<kU, 4>;
+}
+cf_fn pick_cf(int uk, int vk) {
+    return uk == 0 ? pick_cf_u<8>(vk) : uk == 1 ? pick_cf_u<16>(vk) : pick_cf_u<32>(vk);
+}
+template <int kU>
+cf_batch_fn pick_cf_batch_u(int vk) {
+    return vk == 0 ? k_cforest_predict_batch<kU, 1>
+                   : vk == 1 ? k_cforest_predict_batch<kU, 2> : k_cforest_predict_batch<kU, 4>;
+}
+cf_batch_fn pick_cf_batch(int uk, int vk) {
+    return uk == 0 ? pick_cf_batch_u<8>(vk) : uk == 1 ? pick_cf_batch_u<16>(vk) : pick_cf_batch_u<32>(vk);
+}
+
+// LDS of the compiled path: row slots [slots][512] + err + labels + classes + leaf classes.
+size_t cf_lds_bytes(int leaves, int slots) {
+    return (size_t)4 * kCfThreads * slots + kCfThreads + 4 * kCfThreads + 64 + (size_t)((leaves + 15) & ~15);
+}
+
+size_t cf_lds_bound(const Seg& g) { return cf_lds_bytes(g.cf_leaves, g.cf_slots); }
+
+bool cf_usable(const Seg& g, int pb) {
+    return g.cforest && g.cf_slots >= 0 && g.cf_slots <= 32 && g.cf_vote_regs >= 1 && g.cf_vote_regs <= 4 &&
+           g.pos_begin % pb == 0 && cf_lds_bound(g) <= 80 * 1024;
+}
+
+// ---------------------------------------------------------------------------------
 using predict_fn = void (*)(Seg, int64_t);
 using predict_batch_fn = void (*)(const Seg*, int, int64_t, int64_t);
 
@@ -193,6 +464,8 @@ size_t forest_lds_bytes(int n_nodes, int n_trees) {
     return ((size_t)n_nodes * sizeof(ddm_node) + (size_t)n_trees * 4 + 15) & ~(size_t)15;
 }
 
+constexpr int kMaxBlocks = 256 * 8;
+
 }  // namespace
 
 extern "C" int ddm_forest_predict(const float* X, int64_t ld, int32_t n_features, const int32_t* y,
@@ -218,20 +491,30 @@ extern "C" int ddm_forest_predict(const float* X, int64_t ld, int32_t n_features
     }
     const int64_t n = pos_end - pos_begin;
     if (n == 0) return 0;
-    const size_t lds = forest_lds_bytes(forest->n_nodes, forest->n_trees);
-    const bool use_lds = lds <= (size_t)kMaxLdsForest;
-    const predict_fn fn = use_lds ? pick<true>(forest->pure, forest->n_classes)
-                                  : pick<false>(forest->pure, forest->n_classes);
-    const int64_t blocks = std::min<int64_t>(ddm::ceil_div(n, kThreads), 256 * 8);
     Seg sg{X, ld, y, perm, err_out, pred_out, reinterpret_cast<unsigned long long*>(first_err), pos_begin, pos_end,
            forest->nodes, forest->roots, forest->leaf_value, forest->classes, forest->n_trees, forest->n_classes,
-           forest->n_nodes, forest->pure, 0, 0, blocks};
+           forest->n_nodes, forest->pure, 0, 0, 0, forest->cforest, forest->cf_slots, forest->cf_vote_regs,
+           forest->cf_leaves, 0};
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
-    hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kThreads), use_lds ? lds : 0, s, sg, (int64_t)per_batch);
+    if (cf_usable(sg, per_batch)) {
+        const int tile = (kCfThreads / per_batch) * per_batch;
+        sg.nblocks = std::min<int64_t>(ddm::ceil_div(n, tile), kMaxBlocks);
+        hipLaunchKernelGGL(pick_cf(cf_ukind(sg.cf_slots), cf_vkind(sg.cf_vote_regs)), dim3((unsigned)sg.nblocks),
+                           dim3(kCfThreads), cf_lds_bound(sg), s, sg, (int)per_batch);
+    } else {
+        const size_t lds = forest_lds_bytes(forest->n_nodes, forest->n_trees);
+        const bool use_lds = lds <= (size_t)kMaxLdsForest;
+        const predict_fn fn = use_lds ? pick<true>(forest->pure, forest->n_classes)
+                                      : pick<false>(forest->pure, forest->n_classes);
+        sg.nblocks = std::min<int64_t>(ddm::ceil_div(n, kThreads), kMaxBlocks);
+        hipLaunchKernelGGL(fn, dim3((unsigned)sg.nblocks), dim3(kThreads), use_lds ? lds : 0, s, sg,
+                           (int64_t)per_batch);
+    }
+    if (int rc = ddm::launch_status("ddm_forest_predict")) return rc;
     if (ev_end)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
-    return ddm::launch_status("ddm_forest_predict");
+    return 0;
 }
 
 static_assert(sizeof(Seg) == sizeof(ddm_predict_segment), "ddm_predict_segment layout");
@@ -244,15 +527,15 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
         return DDM_E_ARG;
     }
     hipStream_t s = ddm::as_hip(stream);
-    // One launch per kernel variant (pure/impure x classes x LDS-resident forest); every
-    // launch walks the whole device table and only the blocks assigned to its segments
-    // work.  Block counts are proportional to rows, 2048 blocks in total per variant.
+    // One launch per kernel variant; every launch walks the whole device table and only
+    // the blocks assigned to its segments work.  Variants: 16 node-walk kinds (pure x
+    // classes x LDS-resident forest) and 9 compiled kinds (slots x vote registers).
     Seg* hs = reinterpret_cast<Seg*>(const_cast<ddm_predict_segment*>(segs_host));
     for (int i = 0; i < n_segs; ++i) {
         const Seg& g = hs[i];
         if (!g.X || !g.y || !g.perm || !g.err || !g.nodes || !g.roots || !g.classes || g.pos_end < g.pos_begin ||
-            g.n_classes <= 0 || g.n_classes > 64 || g.n_trees <= 0 || (g.pure && g.n_trees > 255) ||
-            (!g.pure && !g.leaf_value)) {
+            g.pos_begin < 0 || g.n_classes <= 0 || g.n_classes > 64 || g.n_trees <= 0 ||
+            (g.pure && g.n_trees > 255) || (!g.pure && !g.leaf_value)) {
             ddm::set_error("ddm_forest_predict_batch: invalid segment %d", i);
             return DDM_E_ARG;
         }
@@ -262,27 +545,32 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
     }
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
-    // Variants (pure/impure x classes x LDS-resident forest) get disjoint global block
-    // ranges, so ONE copy of the table serves one launch per variant present.
+    constexpr int kNV = 16 + 9;
     std::vector<int> variant(n_segs);
     for (int i = 0; i < n_segs; ++i) {
         const Seg& g = hs[i];
-        const bool lds = forest_lds_bytes(g.n_nodes, g.n_trees) <= (size_t)kMaxLdsForest;
-        const int kc = g.n_classes <= 4 ? 0 : g.n_classes <= 8 ? 1 : g.n_classes <= 16 ? 2 : 3;
-        variant[i] = (g.pure ? 1 : 0) * 8 + (lds ? 4 : 0) + kc;
+        if (cf_usable(g, per_batch)) {
+            variant[i] = 16 + 3 * cf_ukind(g.cf_slots) + cf_vkind(g.cf_vote_regs);
+        } else {
+            const bool lds = forest_lds_bytes(g.n_nodes, g.n_trees) <= (size_t)kMaxLdsForest;
+            const int kc = g.n_classes <= 4 ? 0 : g.n_classes <= 8 ? 1 : g.n_classes <= 16 ? 2 : 3;
+            variant[i] = (g.pure ? 1 : 0) * 8 + (lds ? 4 : 0) + kc;
+        }
     }
-    int64_t vbase[17] = {0};
-    size_t vlds[16] = {0};
+    const int tile = (kCfThreads / per_batch) * per_batch;
+    int64_t vbase[kNV + 1] = {0};
+    size_t vlds[kNV] = {0};
     int64_t b0 = 0;
-    for (int v = 0; v < 16; ++v) {
+    for (int v = 0; v < kNV; ++v) {
         vbase[v] = b0;
+        const int unit = v >= 16 ? tile : kThreads;
         int64_t rows = 0;
         for (int i = 0; i < n_segs; ++i)
             if (variant[i] == v) {
                 rows += hs[i].pos_end - hs[i].pos_begin;
-                vlds[v] = std::max(vlds[v], forest_lds_bytes(hs[i].n_nodes, hs[i].n_trees));
+                vlds[v] = std::max(vlds[v], v >= 16 ? cf_lds_bound(hs[i]) : forest_lds_bytes(hs[i].n_nodes, hs[i].n_trees));
             }
-        const int64_t total_blocks = rows ? std::min<int64_t>(ddm::ceil_div(rows, kThreads), 256 * 8) : 0;
+        const int64_t total_blocks = rows ? std::min<int64_t>(ddm::ceil_div(rows, unit), kMaxBlocks) : 0;
         for (int i = 0; i < n_segs; ++i) {
             if (variant[i] != v) continue;
             Seg& g = hs[i];
@@ -292,22 +580,27 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
             b0 += g.nblocks;
         }
     }
-    vbase[16] = b0;
+    vbase[kNV] = b0;
     if (b0 > 0) {
         if (int rc = ddm::hip_status(hipMemcpyAsync(segs_dev, hs, sizeof(Seg) * n_segs, hipMemcpyHostToDevice, s),
                                      "predict_batch table"))
             return rc;
     }
-    for (int v = 0; v < 16; ++v) {
+    for (int v = 0; v < kNV; ++v) {
         const int64_t nb = vbase[v + 1] - vbase[v];
         if (nb == 0) continue;
-        const bool lds = (v & 4) != 0;
-        const bool pure = (v & 8) != 0;
-        const int kmax = (v & 3) == 0 ? 4 : (v & 3) == 1 ? 8 : (v & 3) == 2 ? 16 : 64;
-        const predict_batch_fn fn = lds ? pick_batch<true>(pure, kmax) : pick_batch<false>(pure, kmax);
-        hipLaunchKernelGGL(fn, dim3((unsigned)nb), dim3(kThreads), lds ? vlds[v] : 0, s,
-                           reinterpret_cast<const Seg*>(segs_dev), n_segs, vbase[v],
-                           (int64_t)per_batch);
+        if (v >= 16) {
+            const int uk = (v - 16) / 3, vk = (v - 16) % 3;
+            hipLaunchKernelGGL(pick_cf_batch(uk, vk), dim3((unsigned)nb), dim3(kCfThreads), vlds[v], s,
+                               reinterpret_cast<const Seg*>(segs_dev), n_segs, vbase[v], (int)per_batch);
+        } else {
+            const bool lds = (v & 4) != 0;
+            const bool pure = (v & 8) != 0;
+            const int kmax = (v & 3) == 0 ? 4 : (v & 3) == 1 ? 8 : (v & 3) == 2 ? 16 : 64;
+            const predict_batch_fn fn = lds ? pick_batch<true>(pure, kmax) : pick_batch<false>(pure, kmax);
+            hipLaunchKernelGGL(fn, dim3((unsigned)nb), dim3(kThreads), lds ? vlds[v] : 0, s,
+                               reinterpret_cast<const Seg*>(segs_dev), n_segs, vbase[v], (int64_t)per_batch);
+        }
         if (int rc = ddm::launch_status("ddm_forest_predict_batch")) return rc;
     }
     if (ev_end)

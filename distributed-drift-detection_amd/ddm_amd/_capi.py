@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
@@ -34,10 +34,12 @@ class DdmState(ctypes.Structure):
 class DdmForest(ctypes.Structure):
     _fields_ = [("nodes", ctypes.c_void_p), ("roots", ctypes.c_void_p), ("leaf_value", ctypes.c_void_p),
                 ("classes", ctypes.c_void_p), ("n_trees", ctypes.c_int32), ("n_classes", ctypes.c_int32),
-                ("n_nodes", ctypes.c_int32), ("pure", ctypes.c_int32)]
+                ("n_nodes", ctypes.c_int32), ("pure", ctypes.c_int32), ("cforest", ctypes.c_void_p),
+                ("cf_slots", ctypes.c_int32), ("cf_vote_regs", ctypes.c_int32), ("cf_leaves", ctypes.c_int32),
+                ("cf_pad", ctypes.c_int32)]
 
 
-assert ctypes.sizeof(DdmState) == 56 and ctypes.sizeof(DdmParams) == 24 and ctypes.sizeof(DdmForest) == 48
+assert ctypes.sizeof(DdmState) == 56 and ctypes.sizeof(DdmParams) == 24 and ctypes.sizeof(DdmForest) == 72
 
 _vp, _i32, _i64, _u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
 _f32, _pi32 = ctypes.c_float, ctypes.POINTER(ctypes.c_int32)
@@ -65,6 +67,8 @@ SIGNATURES = {
     "ddm_mt_perms": (ctypes.c_int, [_vp, _pi32, _vp, _i64, _vp, _vp]),
     "ddm_mt_randint31": (ctypes.c_int, [_vp, _pi32, _i64, _vp]),
     "ddm_mt_skip": (ctypes.c_int, [_vp, _pi32, _i64]),
+    "ddm_forest_compile": (ctypes.c_int, [_vp, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _i64,
+                                          ctypes.POINTER(ctypes.c_int64)]),
     "ddm_rf_fit": (ctypes.c_int, [_vp, _i32, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp]),
     "ddm_synth_block_labels": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i32, _vp]),
     "ddm_synth_features": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _i64, _i64, _u64, _f32, _vp]),

@@ -403,6 +403,8 @@ class BatchRunner:
             d = f.desc
             sg["nodes"], sg["roots"], sg["leaf_value"], sg["classes"] = d.nodes, d.roots, d.leaf_value or 0, d.classes
             sg["n_trees"], sg["n_classes"], sg["n_nodes"], sg["pure"] = d.n_trees, d.n_classes, d.n_nodes, d.pure
+            sg["cforest"], sg["cf_slots"], sg["cf_vote_regs"] = d.cforest or 0, d.cf_slots, d.cf_vote_regs
+            sg["cf_leaves"] = d.cf_leaves
         t2 = time.perf_counter()
         host += t2 - t1
         t1 = t2
@@ -438,7 +440,7 @@ class BatchRunner:
             p0, p1 = int(self.off_h[ps.i]), int(self.end_h[ps.i])
             st.predicted_rows += p1 - p0
             if self.timing:
-                st.predict_bytes += (p1 - p0) * (4 * ps.forest.packed.features_used + 6)
+                st.predict_bytes += (p1 - p0) * (4 * ps.forest.features_read + 6)
                 st.scan_rows += min(p1, ps.base + (ps_last + 1) * pb) - p0
             with torch.cuda.stream(stream):
                 if nev:

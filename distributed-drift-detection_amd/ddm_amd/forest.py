@@ -1,19 +1,68 @@
-"""Device-resident forests for ddm_forest_predict (layout: treepack.py)."""
+"""Device-resident forests for ddm_forest_predict (layout: treepack.py).
+
+A pure forest is also compiled (ddm_forest_compile, csrc/forest_compile.cpp) into the
+blob the fast predict kernels read; forests the compiler rejects (impure, > 64 leaves
+in a tree, > 16 classes, > 32 feature columns) are predicted by the node-walk kernels.
+"""
+import ctypes
+
+import numpy as np
 import torch
 
-from ._capi import DdmForest
+from ._capi import DDM_E_FOREST, DdmForest, check, lib
 from .treepack import MAX_CLASSES, MISSING_LEFT_BIT, NODE_DTYPE, PackedForest, pack, pack_sklearn, tree_arrays  # noqa: F401
+
+# ddm_cforest_head (include/ddm_amd.h): the leading int32 fields
+_HEAD_FIELDS = ("n_slots", "n_classes", "vote_regs", "n_stumps", "n_general", "n_leaves", "total_bytes",
+                "any_nanleft")
+
+
+def compile_forest(packed):
+    """The compiled blob (uint8 numpy) and its header fields, or (None, None) when the
+    forest is not compilable."""
+    if not packed.pure:
+        return None, None
+    nodes = np.ascontiguousarray(packed.nodes)
+    roots = np.ascontiguousarray(packed.roots, dtype=np.int32)
+    classes = np.ascontiguousarray(packed.classes, dtype=np.int32)
+    size = ctypes.c_int64()
+    args = (nodes.ctypes.data, len(nodes), roots.ctypes.data, len(roots), classes.ctypes.data, len(classes), 1)
+    rc = lib.ddm_forest_compile(*args, None, 0, ctypes.byref(size))
+    if rc == DDM_E_FOREST:
+        return None, None
+    check(rc, "ddm_forest_compile")
+    blob = np.zeros(size.value, dtype=np.uint8)
+    check(lib.ddm_forest_compile(*args, blob.ctypes.data, blob.size, ctypes.byref(size)), "ddm_forest_compile")
+    head = dict(zip(_HEAD_FIELDS, blob[:4 * len(_HEAD_FIELDS)].view(np.int32).tolist()))
+    return blob, head
 
 
 class DeviceForest:
-    """A PackedForest resident in HBM plus the ddm_forest descriptor pointing at it."""
+    """A PackedForest resident in HBM plus the ddm_forest descriptor pointing at it.
+    compiled=False keeps the node-walk kernels (tests compare both paths)."""
 
-    def __init__(self, packed, device):
+    def __init__(self, packed, device, compiled=True):
         self.packed = packed
         self.nodes = torch.from_numpy(packed.nodes.view('u1')).to(device, non_blocking=False)
         self.roots = torch.from_numpy(packed.roots).to(device)
         self.classes = torch.from_numpy(packed.classes).to(device)
         self.leaf_value = None if packed.pure else torch.from_numpy(packed.leaf_value).to(device)
+        blob, head = compile_forest(packed) if compiled else (None, None)
+        self.cforest = None if blob is None else torch.from_numpy(blob).to(device)
+        self.head = head
         self.desc = DdmForest(self.nodes.data_ptr(), self.roots.data_ptr(),
                               0 if packed.pure else self.leaf_value.data_ptr(), self.classes.data_ptr(),
-                              packed.n_trees, packed.n_classes, packed.n_nodes, 1 if packed.pure else 0)
+                              packed.n_trees, packed.n_classes, packed.n_nodes, 1 if packed.pure else 0,
+                              0 if blob is None else self.cforest.data_ptr(),
+                              head["n_slots"] if head else 0, head["vote_regs"] if head else 0,
+                              head["n_leaves"] if head else 0, 0)
+
+    @property
+    def compiled(self):
+        return self.cforest is not None
+
+    @property
+    def features_read(self):
+        """Feature columns one row loads: the compiled forest's slots, or every column a
+        node of the walk reads."""
+        return self.head["n_slots"] if self.head else self.packed.features_used

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 4
+#define DDM_AMD_ABI_VERSION 5
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -87,7 +87,56 @@ typedef struct ddm_forest {
     int32_t n_classes;           /* <= 64                                          */
     int32_t n_nodes;
     int32_t pure;                /* 1: every leaf is one-hot and n_trees <= 255    */
+    const uint8_t*  cforest;     /* device blob of ddm_forest_compile, or NULL: then the
+                                    node walk above is used                         */
+    int32_t cf_slots;            /* the blob's n_slots, vote_regs and n_leaves            */
+    int32_t cf_vote_regs;        /* (kernel choice and LDS size without reading the blob) */
+    int32_t cf_leaves;
+    int32_t cf_pad;
 } ddm_forest;
+
+/* ---- compiled forests (the fast predict path) -------------------------------------
+ * A pure forest whose trees have <= 64 leaves, <= 16 classes and <= 32 distinct feature
+ * columns is compiled on the host into one blob the predict kernels read with uniform
+ * (scalar) loads:
+ *   * the feature columns the forest reads become slots 0..n_slots-1 (a row loads only
+ *     those: 4*n_slots bytes of X per row);
+ *   * single-leaf trees fold into base_votes (u8 vote counters packed 4 per uint32);
+ *   * stumps (one split, two leaves), NaN-right ones first: vote += right ? delta : 0
+ *     with right = !(x <= thr) (NaN goes right) or x > thr (NaN goes left), thr the
+ *     float32 image of the float64 threshold (x <= thr32 <=> (double)x <= thr for every
+ *     float32 x) and base_votes already holding the left leaf's vote;
+ *   * other trees are evaluated QuickScorer-style: every internal node whose test sends
+ *     the row right clears the leaves of its left subtree from a 64-bit mask; the exit
+ *     leaf is the lowest surviving bit (leaves numbered left to right).
+ * Layout (byte offsets from the blob start, 16-byte aligned sections):
+ *   ddm_cforest_head | stumps u32[S][stump_words] ({float32 thr bits, slot, delta[vote_regs]},
+ *                                                  stump_words = 4 (vote_regs <= 2) or 8)
+ *   | trees ddm_cforest_tree[n_general] | nodes ddm_cforest_node[] | leaf class u8[n_leaves] */
+typedef struct ddm_cforest_head {
+    int32_t n_slots, n_classes, vote_regs, n_stumps;
+    int32_t n_general, n_leaves, total_bytes, any_nanleft;
+    int32_t stumps_off, stump_words, n_stumps_right, trees_off;  /* stumps [0, n_stumps_right)
+                                                                     send NaN right */
+    int32_t nodes_off, leafcls_off, pad0, pad1;
+    uint32_t base_votes[4];
+    int32_t cols[32];            /* feature column of each slot                          */
+    int32_t classes[16];         /* classes_ labels                                      */
+} ddm_cforest_head;
+
+typedef struct ddm_cforest_tree { int32_t node_begin, n_nodes, leaf_begin, n_leaves; } ddm_cforest_tree;
+typedef struct ddm_cforest_node {
+    float threshold; int32_t slot_nanleft;   /* slot | (NaN goes left) << 8 */
+    uint32_t left_lo, left_hi;               /* leaves of the left subtree   */
+} ddm_cforest_node;
+
+/* Compile a packed host forest (nodes/roots as ddm_forest describes; classes host int32).
+ * Returns 0 and *out_bytes = blob size when it fits `cap` (cap 0 / out NULL: size query),
+ * DDM_E_FOREST when the forest is not compilable (impure, > 64 leaves in a tree, > 16
+ * classes, > 32 feature columns): use the node walk. */
+int ddm_forest_compile(const ddm_node* nodes, int32_t n_nodes, const int32_t* roots, int32_t n_trees,
+                       const int32_t* classes, int32_t n_classes, int32_t pure, uint8_t* out,
+                       int64_t cap, int64_t* out_bytes);
 
 int ddm_abi_version(void);
 const char* ddm_last_error(void);
@@ -119,6 +168,9 @@ typedef struct ddm_predict_segment {
     int32_t n_trees, n_classes, n_nodes, pure;
     int64_t row_base;       /* row = (g / per_batch) * per_batch + perm[g] - row_base (g: position) */
     int64_t block0, nblocks;
+    const uint8_t* cforest; /* compiled forest (device) or NULL                              */
+    int32_t cf_slots, cf_vote_regs;   /* its n_slots, vote_regs, n_leaves                   */
+    int32_t cf_leaves, cf_pad;
 } ddm_predict_segment;
 
 int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, ddm_predict_segment* segs_dev,
