@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--features", type=int, default=27)
     ap.add_argument("--refit", default="native", choices=["native", "sklearn"],
                     help="native: ddm_rf_fit (identical trees to sklearn 1.7.2); sklearn: host sklearn")
-    ap.add_argument("--fit-threads", type=int, default=8, help="host threads for parallel native refits")
+    ap.add_argument("--fit-threads", type=int, default=16, help="host threads for the tree-parallel native refits")
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-sample-rows", type=int, default=150_000)
@@ -145,7 +145,8 @@ def run_c3(args, world, rank, dev, torch, dist):
     st = [runner.stats]
     agg = {k: sum(getattr(s, k) for s in st) for k in ("epochs", "refits", "predicted_rows", "refit_s",
                                                         "predict_ms", "predict_bytes", "scan_ms", "scan_rows",
-                                                        "shuffle_ms", "host_s", "gpu_s")}
+                                                        "shuffle_ms", "host_s", "gpu_s", "refit_fit_s",
+                                                        "refit_readback_s", "prep_s")}
     drifts = int(sum((r[:, 1] >= 0).sum() for r in results.values()))
     warns = int(sum((r[:, 0] >= 0).sum() for r in results.values()))
     rows_rank = n * args.parts * args.steps
@@ -161,8 +162,8 @@ def run_c3(args, world, rank, dev, torch, dist):
                     f"class blocks of {block} global rows, INSTANCES={instances} (row % INSTANCES), "
                     f"{args.parts} partitions x {n} rows per GPU",
         "rows_per_gpu_step": n * args.parts, "partitions_per_gpu": args.parts,
-        "refit": ("native ddm_rf_fit (sklearn 1.7.2 RandomForestClassifier restated, identical trees), "
-                  "refits of different partitions in parallel host threads") if args.refit == "native" else
+        "refit": ("native ddm_rf_fit_many (sklearn 1.7.2 RandomForestClassifier restated, identical trees), "
+                  f"all trees of an epoch's refits on {args.fit_threads} host threads") if args.refit == "native" else
                  "host sklearn RandomForestClassifier(100 trees), in-process",
         "shuffle": "batch shuffles generated on the GPU from the partition's MT19937 stream (ddm_shuffle_*)",
         "execution": "all partitions of the GPU in lockstep epochs: one batched shuffle, predict and scan "
@@ -175,7 +176,10 @@ def run_c3(args, world, rank, dev, torch, dist):
              "predict_kernel_ms_per_step": agg["predict_ms"] / args.steps,
              "scan_kernel_ms_per_step": agg["scan_ms"] / args.steps,
              "shuffle_kernels_ms_per_step": agg["shuffle_ms"] / args.steps,
-             "host_s_per_step": agg["host_s"] / args.steps, "gpu_wait_s_per_step": agg["gpu_s"] / args.steps}
+             "host_s_per_step": agg["host_s"] / args.steps, "gpu_wait_s_per_step": agg["gpu_s"] / args.steps,
+             "refit_native_fit_s_per_step": agg["refit_fit_s"] / args.steps,
+             "refit_readback_s_per_step": agg["refit_readback_s"] / args.steps,
+             "stream_prep_s_per_step": agg["prep_s"] / args.steps}
     roofline = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_from_profile("ddm_forest_predict", rows_per_launch),
                 "kernel": "ddm_forest_predict", "alg_bytes_per_row": "4*F_used + 6",

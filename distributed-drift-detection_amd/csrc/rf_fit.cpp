@@ -28,6 +28,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/ddm_amd.h"
@@ -35,28 +40,50 @@
 namespace {
 
 // ---- numpy legacy MT19937 seeded by init_genrand (RandomState(int)) -------------------
+// The twist is done lazily, word by word: new word i needs old words i, i+1 and i+397
+// (or the new word i-227), all available in order, so a tree pays for the ~130 words
+// its bootstrap draws instead of a full 624-word block.
 struct MT {
     uint32_t mt[624];
-    int pos;
+    int pos;          // next word to return
+    int twisted;      // words [0, twisted) of the current block are already regenerated
     explicit MT(uint32_t s) {
         mt[0] = s;
         for (int i = 1; i < 624; ++i) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
         pos = 624;
+        twisted = 624;
     }
-    uint32_t next() {
-        if (pos >= 624) {
-            for (int i = 0; i < 624; ++i) {
-                const uint32_t y = (mt[i] & 0x80000000u) | (mt[(i + 1) % 624] & 0x7fffffffu);
-                mt[i] = mt[(i + 397) % 624] ^ (y >> 1) ^ (-(y & 1u) & 0x9908b0dfu);
-            }
-            pos = 0;
+    uint32_t raw(int i) {                       // word i of the next block, twisting on demand
+        while (twisted <= i) {
+            const int k = twisted++;
+            const uint32_t y = (mt[k] & 0x80000000u) | (mt[(k + 1) % 624] & 0x7fffffffu);
+            mt[k] = mt[(k + 397) % 624] ^ (y >> 1) ^ (-(y & 1u) & 0x9908b0dfu);
         }
-        uint32_t y = mt[pos++];
+        return mt[i];
+    }
+    static uint32_t temper(uint32_t y) {
         y ^= y >> 11;
         y ^= (y << 7) & 0x9d2c5680u;
         y ^= (y << 15) & 0xefc60000u;
         y ^= y >> 18;
         return y;
+    }
+    uint32_t next() {
+        if (pos >= 624) {
+            if (twisted < 624) raw(623);            // finish the block before starting another
+            pos = 0;
+            twisted = 0;
+        }
+        return temper(raw(pos++));
+    }
+    // tempered word k positions ahead of the next one (k small), without consuming it
+    uint32_t peek(int k) {
+        if (pos >= 624) {
+            if (twisted < 624) raw(623);
+            pos = 0;
+            twisted = 0;
+        }
+        return temper(raw(pos + k));
     }
     uint32_t interval(uint32_t mx) {
         if (mx == 0) return 0;
@@ -256,13 +283,19 @@ struct Builder {
     }
 
     void build(uint32_t seed, Tree& t) {
-        // bootstrap (ensemble/_forest.py _generate_sample_indices)
+        // bootstrap (ensemble/_forest.py _generate_sample_indices) and the splitter seed,
+        // which is the first randint(0, 2**31-1) of a fresh RandomState(seed)
+        // (tree/_classes.py check_random_state): the same stream, so it is peeked from the
+        // bootstrap generator before that consumes anything
         MT boot(seed);
+        {
+            int k = 0;
+            uint32_t v;
+            while ((v = boot.peek(k) & 0x7fffffffu) > kRandRMax - 1u) ++k;
+            rand_r_state = v;
+        }
         std::fill(w.begin(), w.end(), 0.0);
         for (int i = 0; i < n; ++i) w[boot.interval((uint32_t)(n - 1))] += 1.0;
-        // splitter RNG: a fresh RandomState(seed) (tree/_classes.py check_random_state)
-        MT split_rs(seed);
-        rand_r_state = split_rs.interval(kRandRMax - 1u);
         samples.clear();
         weighted_n_samples = 0.0;
         for (int i = 0; i < n; ++i) {
@@ -314,54 +347,13 @@ struct Builder {
     }
 };
 
-}  // namespace
-
-extern "C" int ddm_rf_fit(const float* X, int32_t n, int32_t n_features, const int32_t* y_idx, int32_t n_classes,
-                          const int64_t* seeds, int32_t n_trees, int32_t max_features, ddm_node* nodes,
-                          int64_t nodes_cap, int32_t* roots, double* leaf_value, int64_t leaf_rows_cap,
-                          int64_t* out_info) {
-    if (!X || !y_idx || !seeds || !nodes || !roots || !out_info || n <= 0 || n_features <= 0 || n_classes <= 0 ||
-        n_trees <= 0 || max_features <= 0 || nodes_cap < (int64_t)n_trees * (2 * (int64_t)n - 1))
-        return DDM_E_ARG;
-    for (int64_t i = 0; i < (int64_t)n * n_features; ++i)
-        if (X[i] != X[i]) return DDM_E_NAN;
-    for (int i = 0; i < n; ++i)
-        if (y_idx[i] < 0 || y_idx[i] >= n_classes) return DDM_E_ARG;
-    Builder b;
-    b.X = X;
-    b.n = n;
-    b.F = n_features;
-    b.K = n_classes;
-    b.max_features = max_features;
-    b.y = y_idx;
-    b.w.assign(n, 0.0);
-    b.fv.assign(n, 0.0f);
-    b.features.assign(n_features, 0);
-    b.constant.assign(n_features, 0);
-    b.sum_total.assign(n_classes, 0.0);
-    b.sum_left.assign(n_classes, 0.0);
-    b.sum_right.assign(n_classes, 0.0);
-    b.samples.reserve(n);
-    std::vector<Tree> trees(n_trees);
-    bool pure = n_trees <= 255;
-    for (int t = 0; t < n_trees; ++t) {
-        b.build((uint32_t)seeds[t], trees[t]);
-        const Tree& tr = trees[t];
-        for (size_t u = 0; pure && u < tr.left.size(); ++u) {
-            if (tr.left[u] != -1) continue;
-            int ones = 0, others = 0;
-            for (int c = 0; c < n_classes; ++c) {
-                const double v = tr.value[u * n_classes + c];
-                ones += v == 1.0;
-                others += (v != 0.0 && v != 1.0);
-            }
-            pure = (ones == 1 && others == 0);
-        }
-    }
-    // pack: BFS renumbering with adjacent siblings (treepack.py:pack)
+// Pack trees into the ddm_node layout: BFS renumbering with adjacent siblings
+// (treepack.py:pack).  Returns 0 or DDM_E_IMPURE (leaf_value missing / too small).
+int pack_trees(const std::vector<Tree>& trees, int n_classes, bool pure, ddm_node* nodes, int32_t* roots,
+               double* leaf_value, int64_t leaf_rows_cap, int64_t* out_info) {
     int64_t base = 0, leaf_rows = 0;
     std::vector<int64_t> order, new_id;
-    for (int t = 0; t < n_trees; ++t) {
+    for (size_t t = 0; t < trees.size(); ++t) {
         const Tree& tr = trees[t];
         const int64_t m = (int64_t)tr.left.size();
         new_id.assign(m, 0);
@@ -404,5 +396,203 @@ extern "C" int ddm_rf_fit(const float* X, int32_t n, int32_t n_features, const i
     out_info[0] = base;
     out_info[1] = pure ? 1 : 0;
     out_info[2] = leaf_rows;
+    return 0;
+}
+
+bool tree_is_pure(const Tree& tr, int n_classes) {
+    for (size_t u = 0; u < tr.left.size(); ++u) {
+        if (tr.left[u] != -1) continue;
+        int ones = 0, others = 0;
+        for (int c = 0; c < n_classes; ++c) {
+            const double v = tr.value[u * n_classes + c];
+            ones += v == 1.0;
+            others += (v != 0.0 && v != 1.0);
+        }
+        if (!(ones == 1 && others == 0)) return false;
+    }
+    return true;
+}
+
+void builder_init(Builder& b, const float* X, int n, int F, const int32_t* y, int K, int max_features) {
+    b.X = X;
+    b.n = n;
+    b.F = F;
+    b.K = K;
+    b.max_features = max_features;
+    b.y = y;
+    b.w.assign(n, 0.0);
+    b.fv.assign(n, 0.0f);
+    b.features.assign(F, 0);
+    b.constant.assign(F, 0);
+    b.sum_total.assign(K, 0.0);
+    b.sum_left.assign(K, 0.0);
+    b.sum_right.assign(K, 0.0);
+    b.samples.reserve(n);
+}
+
+int check_inputs(const float* X, int32_t n, int32_t n_features, const int32_t* y_idx, int32_t n_classes) {
+    for (int64_t i = 0; i < (int64_t)n * n_features; ++i)
+        if (X[i] != X[i]) return DDM_E_NAN;
+    for (int i = 0; i < n; ++i)
+        if (y_idx[i] < 0 || y_idx[i] >= n_classes) return DDM_E_ARG;
+    return 0;
+}
+
+// ---- a small persistent worker pool for ddm_rf_fit_many ------------------------------
+class Pool {
+  public:
+    // Runs fn(i) for i in [0, n) on up to `threads` threads (the caller included).
+    void run(int threads, int64_t n, const std::function<void(int64_t)>& fn) {
+        if (threads <= 1 || n <= 1) {
+            for (int64_t i = 0; i < n; ++i) fn(i);
+            return;
+        }
+        std::unique_lock<std::mutex> lk(mu_);     // one batch at a time
+        ensure(threads - 1);
+        fn_ = &fn;
+        n_ = n;
+        next_.store(0);
+        active_ = (int)std::min<int64_t>(threads - 1, (int64_t)workers_.size());
+        done_ = 0;
+        ++gen_;
+        cv_.notify_all();
+        lk.unlock();
+        drain();
+        lk.lock();
+        cv_done_.wait(lk, [&] { return done_ == active_; });
+        fn_ = nullptr;
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+
+  private:
+    void ensure(int k) {
+        while ((int)workers_.size() < k) {
+            const int id = (int)workers_.size();
+            workers_.emplace_back([this, id] { loop(id); });
+        }
+    }
+    void drain() {
+        for (;;) {
+            const int64_t i = next_.fetch_add(1);
+            if (i >= n_) break;
+            (*fn_)(i);
+        }
+    }
+    void loop(int id) {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            if (id >= active_) continue;
+            lk.unlock();
+            drain();
+            lk.lock();
+            if (++done_ == active_) cv_done_.notify_all();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_, cv_done_;
+    std::vector<std::thread> workers_;
+    const std::function<void(int64_t)>* fn_ = nullptr;
+    std::atomic<int64_t> next_{0};
+    int64_t n_ = 0;
+    int active_ = 0, done_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+Pool& pool() {
+    static Pool p;
+    return p;
+}
+
+}  // namespace
+
+extern "C" int ddm_rf_fit(const float* X, int32_t n, int32_t n_features, const int32_t* y_idx, int32_t n_classes,
+                          const int64_t* seeds, int32_t n_trees, int32_t max_features, ddm_node* nodes,
+                          int64_t nodes_cap, int32_t* roots, double* leaf_value, int64_t leaf_rows_cap,
+                          int64_t* out_info) {
+    if (!X || !y_idx || !seeds || !nodes || !roots || !out_info || n <= 0 || n_features <= 0 || n_classes <= 0 ||
+        n_trees <= 0 || max_features <= 0 || nodes_cap < (int64_t)n_trees * (2 * (int64_t)n - 1))
+        return DDM_E_ARG;
+    if (int rc = check_inputs(X, n, n_features, y_idx, n_classes)) return rc;
+    Builder b;
+    builder_init(b, X, n, n_features, y_idx, n_classes, max_features);
+    std::vector<Tree> trees(n_trees);
+    bool pure = n_trees <= 255;
+    for (int t = 0; t < n_trees; ++t) {
+        b.build((uint32_t)seeds[t], trees[t]);
+        pure = pure && tree_is_pure(trees[t], n_classes);
+    }
+    return pack_trees(trees, n_classes, pure, nodes, roots, leaf_value, leaf_rows_cap, out_info);
+}
+
+extern "C" int ddm_rf_fit_many(ddm_fit_job* jobs, int32_t n_jobs, int32_t n_threads) {
+    if (!jobs || n_jobs < 0) return DDM_E_ARG;
+    std::vector<std::vector<Tree>> trees(n_jobs);
+    std::vector<int64_t> first(n_jobs + 1, 0);
+    for (int j = 0; j < n_jobs; ++j) {
+        ddm_fit_job& jb = jobs[j];
+        jb.status = 0;
+        jb.blob_bytes = 0;
+        if (!jb.X || !jb.y_idx || !jb.seeds || !jb.nodes || !jb.roots || !jb.classes || jb.n <= 0 ||
+            jb.n_features <= 0 || jb.n_classes <= 0 || jb.n_trees <= 0 || jb.max_features <= 0 ||
+            jb.nodes_cap < (int64_t)jb.n_trees * (2 * (int64_t)jb.n - 1))
+            jb.status = DDM_E_ARG;
+        else
+            jb.status = check_inputs(jb.X, jb.n, jb.n_features, jb.y_idx, jb.n_classes);
+        trees[j].resize(jb.status ? 0 : jb.n_trees);
+        first[j + 1] = first[j] + (int64_t)trees[j].size();
+    }
+    // every (job, tree) is an independent task
+    // each thread keeps one Builder, re-initialised when it moves to another job (or call)
+    static std::atomic<uint64_t> calls{0};
+    const uint64_t call = ++calls;
+    static thread_local Builder tb;
+    static thread_local uint64_t tb_call = 0;
+    static thread_local int tb_job = -1;
+    pool().run(std::max(1, (int)n_threads), first[n_jobs], [&](int64_t task) {
+        const int j = (int)(std::upper_bound(first.begin(), first.end(), task) - first.begin()) - 1;
+        const ddm_fit_job& jb = jobs[j];
+        if (tb_call != call || tb_job != j) {
+            builder_init(tb, jb.X, jb.n, jb.n_features, jb.y_idx, jb.n_classes, jb.max_features);
+            tb_call = call;
+            tb_job = j;
+        }
+        const int t = (int)(task - first[j]);
+        tb.build((uint32_t)jb.seeds[t], trees[j][t]);
+    });
+    // pack + compile each job
+    pool().run(std::max(1, (int)n_threads), n_jobs, [&](int64_t j) {
+        ddm_fit_job& jb = jobs[j];
+        if (jb.status) return;
+        bool pure = jb.n_trees <= 255;
+        for (const Tree& t : trees[j]) pure = pure && tree_is_pure(t, jb.n_classes);
+        jb.status = pack_trees(trees[j], jb.n_classes, pure, jb.nodes, jb.roots, jb.leaf_value, jb.leaf_rows_cap,
+                               jb.info);
+        if (jb.status || !jb.blob) return;
+        int64_t bytes = 0;
+        const int rc = ddm_forest_compile(jb.nodes, (int32_t)jb.info[0], jb.roots, jb.n_trees, jb.classes,
+                                          jb.n_classes, (int32_t)jb.info[1], jb.blob, jb.blob_cap, &bytes);
+        if (rc == 0) {
+            jb.blob_bytes = bytes;
+            const ddm_cforest_head* h = reinterpret_cast<const ddm_cforest_head*>(jb.blob);
+            jb.cf_slots = h->n_slots;
+            jb.cf_vote_regs = h->vote_regs;
+            jb.cf_leaves = h->n_leaves;
+        }
+    });
+    for (int j = 0; j < n_jobs; ++j)
+        if (jobs[j].status) return jobs[j].status;
     return 0;
 }

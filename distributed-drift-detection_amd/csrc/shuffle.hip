@@ -115,27 +115,32 @@ __global__ __launch_bounds__(256) void k_mt_generate_batch(const GenJob* __restr
     mt_generate(j.state, j.R, j.n);
 }
 
-// Tsub[sub][s-1] = end_state | batches_done << 8, for s in [1, L-1].
+// Tsub[sub][s-1] = end_state | batches_done << 8, for s in [1, L-1].  A 256-thread block
+// serves 256 / G sub-chunks at once, G = the start states rounded up to a wave multiple
+// (L = 100: two sub-chunks of 99 states per block, 77% of the lanes busy).
 __global__ __launch_bounds__(256) void k_fsm_sub(const uint32_t* __restrict__ R, int64_t sub0, int64_t nsub,
                                                  int L, uint16_t* __restrict__ Tsub) {
-    __shared__ uint32_t draws[kSub];
+    __shared__ uint32_t draws[4][kSub];
     const int S = L - 1;
-    for (int64_t sb = sub0 + blockIdx.x; sb < sub0 + nsub; sb += gridDim.x) {
+    const int G = (S + 63) & ~63;               // lanes per sub-chunk
+    const int per = 256 / G >= 1 ? 256 / G : 1; // sub-chunks per block (1, 2 or 4)
+    const int q = threadIdx.x / G, lane_s = threadIdx.x % G;
+    for (int64_t sb0 = sub0 + (int64_t)blockIdx.x * per; sb0 < sub0 + nsub; sb0 += (int64_t)gridDim.x * per) {
         __syncthreads();
-        if (threadIdx.x < kSub) draws[threadIdx.x] = R[sb * kSub + threadIdx.x];
+        for (int k = threadIdx.x; k < per * kSub; k += 256) {
+            const int64_t sb = sb0 + k / kSub;
+            draws[k / kSub][k % kSub] = sb < sub0 + nsub ? R[sb * kSub + k % kSub] : 0u;
+        }
         __syncthreads();
-        for (int s0 = threadIdx.x + 1; s0 <= S; s0 += 256) {
+        const int64_t sb = sb0 + q;
+        if (q >= per || sb >= sub0 + nsub) continue;
+        for (int s0 = lane_s + 1; s0 <= S; s0 += G) {
             uint32_t s = (uint32_t)s0, done = 0;
             for (int k = 0; k < kSub; ++k) {
-                const bool acc = (draws[k] & imask(s)) <= s;
-                if (acc) {
-                    if (s == 1) {
-                        s = (uint32_t)S;
-                        ++done;
-                    } else {
-                        --s;
-                    }
-                }
+                const bool acc = (draws[q][k] & imask(s)) <= s;
+                const bool wrap = acc && s == 1;
+                done += wrap ? 1u : 0u;
+                s = wrap ? (uint32_t)S : (acc ? s - 1 : s);
             }
             Tsub[sb * S + (s0 - 1)] = (uint16_t)(s | (done << 8));
         }

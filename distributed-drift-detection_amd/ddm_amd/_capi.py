@@ -69,6 +69,7 @@ SIGNATURES = {
     "ddm_mt_skip": (ctypes.c_int, [_vp, _pi32, _i64]),
     "ddm_forest_compile": (ctypes.c_int, [_vp, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _i64,
                                           ctypes.POINTER(ctypes.c_int64)]),
+    "ddm_rf_fit_many": (ctypes.c_int, [_vp, _i32, _i32]),
     "ddm_rf_fit": (ctypes.c_int, [_vp, _i32, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp]),
     "ddm_synth_block_labels": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i32, _vp]),
     "ddm_synth_features": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _i64, _i64, _u64, _f32, _vp]),

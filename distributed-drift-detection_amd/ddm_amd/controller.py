@@ -28,11 +28,11 @@ import pandas as pd
 import torch
 
 from . import kernels
-from .forest import DeviceForest
+from .forest import upload_forests
 from .params import OUTPUT_COLUMNS, DDMSettings, infer_x_features
 from .rng import MTStream
-from .shuffle import GpuShuffle, expected_draws_per_batch
-from .trainer import NativeForestTrainer
+from .shuffle import GpuShuffle, expected_draws_per_batch, fy_from_words, randint31_from_words
+from .trainer import BatchForestTrainer
 
 def _round_up(n, m):
     return (n + m - 1) // m * m
@@ -100,12 +100,14 @@ def sklearn_refit(settings):
 
 class RunStats:
     __slots__ = ("epochs", "refits", "predicted_rows", "refit_s", "gpu_s", "host_s", "predict_ms", "predict_bytes",
-                 "scan_ms", "scan_rows", "shuffle_ms", "sklearn_refits")
+                 "scan_ms", "scan_rows", "shuffle_ms", "sklearn_refits", "refit_fit_s", "refit_readback_s",
+                 "prep_s")
 
     def __init__(self):
         self.epochs = self.refits = self.predicted_rows = self.predict_bytes = self.scan_rows = 0
         self.sklearn_refits = 0
         self.refit_s = self.gpu_s = self.host_s = self.predict_ms = self.scan_ms = self.shuffle_ms = 0.0
+        self.refit_fit_s = self.refit_readback_s = self.prep_s = 0.0
 
     def as_dict(self):
         return {k: getattr(self, k) for k in self.__slots__}
@@ -129,9 +131,9 @@ class BatchRunner:
     Partitions are independent (DDM_Process.py:226 groups by device_id), so a partition
     that is done simply drops out of the tables.
 
-    refit: "native" (ddm_rf_fit, identical trees to sklearn 1.7.2; sklearn itself for NaN
-    inputs) or "sklearn".  Refits of different partitions run in parallel threads (the
-    native fit releases the GIL)."""
+    refit: "native" (ddm_rf_fit_many, identical trees to sklearn 1.7.2; sklearn itself for
+    NaN inputs) or "sklearn".  The native refits of all partitions that drifted in an
+    epoch are one call: every tree on a pool of `fit_threads` host threads."""
 
     def __init__(self, parts, settings=None, stream=None, refit="native", timing=False, fit_threads=8):
         self.parts = list(parts)
@@ -148,7 +150,8 @@ class BatchRunner:
         pb = self.s.per_batch
         if not 2 <= pb <= 256:
             raise ValueError("per_batch must be in [2, 256] on the device path")
-        self.trainers = [NativeForestTrainer(self.s.n_estimators) for _ in self.parts]
+        self.batch_trainer = BatchForestTrainer(self.s.n_estimators, self.fit_threads)
+        self.words_h = None
         self.sk_refit = sklearn_refit(self.s)
         self.timing = timing
         # HIP events recorded by the C-ABI right around each batched launch
@@ -196,35 +199,51 @@ class BatchRunner:
         self.bbase_h[:] = self.ev_bases
         self.segs = kernels.PinnedTable(kernels.SEG_DTYPE, n, dev)
         self.jobs = kernels.PinnedTable(kernels.JOB_DTYPE, n, dev)
-        self.gens = kernels.PinnedTable(kernels.GEN_DTYPE, n, dev)
+        # the partitions' MT19937 streams are generated and tabulated on a side stream, in
+        # pieces, while the epochs run (GpuShuffle.wait_for orders the consumers)
+        self.gen_stream = torch.cuda.Stream(dev)
+        self.gen_tables = []
         # pinned staging per partition: [0] batch-j shuffle of a refit epoch, [1] short last
         # batch, [2] drift batch's shuffle read back
         self.small_h = [[torch.empty(256, dtype=torch.uint8, pin_memory=True) for _ in range(3)] for _ in self.parts]
         self.shuffles = []
         for part, nb, mw in zip(self.parts, self.nbs, self.max_wins):
             cap = int(nb * expected_draws_per_batch(pb) * 1.2) + 64 * 1024
-            self.shuffles.append(GpuShuffle(dev, pb, cap, mw, self.stream))
+            self.shuffles.append(GpuShuffle(dev, pb, cap, mw, self.stream, self.gen_stream))
         self.stats = RunStats()
 
     # -- helpers
     def _dptr(self, off, i, size):
         return self.ctrl_d.data_ptr() + off + size * i
 
-    def _ensure_all(self, wants):
-        """wants: [(partition index, draws needed)] -> one batched generate launch + tables."""
+    def _ensure_all(self, wants, wait=True):
+        """wants: [(partition index, draws needed)].  Partitions whose enqueued stream falls
+        short get one batched generate launch plus their tables on the side stream, closed
+        by one event; then (wait=True) the epoch stream waits for what it will read."""
         reqs, tabs = [], []
         for i, upto in wants:
-            req, need = self.shuffles[i].gen_request(upto)
-            if req is not None:
-                reqs.append(req)
-            tabs.append((i, need))
+            sh = self.shuffles[i]
+            if sh.chunks_for(upto) > sh.tab:
+                req, need = sh.gen_request(upto)
+                if req is not None:
+                    reqs.append(req)
+                tabs.append((i, need))
         if reqs:
-            rec = self.gens.rec
+            table = kernels.PinnedTable(kernels.GEN_DTYPE, len(reqs), self.device)   # read by the async copy
             for k, (st, R, cnt) in enumerate(reqs):
-                rec[k] = (st, R, cnt)
-            kernels.shuffle_generate_batch(self.gens, len(reqs), self.stream)
-        for i, need in tabs:
-            self.shuffles[i].tables_to(need)
+                table.rec[k] = (st, R, cnt)
+            kernels.shuffle_generate_batch(table, len(reqs), self.gen_stream)
+            self.gen_tables.append(table)
+        if tabs:
+            for i, need in tabs:
+                self.shuffles[i].tables_to(need)
+            ev = torch.cuda.Event()
+            ev.record(self.gen_stream)
+            for i, _ in tabs:
+                self.shuffles[i].mark_ready(ev)
+        if wait:
+            for i, upto in wants:
+                self.shuffles[i].wait_for(upto)
 
     def _upload_perm(self, i, b, perm, slot):
         pb = self.s.per_batch
@@ -234,41 +253,79 @@ class BatchRunner:
         with torch.cuda.stream(self.stream):
             self.perm_all[at:at + len(perm)].copy_(h[:len(perm)], non_blocking=True)
 
-    def _fit_one(self, i, X32, y, seeds, P_seeds):
-        packed = None
-        if self.refit_kind == "native":
-            packed = self.trainers[i].fit(X32, y, seeds)
-        if packed is None:                    # sklearn requested, or NaN in X (missing values)
-            packed = self.sk_refit(X32, y, self.shuffles[i].numpy_state(P_seeds))
-            return packed, True
-        return packed, False
-
     def _refits(self, need):
-        """Refit every partition in `need` on its drift batch (train_rows, shuffled order)."""
-        st, T = self.stats, self.s.n_estimators
+        """Refit every partition in `need` on its drift batch (train_rows, shuffled order).
+
+        One read-back serves all of them: the stream words from each P (batch j's shuffle,
+        then the T tree seeds, DDM_Process.py:190,:102) and the drift batches' rows; the
+        native fits of all partitions run tree-parallel in one call (ddm_rf_fit_many) and
+        the forests go back to HBM in one copy."""
+        st, T, pb = self.stats, self.s.n_estimators, self.s.per_batch
         t0 = time.perf_counter()
-        work = []
+        n_words = 3 * pb + T + 64
+        if self.words_h is None or self.words_h.shape[0] < len(need):
+            self.words_h = torch.empty((len(self.parts), n_words), dtype=torch.int32, pin_memory=True)
         for ps in need:
+            self.shuffles[ps.i].ensure(ps.P + n_words)
+        rows_dev = []
+        with torch.cuda.stream(self.stream):
+            for k, ps in enumerate(need):
+                sh = self.shuffles[ps.i]
+                self.words_h[k].copy_(sh.R[ps.P:ps.P + n_words], non_blocking=True)
+                part = self.parts[ps.i]
+                if part.host_X32 is None:
+                    idx_h = torch.from_numpy(np.asarray(ps.train_rows, dtype=np.int64)).pin_memory()
+                    idx = idx_h.to(self.device, non_blocking=True)
+                    xh = torch.empty((len(idx_h), part.X.shape[0]), dtype=torch.float32, pin_memory=True)
+                    yh = torch.empty(len(idx_h), dtype=torch.int32, pin_memory=True)
+                    xh.copy_(part.X.t().index_select(0, idx), non_blocking=True)
+                    yh.copy_(part.y.index_select(0, idx), non_blocking=True)
+                    rows_dev.append((xh, yh, idx_h))
+                else:
+                    rows_dev.append(None)
+        self.stream.synchronize()
+        t1 = time.perf_counter()
+        st.refit_readback_s += t1 - t0
+        work = []
+        for k, ps in enumerate(need):
             sh = self.shuffles[ps.i]
-            permj, ps.P = sh.host_perm(ps.P, ps.blen(ps.j))     # batch_b.sample before the fit (:190, :194)
-            self._upload_perm(ps.i, ps.j, permj, 0)
-            P_seeds = ps.P
-            seeds, ps.P = sh.host_seeds(P_seeds, T)              # 100 tree seeds follow the shuffle
+            words = self.words_h[k].numpy().view(np.uint32)
+            L = ps.blen(ps.j)
+            r = fy_from_words(words, L)
+            seeds = None if r is None else randint31_from_words(words[r[1]:], T)
+            if r is None or seeds is None:                      # rejections ran past the read-back
+                permj, P1 = sh.host_perm(ps.P, L)
+                seeds, P2 = sh.host_seeds(P1, T)
+            else:
+                permj, P1 = r[0], ps.P + r[1]
+                seeds, P2 = seeds[0], P1 + seeds[1]
+            self._upload_perm(ps.i, ps.j, permj, 0)             # batch_b.sample before the fit (:190, :194)
+            P_seeds, ps.P = P1, P2                              # 100 tree seeds follow the shuffle
             ps.P_after_first = ps.P
-            X32, y = self.parts[ps.i].rows(ps.train_rows, self.stream)
+            if rows_dev[k] is None:
+                X32, y = self.parts[ps.i].rows(ps.train_rows, self.stream)
+            else:
+                X32, y = rows_dev[k][0].numpy(), rows_dev[k][1].numpy().astype(np.int64)
             work.append((ps, X32, y, seeds, P_seeds))
-        if self.refit_kind == "native" and len(work) > 1 and self.fit_threads > 1:
-            pool = self._pool()
-            res = list(pool.map(lambda w: self._fit_one(w[0].i, *w[1:]), work))
-        else:
-            res = [self._fit_one(w[0].i, *w[1:]) for w in work]
-        for (ps, *_), (packed, used_sk) in zip(work, res):
-            ps.forest = DeviceForest(packed, self.device)
+        fits = [None] * len(work)
+        if self.refit_kind == "native":
+            t2 = time.perf_counter()
+            fits = self.batch_trainer.fit_many([(X32, y, seeds) for _, X32, y, seeds, _ in work])
+            st.refit_fit_s += time.perf_counter() - t2
+        entries = []
+        for (ps, X32, y, seeds, P_seeds), fit in zip(work, fits):
+            if fit is None:                    # sklearn requested, or NaN in X (missing values)
+                entries.append((self.sk_refit(X32, y, self.shuffles[ps.i].numpy_state(P_seeds)), None, None))
+                st.sklearn_refits += 1
+            else:
+                entries.append(fit)
+        forests = upload_forests(entries, self.device, self.stream)
+        for (ps, *_), f in zip(work, forests):
+            ps.forest = f
             ps.retrain = False
             ps.state = kernels.fresh_states(1)                  # ddm = None -> new DDM (:136-139)
             ps.g0 = ps.j + 1
             ps.seg_start = ps.j
-            st.sklearn_refits += int(used_sk)
         st.refits += len(work)
         st.refit_s += time.perf_counter() - t0
 
@@ -322,7 +379,20 @@ class BatchRunner:
         try:
             # each partition's whole stream up front (one batched generate + tables);
             # windows extend it if drifts (100 seed draws each) push it further
-            self._ensure_all([(ps.i, int(ps.nb * expected_draws_per_batch(pb) * 1.02)) for ps in pss])
+            # the whole stream of every partition, in growing pieces on the side stream: the
+            # first epochs only wait for the first piece
+            tp = time.perf_counter()
+            self.gen_tables = []
+            total = max(int(ps.nb * expected_draws_per_batch(pb) * 1.02) for ps in pss)
+            upto = 1 << 19
+            while True:
+                self._ensure_all([(ps.i, min(upto, int(ps.nb * expected_draws_per_batch(pb) * 1.02))) for ps in pss],
+                                 wait=False)
+                if upto >= total:
+                    break
+                upto = min(total, upto * 4)
+            if self.timing:
+                st.prep_s += time.perf_counter() - tp
             for ps in pss:
                 perm0, ps.P = self.shuffles[ps.i].host_perm(0, ps.blen(0))   # batches[0].sample (:187)
                 started.append(ps)
@@ -501,8 +571,8 @@ class BatchRunner:
 class PartitionRunner(BatchRunner):
     """One partition (the reference's per-UDF-call unit) on one HIP stream."""
 
-    def __init__(self, part, settings=None, stream=None, refit="native", timing=False):
-        super().__init__([part], settings, stream, refit, timing, fit_threads=1)
+    def __init__(self, part, settings=None, stream=None, refit="native", timing=False, fit_threads=8):
+        super().__init__([part], settings, stream, refit, timing, fit_threads=fit_threads)
         self.part = part
 
     def run(self, rng):

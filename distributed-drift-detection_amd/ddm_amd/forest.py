@@ -57,6 +57,21 @@ class DeviceForest:
                               head["n_slots"] if head else 0, head["vote_regs"] if head else 0,
                               head["n_leaves"] if head else 0, 0)
 
+    @classmethod
+    def from_buffer(cls, packed, blob, head, dev, off, host_keepalive=None):
+        """A forest whose arrays live in a shared device buffer at byte offsets `off`."""
+        f = cls.__new__(cls)
+        f.packed, f.head, f._buf, f._host = packed, head, dev, host_keepalive
+        base = dev.data_ptr()
+        f.nodes = f.roots = f.classes = f.leaf_value = None
+        f.cforest = None if blob is None else dev[off["blob"]:off["blob"] + blob.size]
+        f.desc = DdmForest(base + off["nodes"], base + off["roots"], 0 if packed.pure else base + off["leaf"],
+                           base + off["classes"], packed.n_trees, packed.n_classes, packed.n_nodes,
+                           1 if packed.pure else 0, 0 if blob is None else base + off["blob"],
+                           head["n_slots"] if head else 0, head["vote_regs"] if head else 0,
+                           head["n_leaves"] if head else 0, 0)
+        return f
+
     @property
     def compiled(self):
         return self.cforest is not None
@@ -66,3 +81,36 @@ class DeviceForest:
         """Feature columns one row loads: the compiled forest's slots, or every column a
         node of the walk reads."""
         return self.head["n_slots"] if self.head else self.packed.features_used
+
+
+def upload_forests(entries, device, stream):
+    """entries: [(PackedForest, blob or None, head or None)] -> [DeviceForest], all copied
+    to HBM with ONE host->device transfer (a pinned staging buffer, 256-byte aligned
+    pieces); the device buffer is shared by the returned forests."""
+    pieces, layout = [], []
+    off = 0
+
+    def put(arr):
+        nonlocal off
+        b = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+        at = off
+        pieces.append((at, b))
+        off = (off + b.size + 255) & ~255
+        return at
+
+    for pf, blob, head in entries:
+        o = {"nodes": put(pf.nodes), "roots": put(pf.roots), "classes": put(pf.classes)}
+        o["leaf"] = None if pf.pure else put(pf.leaf_value)
+        o["blob"] = None if blob is None else put(blob)
+        layout.append(o)
+    host = torch.empty(max(off, 256), dtype=torch.uint8, pin_memory=True)
+    hn = host.numpy()
+    for at, b in pieces:
+        hn[at:at + b.size] = b
+    with torch.cuda.stream(stream):
+        dev = host.to(device, non_blocking=True)
+    # keep the staging buffer alive until the copy has run (the caller's stream orders it)
+    out = []
+    for (pf, blob, head), o in zip(entries, layout):
+        out.append(DeviceForest.from_buffer(pf, blob, head, dev, o, host))
+    return out

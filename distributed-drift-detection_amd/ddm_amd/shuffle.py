@@ -84,12 +84,17 @@ def randint31_from_words(words, T):
 
 
 class GpuShuffle:
-    """One partition's MT19937 stream resident in HBM, with FSM tables for batch length L."""
+    """One partition's MT19937 stream resident in HBM, with FSM tables for batch length L.
 
-    def __init__(self, device, L, capacity_draws, max_window, stream):
+    R and the tables are produced on `gen_stream` (by default the consuming `stream`
+    itself) in pieces, each closed by an event; consumers on `stream` wait on the event of
+    the piece that covers what they read (`wait_for`), so generation overlaps the epochs."""
+
+    def __init__(self, device, L, capacity_draws, max_window, stream, gen_stream=None):
         if not 2 <= L <= 256:
             raise ValueError("GPU shuffles need 2 <= batch length <= 256")
         self.device, self.L, self.S, self.stream = device, L, L - 1, stream
+        self.gen_stream = gen_stream or stream
         self.max_window = int(max_window)
         self.mt = torch.zeros(625, dtype=torch.int32, device=device)
         self._alloc(max(2 * CHUNK, int(capacity_draws)))
@@ -100,6 +105,8 @@ class GpuShuffle:
         self.E = torch.zeros(self.max_window, dtype=torch.int64, device=device)
         self.words_h = torch.empty(4096, dtype=torch.int32, pin_memory=True)
         self.gen = self.tab = 0
+        self.ready = []          # [(chunks covered by the tables, event)] in enqueue order
+        self.waited = 0          # chunks the consuming stream has waited for
         self.init_key = None
         self.init_pos = 624
 
@@ -109,10 +116,11 @@ class GpuShuffle:
         Ts = torch.empty(cap // SUB * self.S, dtype=torch.int16, device=self.device)
         Tc = torch.empty(cap // CHUNK * self.S, dtype=torch.int32, device=self.device)
         if getattr(self, "R", None) is not None and self.gen:
-            with torch.cuda.stream(self.stream):
-                R[:self.gen].copy_(self.R[:self.gen])
-                Ts[:self.tab * (CHUNK // SUB) * self.S].copy_(self.Tsub[:self.tab * (CHUNK // SUB) * self.S])
-                Tc[:self.tab * self.S].copy_(self.Tchunk[:self.tab * self.S])
+            torch.cuda.synchronize(self.device)          # rare: growth past the initial estimate
+            R[:self.gen].copy_(self.R[:self.gen])
+            Ts[:self.tab * (CHUNK // SUB) * self.S].copy_(self.Tsub[:self.tab * (CHUNK // SUB) * self.S])
+            Tc[:self.tab * self.S].copy_(self.Tchunk[:self.tab * self.S])
+            torch.cuda.synchronize(self.device)
         self.R, self.Tsub, self.Tchunk, self.cap = R, Ts, Tc, cap
 
     def reset(self, rng):
@@ -122,21 +130,31 @@ class GpuShuffle:
         st = np.empty(625, dtype=np.uint32)
         st[:624] = self.init_key
         st[624] = self.init_pos
-        with torch.cuda.stream(self.stream):
+        self.stream.synchronize()
+        self.gen_stream.synchronize()       # nothing of the previous run may still read R
+        with torch.cuda.stream(self.gen_stream):
             self.mt.copy_(torch.from_numpy(st.view(np.int32)))
-        self.gen = self.tab = 0
+        self.gen = self.tab = self.waited = 0
+        self.ready = []
 
     def _sp(self):
         return ctypes.c_void_p(self.stream.cuda_stream)
+
+    def _gp(self):
+        return ctypes.c_void_p(self.gen_stream.cuda_stream)
 
     def window_draws(self, W):
         """Draws a window of W batches may need (mean + 15% + slack; windows grow R on demand)."""
         return int(W * expected_draws_per_batch(self.L) * 1.15) + 4 * CHUNK
 
+    @staticmethod
+    def chunks_for(upto):
+        return (int(upto) + CHUNK - 1) // CHUNK + 1
+
     def gen_request(self, upto):
         """Grow R to cover draws [0, upto) plus one chunk; returns the (state, R, n) generate
-        job still to launch (or None) and the chunk count the tables must reach."""
-        need_chunks = (int(upto) + CHUNK - 1) // CHUNK + 1
+        job still to launch on gen_stream (or None) and the chunk count the tables must reach."""
+        need_chunks = self.chunks_for(upto)
         target = need_chunks * CHUNK
         if target > self.cap:
             self._alloc(max(target, int(self.cap * 1.5)))
@@ -147,25 +165,49 @@ class GpuShuffle:
         return req, need_chunks
 
     def tables_to(self, need_chunks):
+        """Tabulate up to need_chunks on gen_stream (after the words they read)."""
         if need_chunks > self.tab:
             check(lib.ddm_shuffle_tables(self.R.data_ptr(), self.tab, need_chunks - self.tab, self.L,
-                                         self.Tsub.data_ptr(), self.Tchunk.data_ptr(), self._sp()),
+                                         self.Tsub.data_ptr(), self.Tchunk.data_ptr(), self._gp()),
                   "ddm_shuffle_tables")
             self.tab = need_chunks
 
+    def mark_ready(self, event):
+        """Everything enqueued on gen_stream so far is complete once `event` fires."""
+        self.ready.append((self.tab, event))
+
+    def wait_for(self, upto):
+        """Make the consuming stream wait until draws [0, upto) and their tables exist."""
+        need = self.chunks_for(upto)
+        if need <= self.waited:
+            return
+        for cov, ev in self.ready:
+            if cov >= need:
+                if self.gen_stream is not self.stream:
+                    self.stream.wait_event(ev)
+                self.waited = cov
+                return
+        raise RuntimeError(f"draws up to {upto} were never enqueued (tables cover {self.tab} chunks)")
+
     def ensure(self, upto):
-        """Generate R and tabulate chunks so that draws [0, upto) are covered."""
-        req, need_chunks = self.gen_request(upto)
-        if req is not None:
-            check(lib.ddm_shuffle_generate(req[0], req[1], req[2], self._sp()), "ddm_shuffle_generate")
-        self.tables_to(need_chunks)
+        """Generate R and tabulate chunks so that draws [0, upto) are covered and visible to
+        the consuming stream."""
+        if self.chunks_for(upto) > self.tab:
+            req, need_chunks = self.gen_request(upto)
+            if req is not None:
+                check(lib.ddm_shuffle_generate(req[0], req[1], req[2], self._gp()), "ddm_shuffle_generate")
+            self.tables_to(need_chunks)
+            ev = torch.cuda.Event()
+            ev.record(self.gen_stream)
+            self.mark_ready(ev)
+        self.wait_for(upto)
 
     def fill_job(self, rec, P, W, perm_out_ptr, stop_ptr=0, pick_offset=0, pick_last=0, pick_out_ptr=0):
         """One ddm_shuffle_job record (kernels.JOB_DTYPE) for a window of W batches from draw P;
         R must already cover it (window_draws)."""
         assert 0 <= W <= self.max_window
         rec["R"], rec["Tsub"], rec["Tchunk"] = self.R.data_ptr(), self.Tsub.data_ptr(), self.Tchunk.data_ptr()
-        rec["avail"], rec["P"], rec["W"] = self.tab * CHUNK, int(P), int(W)
+        rec["avail"], rec["P"], rec["W"] = self.waited * CHUNK, int(P), int(W)
         rec["pieces"], rec["info"] = self.pieces.data_ptr(), self.info.data_ptr()
         rec["J"], rec["E"], rec["perm_out"] = self.J.data_ptr(), self.E.data_ptr(), int(perm_out_ptr)
         rec["stop"], rec["pick_offset"], rec["pick_last"] = int(stop_ptr), int(pick_offset), int(pick_last)
@@ -178,7 +220,7 @@ class GpuShuffle:
         self.ensure(P + self.window_draws(W))
         ev = (None, None) if timer is None else (timer.ev[0], timer.ev[1])
         check(lib.ddm_shuffle_window(self.R.data_ptr(), self.Tsub.data_ptr(), self.Tchunk.data_ptr(),
-                                     self.tab * CHUNK, int(P), int(W), self.L, self.pieces.data_ptr(),
+                                     self.waited * CHUNK, int(P), int(W), self.L, self.pieces.data_ptr(),
                                      self.max_pieces, self.info.data_ptr(), self.J.data_ptr(), self.E.data_ptr(),
                                      perm_out.data_ptr(), self._sp(), *ev), "ddm_shuffle_window")
 

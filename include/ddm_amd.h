@@ -288,6 +288,23 @@ int ddm_rf_fit(const float* X, int32_t n, int32_t n_features, const int32_t* y_i
                int64_t nodes_cap, int32_t* roots, double* leaf_value, int64_t leaf_rows_cap,
                int64_t* out_info);
 
+/* Many refits at once (one per partition that drifted): every (job, tree) pair is fitted
+ * on a persistent pool of n_threads host threads (the calling thread included), then each
+ * job is packed like ddm_rf_fit and, when `blob` is given and the forest compiles,
+ * compiled with ddm_forest_compile (blob_bytes > 0, cf_* filled).  status per job: 0,
+ * DDM_E_NAN (use sklearn), DDM_E_IMPURE or DDM_E_ARG; the call returns the first
+ * non-zero status (the other jobs are still done). */
+typedef struct ddm_fit_job {
+    const float* X; const int32_t* y_idx; const int64_t* seeds; const int32_t* classes;
+    int32_t n, n_features, n_classes, n_trees, max_features, status;
+    ddm_node* nodes; int64_t nodes_cap; int32_t* roots; double* leaf_value; int64_t leaf_rows_cap;
+    int64_t info[3];                   /* out: n_nodes, pure, n_leaf_rows */
+    uint8_t* blob; int64_t blob_cap; int64_t blob_bytes;
+    int32_t cf_slots, cf_vote_regs, cf_leaves, pad;
+} ddm_fit_job;
+
+int ddm_rf_fit_many(ddm_fit_job* jobs, int32_t n_jobs, int32_t n_threads);
+
 /* ---- synthetic inputs (benchmark configs) ------------------------- */
 
 /* Labels of a class-block stream partitioned as DDM_Process.py:225 (row % n_parts):
