@@ -192,6 +192,212 @@ __global__ __launch_bounds__(256) void k_scan_streams(
     if (nev_out) nev_out[sid] = nev;
 }
 
+
+// ---------------------------------------------------------------------------------
+// Production scan (no p/s trace): the same decisions and states, bit for bit, with a
+// cheaper exact row and shortcuts that need no arithmetic at all.
+//
+//  * Division by n: q = RN(a / n) from r = RN(1/n) with one Markstein correction,
+//    q0 = a*r, e = fma(-q0, n, a), q = fma(e, r, q0) (exact remainder; correctly rounded
+//    quotient for a correctly rounded reciprocal).  RN(1/n) comes from an LDS table for
+//    n < kRcpN, otherwise from an IEEE division.
+//  * Fresh detector + two zero rows == the trivial state with n = 3 (p, s and the three
+//    minima all 0) without evaluating them.
+//  * Trivial state (gate passed) + an error row: p + s > 0 = p_min + c * s_min, i.e. a
+//    change at that row (and no warning, the `elif`).  In mode 1 the detector is then
+//    dropped, so nothing of that row needs computing; mode 0 stops there and computes the
+//    row exactly for the carried state.
+//  * Each lane works through several streams (grid-stride), which evens out the very
+//    different amounts of exact rows per stream across the 64 lanes of a wave.
+constexpr int kRcpN = 4096;
+constexpr int kFastThreads = 256;
+
+__device__ __forceinline__ double div_rn(double a, double n, double r) {
+    const double q0 = a * r;
+    const double e = __builtin_fma(-q0, n, a);
+    return __builtin_fma(e, r, q0);
+}
+
+__device__ __forceinline__ void det_add_fast(Det& d, int x, int min_inst, double wl, double cl,
+                                             const double* __restrict__ rcp) {
+    if (d.chg) det_reset(d);
+    const double n = (double)d.n;
+    const double r = d.n < kRcpN ? rcp[d.n] : 1.0 / n;
+    const double p = d.p + div_rn((double)x - d.p, n, r);
+    const double s = sqrt(div_rn(p * (1.0 - p), n, r));
+    d.p = p;
+    d.s = s;
+    d.n += 1;
+    d.chg = 0;
+    d.warn = 0;
+    if (d.n < min_inst) return;
+    const double ps = p + s;
+    if (ps <= d.psmin) {
+        d.pmin = p;
+        d.smin = s;
+        d.psmin = ps;
+    }
+    if (ps > d.pmin + cl * d.smin) d.chg = 1;
+    else if (ps > d.pmin + wl * d.smin) d.warn = 1;
+}
+
+__device__ __forceinline__ bool det_fresh(const Det& d) {
+    return d.chg || (d.n == 1 && d.p == 1.0 && d.s == 0.0 && d.psmin == __builtin_huge_val() &&
+                     d.pmin == __builtin_huge_val() && d.smin == __builtin_huge_val());
+}
+
+__device__ __forceinline__ int byte_at(uint64_t lo, uint64_t hi, int k) {
+    return (int)(((k < 8 ? lo >> (8 * k) : hi >> (8 * (k - 8)))) & 0xff);
+}
+
+// One lane = a persistent worker over streams sid, sid + nthreads, ...  The body is ONE
+// flat loop whose iterations each do one step of one kind (start/finish a stream, two
+// leading zeros, a zero run, a trivial-state change, or an exact row): no nested loops,
+// so a lane that finishes a stream starts its next one at once instead of idling until
+// the slowest lane of its wave is done with the same round.
+__global__ __launch_bounds__(kFastThreads) void k_scan_fast(
+    const uint8_t* __restrict__ err, const int64_t* __restrict__ off, int64_t n_streams, ddm_params P,
+    ddm_state* __restrict__ state, const uint64_t* __restrict__ first_nz, const int64_t* __restrict__ batch_base,
+    int32_t* __restrict__ ev, int32_t* __restrict__ stop_out, int64_t* __restrict__ nev_out, int mode,
+    const uint8_t* __restrict__ pmap, const int64_t* __restrict__ stream_end) {
+    __shared__ double rcp[kRcpN];
+    for (int k = threadIdx.x; k < kRcpN; k += kFastThreads) rcp[k] = 1.0 / (double)(k > 0 ? k : 1);
+    __syncthreads();
+    const int64_t pb = P.per_batch;
+    const int min_inst = P.min_num_instances;
+    const double wl = P.warning_level, cl = P.out_control_level;
+    const bool shortcuts = min_inst == 3;   // the trivial-state shortcuts assume the reference gate
+    const int64_t nthreads = (int64_t)gridDim.x * kFastThreads;
+
+    int64_t sid = (int64_t)blockIdx.x * kFastThreads + threadIdx.x - nthreads;   // advanced on the first step
+    int64_t lo = 0, hi = 0, b = 0, bstart = 0, bend = 0, i = 0, cbase = -1, nev = 0;
+    uint64_t hint = 0, clo = 0, chi = 0;
+    int32_t* evs = ev;
+    int32_t stop = -1;
+    int wpos = -1;
+    bool open = false;                      // a stream is loaded
+    Det d;
+    d.p = d.s = d.pmin = d.smin = d.psmin = 0.0;
+    d.n = 1;
+    d.chg = d.warn = 0;
+
+    for (;;) {
+        if (!open || i >= hi) {
+            if (open) {                     // finish the stream
+                ddm_state st;
+                st.miss_prob = d.p;
+                st.miss_std = d.s;
+                st.miss_prob_min = d.pmin;
+                st.miss_sd_min = d.smin;
+                st.miss_prob_sd_min = d.psmin;
+                st.sample_count = d.n;
+                st.in_concept_change = d.chg;
+                st.in_warning_zone = d.warn;
+                state[sid] = st;
+                if (stop_out) stop_out[sid] = stop;
+                if (nev_out) nev_out[sid] = nev;
+            }
+            sid += nthreads;
+            if (sid >= n_streams) break;
+            lo = off[sid];
+            hi = stream_end ? stream_end[sid] : off[sid + 1];
+            const ddm_state st = state[sid];
+            d.p = st.miss_prob;
+            d.s = st.miss_std;
+            d.pmin = st.miss_prob_min;
+            d.smin = st.miss_sd_min;
+            d.psmin = st.miss_prob_sd_min;
+            d.n = st.sample_count;
+            d.chg = st.in_concept_change;
+            d.warn = st.in_warning_zone;
+            hint = first_nz ? first_nz[sid] : 0ull;
+            evs = ev + 2 * batch_base[sid];
+            nev = 0;
+            stop = -1;
+            b = 0;
+            bstart = lo;
+            bend = min(lo + pb, hi);
+            wpos = -1;
+            i = lo;
+            cbase = -1;
+            open = true;
+            continue;
+        }
+        // the 16-byte chunk holding row i (and row i+1 for the two-zero test)
+        const int64_t cb = i & ~(int64_t)15;
+        if (cb != cbase) {
+            const uint4 v = *reinterpret_cast<const uint4*>(err + cb);
+            clo = (uint64_t)v.x | ((uint64_t)v.y << 32);
+            chi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+            cbase = cb;
+        }
+        const int k = (int)(i - cb);
+        const int xi = byte_at(clo, chi, k);
+        const bool triv = det_trivial(d);
+        bool changed = false;
+        if (shortcuts && !triv && i + 1 < bend && det_fresh(d) && xi == 0 &&
+            (k < 15 ? byte_at(clo, chi, k + 1) : (int)err[i + 1]) == 0) {
+            // fresh detector, two zero rows: the trivial state with the gate passed
+            d.p = d.s = d.pmin = d.smin = d.psmin = 0.0;
+            d.n = 3;
+            d.chg = d.warn = 0;
+            i += 2;
+        } else if (triv && xi == 0) {
+            // a zero run in the trivial state: to the hinted first nonzero row, or past the
+            // zero bytes of this chunk (never past the current batch)
+            int64_t j;
+            if (hint > (uint64_t)i) {
+                j = hint < (uint64_t)hi ? (int64_t)hint : hi;
+            } else {
+                const int lim = (int)min((int64_t)16, min(hi, bend) - cb);
+                j = cb + first_nonzero_byte(clo, chi, k, lim);
+            }
+            d.n += j - i;
+            d.warn = 0;
+            i = j;
+            if (i >= bend) {                // whole batches of zeros: no event can have occurred
+                b = (i - lo) / pb;
+                bstart = lo + b * pb;
+                bend = min(bstart + pb, hi);
+                wpos = -1;
+            }
+        } else if (shortcuts && triv && mode == 1 && d.n >= 3) {
+            // an error row in the trivial state: change here (p + s > 0); the detector is
+            // dropped, so the row needs no arithmetic
+            changed = true;
+            det_reset(d);
+            ++i;
+        } else {
+            det_add_fast(d, xi != 0, min_inst, wl, cl, rcp);
+            if (d.warn && wpos < 0) wpos = (int)(i - bstart);
+            ++i;
+            changed = d.chg != 0;
+            if (changed && mode == 1) det_reset(d);   // DDM dropped (DDM_Process.py:209)
+        }
+        if (changed) {
+            const int cpos = (int)(i - 1 - bstart);
+            evs[2 * b] = (pmap && wpos >= 0) ? (int)pmap[bstart + wpos] : wpos;
+            evs[2 * b + 1] = pmap ? (int)pmap[bstart + cpos] : cpos;
+            ++nev;
+            if (mode == 0) {
+                stop = (int32_t)b;
+                i = hi;                     // finish this stream
+                continue;
+            }
+            i = bend;                       // fresh detector from the next batch
+        } else if (i >= bend && wpos >= 0) {
+            evs[2 * b] = pmap ? (int)pmap[bstart + wpos] : wpos;
+            ++nev;
+        }
+        if (i >= bend && i < hi) {
+            ++b;
+            bstart = bend;
+            bend = min(bstart + pb, hi);
+            wpos = -1;
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" int ddm_scan_streams(const uint8_t* err, const int64_t* stream_off, int64_t n_streams,
@@ -214,9 +420,19 @@ extern "C" int ddm_scan_streams(const uint8_t* err, const int64_t* stream_off, i
     const int64_t blocks = ddm::ceil_div(n_streams, threads);
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
-    hipLaunchKernelGGL(k_scan_streams, dim3((unsigned)blocks), dim3(threads), 0, s, err, stream_off, n_streams, *prm,
-                       state_io, first_nz, batch_base, ev_out, stop_out, nev_out, (int)mode, ps_out, perm_map,
-                       stream_end);
+    if (ps_out) {                       // p/s trace: the reference-shaped exact kernel
+        hipLaunchKernelGGL(k_scan_streams, dim3((unsigned)blocks), dim3(threads), 0, s, err, stream_off, n_streams,
+                           *prm, state_io, first_nz, batch_base, ev_out, stop_out, nev_out, (int)mode, ps_out,
+                           perm_map, stream_end);
+    } else {
+        // persistent lanes: one resident round of workgroups (the 32 KB reciprocal table
+        // allows 5 per CU), each lane working through ~n_streams / (1280 * 256) streams
+        const int64_t fast_blocks = std::max<int64_t>(1, std::min<int64_t>(ddm::ceil_div(n_streams, kFastThreads),
+                                                                           256 * 5 * 4));
+        hipLaunchKernelGGL(k_scan_fast, dim3((unsigned)fast_blocks), dim3(kFastThreads), 0, s, err, stream_off,
+                           n_streams, *prm, state_io, first_nz, batch_base, ev_out, stop_out, nev_out, (int)mode,
+                           perm_map, stream_end);
+    }
     if (ev_end)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
     return ddm::launch_status("ddm_scan_streams");

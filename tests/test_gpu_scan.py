@@ -171,3 +171,36 @@ def test_scan_lazy_reset_on_carried_change():
     for t, v in enumerate(x):
         d.add(int(v))
         assert ps[t, 0] == d.miss_prob and ps[t, 1] == d.miss_std
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("min_inst", [3, 5])
+@pytest.mark.parametrize("per_batch", [3, 100])
+def test_fast_scan_equals_trace_scan(oracle_lib, mode, min_inst, per_batch):
+    """The production scan (Markstein division, fresh/trivial shortcuts, several streams per
+    lane) against the reference-shaped trace kernel and the C oracle: events, stop batch,
+    event counts and the carried state, bit for bit."""
+    rs = np.random.RandomState(1000 + 10 * mode + min_inst + per_batch)
+    err, off = random_streams(rs, 3000, max_len=5000)
+    hint = first_nonzero(err, off)
+    fast = gpu_scan(err, off, per_batch=per_batch, mode=mode, hint=hint, min_inst=min_inst)
+    slow = gpu_scan(err, off, per_batch=per_batch, mode=mode, hint=hint, min_inst=min_inst, trace=True)
+    for a, b in zip(fast[:3], slow[:3]):
+        assert np.array_equal(a, b)
+    np.testing.assert_array_equal(_state_matrix(fast[3]), _state_matrix(slow[3]))
+    if min_inst == 3:
+        oev, ostop, ost, _ = oracle_scan_c(oracle_lib, err, off, per_batch=per_batch, mode=mode)
+        assert np.array_equal(fast[0], oev)
+        np.testing.assert_array_equal(_state_matrix(fast[3]), ost)
+
+
+def test_fast_scan_long_counts_use_ieee_reciprocal(oracle_lib):
+    """Detectors past n = 4096 (reciprocal table) divide exactly as well."""
+    rs = np.random.RandomState(5)
+    s = np.concatenate([rs.binomial(1, 0.3, 20000), rs.binomial(1, 0.6, 20000)]).astype(np.uint8)
+    off = np.array([0, len(s)], np.int64)
+    for mode in (0, 1):
+        fast = gpu_scan(s, off, per_batch=256, mode=mode)
+        oev, ostop, ost, _ = oracle_scan_c(oracle_lib, s, off, per_batch=256, mode=mode)
+        assert np.array_equal(fast[0], oev) and np.array_equal(fast[1], ostop)
+        np.testing.assert_array_equal(_state_matrix(fast[3]), ost)
