@@ -151,3 +151,36 @@ extern "C" int ddm_mt_skip(uint32_t* key, int32_t* pos, int64_t n_draws) {
     *pos = g.pos;
     return 0;
 }
+
+// From already tempered words of the stream (a read-back of the device copy R): one
+// batch's legacy permutation(L) followed by T randint(2**31-1) tree seeds — the draws a
+// refit consumes (DDM_Process.py:190 then :102).  used[0] / used[1] = words taken by the
+// shuffle / the seeds.  DDM_E_ARG when n_words runs out (read more words).
+extern "C" int ddm_words_perm_seeds(const uint32_t* words, int64_t n_words, int32_t L, int32_t T,
+                                    uint8_t* perm_out, int64_t* seeds_out, int64_t* used) {
+    if (!words || !used || L < 0 || L > 256 || T < 0 || (L && !perm_out) || (T && !seeds_out)) return DDM_E_ARG;
+    int64_t k = 0;
+    for (int32_t i = 0; i < L; ++i) perm_out[i] = (uint8_t)i;
+    for (int32_t i = L - 1; i >= 1; --i) {
+        const uint32_t mask = 0xffffffffu >> __builtin_clz((uint32_t)i);
+        uint32_t j;
+        do {
+            if (k >= n_words) return DDM_E_ARG;
+            j = words[k++] & mask;
+        } while (j > (uint32_t)i);
+        const uint8_t t = perm_out[i];
+        perm_out[i] = perm_out[j];
+        perm_out[j] = t;
+    }
+    used[0] = k;
+    for (int32_t t = 0; t < T; ++t) {
+        uint32_t v;
+        do {
+            if (k >= n_words) return DDM_E_ARG;
+            v = words[k++] & 0x7fffffffu;
+        } while (v > 0x7ffffffeu);
+        seeds_out[t] = (int64_t)v;
+    }
+    used[1] = k - used[0];
+    return 0;
+}

@@ -136,9 +136,42 @@ struct Builder {
     double weighted_n_samples = 0, wn_node = 0, wn_left = 0, wn_right = 0;
     int64_t start = 0, end = 0, pos = 0;
     uint32_t rand_r_state = 0;
-    std::vector<std::pair<float, int64_t>> sortbuf;
+    // Presorted features: order[f] = the n training rows by ascending X[:, f], shared by
+    // every tree and node.  A node's samples carry the node's tag, so its values sorted
+    // by f are a filtered pass over order[f] (O(n)) instead of a sort.  Equal values may
+    // come out in another order than sklearn's sort leaves them; split search and
+    // partition depend only on the values and the (exact, integer) class sums.
+    std::vector<int32_t> own_order;   // [F][n] when this builder sorted itself
+    const int32_t* order = nullptr;   // [F][n] (own_order or a job's shared copy)
+    std::vector<uint32_t> tag;        // [n]
+    uint32_t cur_tag = 0;
 
     float x(int64_t s, int64_t f) const { return X[s * F + f]; }
+
+    static void presort_into(const float* X, int n, int F, int32_t* order) {
+        std::vector<std::pair<float, int32_t>> buf(n);
+        for (int f = 0; f < F; ++f) {
+            for (int i = 0; i < n; ++i) buf[i] = {X[(int64_t)i * F + f], i};
+            std::sort(buf.begin(), buf.end(),
+                      [](const std::pair<float, int32_t>& a, const std::pair<float, int32_t>& b) { return a.first < b.first; });
+            for (int i = 0; i < n; ++i) order[(size_t)f * n + i] = buf[i].second;
+        }
+    }
+    void use_order(const int32_t* shared) {
+        if (shared) {
+            order = shared;
+        } else {
+            own_order.assign((size_t)F * n, 0);
+            presort_into(X, n, F, own_order.data());
+            order = own_order.data();
+        }
+        tag.assign(n, 0);
+        cur_tag = 0;
+    }
+    void tag_node() {                 // samples[start:end] belong to the node being split
+        ++cur_tag;
+        for (int64_t p = start; p < end; ++p) tag[samples[p]] = cur_tag;
+    }
 
     // ClassificationCriterion.init over samples[start:end]
     void crit_init(int64_t s0, int64_t s1) {
@@ -197,13 +230,15 @@ struct Builder {
     }
 
     void sort_feature(int64_t f) {
-        sortbuf.clear();
-        for (int64_t p = start; p < end; ++p) sortbuf.emplace_back(x(samples[p], f), samples[p]);
-        std::sort(sortbuf.begin(), sortbuf.end(),
-                  [](const std::pair<float, int64_t>& a, const std::pair<float, int64_t>& b) { return a.first < b.first; });
-        for (int64_t p = start; p < end; ++p) {
-            fv[p] = sortbuf[p - start].first;
-            samples[p] = sortbuf[p - start].second;
+        const int32_t* o = order + (size_t)f * n;
+        int64_t k = start;
+        for (int i = 0; i < n; ++i) {
+            const int32_t r = o[i];
+            if (tag[r] == cur_tag) {
+                samples[k] = r;
+                fv[k] = x(r, f);
+                ++k;
+            }
         }
     }
 
@@ -282,6 +317,14 @@ struct Builder {
         return best;
     }
 
+    struct Rec {
+        int64_t start, end, depth, parent;
+        int is_left;
+        double impurity;
+        int64_t n_const;
+    };
+    std::vector<Rec> stack;
+
     void build(uint32_t seed, Tree& t) {
         // bootstrap (ensemble/_forest.py _generate_sample_indices) and the splitter seed,
         // which is the first randint(0, 2**31-1) of a fresh RandomState(seed)
@@ -303,14 +346,13 @@ struct Builder {
             weighted_n_samples += w[i];
         }
         for (int f = 0; f < F; ++f) features[f] = f;
-        t = Tree();
-        struct Rec {
-            int64_t start, end, depth, parent;
-            int is_left;
-            double impurity;
-            int64_t n_const;
-        };
-        std::vector<Rec> stack;
+        t.left.clear();                 // keep the capacity of a reused tree
+        t.right.clear();
+        t.feature.clear();
+        t.threshold.clear();
+        t.missing_left.clear();
+        t.value.clear();
+        stack.clear();
         stack.push_back({0, (int64_t)samples.size(), 0, -1, 0, INFINITY, 0});
         bool first = true;
         while (!stack.empty()) {
@@ -328,6 +370,7 @@ struct Builder {
             Split sp{r.end, 0, 0.0, -INFINITY, INFINITY, INFINITY, false};
             int64_t n_const = r.n_const;
             if (!is_leaf) {
+                tag_node();
                 sp = node_split(impurity, &n_const);
                 is_leaf = sp.pos >= r.end || sp.improvement + kEpsilon < 0.0;
             }
@@ -349,11 +392,11 @@ struct Builder {
 
 // Pack trees into the ddm_node layout: BFS renumbering with adjacent siblings
 // (treepack.py:pack).  Returns 0 or DDM_E_IMPURE (leaf_value missing / too small).
-int pack_trees(const std::vector<Tree>& trees, int n_classes, bool pure, ddm_node* nodes, int32_t* roots,
+int pack_trees(const Tree* trees, int n_trees, int n_classes, bool pure, ddm_node* nodes, int32_t* roots,
                double* leaf_value, int64_t leaf_rows_cap, int64_t* out_info) {
     int64_t base = 0, leaf_rows = 0;
     std::vector<int64_t> order, new_id;
-    for (size_t t = 0; t < trees.size(); ++t) {
+    for (int t = 0; t < n_trees; ++t) {
         const Tree& tr = trees[t];
         const int64_t m = (int64_t)tr.left.size();
         new_id.assign(m, 0);
@@ -413,7 +456,8 @@ bool tree_is_pure(const Tree& tr, int n_classes) {
     return true;
 }
 
-void builder_init(Builder& b, const float* X, int n, int F, const int32_t* y, int K, int max_features) {
+void builder_init(Builder& b, const float* X, int n, int F, const int32_t* y, int K, int max_features,
+                  const int32_t* shared_order = nullptr) {
     b.X = X;
     b.n = n;
     b.F = F;
@@ -428,6 +472,7 @@ void builder_init(Builder& b, const float* X, int n, int F, const int32_t* y, in
     b.sum_left.assign(K, 0.0);
     b.sum_right.assign(K, 0.0);
     b.samples.reserve(n);
+    b.use_order(shared_order);
 }
 
 int check_inputs(const float* X, int32_t n, int32_t n_features, const int32_t* y_idx, int32_t n_classes) {
@@ -534,12 +579,16 @@ extern "C" int ddm_rf_fit(const float* X, int32_t n, int32_t n_features, const i
         b.build((uint32_t)seeds[t], trees[t]);
         pure = pure && tree_is_pure(trees[t], n_classes);
     }
-    return pack_trees(trees, n_classes, pure, nodes, roots, leaf_value, leaf_rows_cap, out_info);
+    return pack_trees(trees.data(), n_trees, n_classes, pure, nodes, roots, leaf_value, leaf_rows_cap, out_info);
 }
 
 extern "C" int ddm_rf_fit_many(ddm_fit_job* jobs, int32_t n_jobs, int32_t n_threads) {
     if (!jobs || n_jobs < 0) return DDM_E_ARG;
-    std::vector<std::vector<Tree>> trees(n_jobs);
+    // trees persist across calls so their node vectors keep their capacity
+    static std::vector<std::vector<Tree>> trees;
+    static std::mutex trees_mu;
+    std::lock_guard<std::mutex> trees_lock(trees_mu);
+    if ((int)trees.size() < n_jobs) trees.resize(n_jobs);
     std::vector<int64_t> first(n_jobs + 1, 0);
     for (int j = 0; j < n_jobs; ++j) {
         ddm_fit_job& jb = jobs[j];
@@ -551,9 +600,17 @@ extern "C" int ddm_rf_fit_many(ddm_fit_job* jobs, int32_t n_jobs, int32_t n_thre
             jb.status = DDM_E_ARG;
         else
             jb.status = check_inputs(jb.X, jb.n, jb.n_features, jb.y_idx, jb.n_classes);
-        trees[j].resize(jb.status ? 0 : jb.n_trees);
-        first[j + 1] = first[j] + (int64_t)trees[j].size();
+        if (!jb.status && (int)trees[j].size() < jb.n_trees) trees[j].resize(jb.n_trees);
+        first[j + 1] = first[j] + (jb.status ? 0 : jb.n_trees);
     }
+    // presorted feature orders, one per job, shared read-only by the tree tasks
+    std::vector<std::vector<int32_t>> orders(n_jobs);
+    pool().run(std::max(1, (int)n_threads), n_jobs, [&](int64_t j) {
+        const ddm_fit_job& jb = jobs[j];
+        if (jb.status) return;
+        orders[j].assign((size_t)jb.n_features * jb.n, 0);
+        Builder::presort_into(jb.X, jb.n, jb.n_features, orders[j].data());
+    });
     // every (job, tree) is an independent task
     // each thread keeps one Builder, re-initialised when it moves to another job (or call)
     static std::atomic<uint64_t> calls{0};
@@ -565,7 +622,7 @@ extern "C" int ddm_rf_fit_many(ddm_fit_job* jobs, int32_t n_jobs, int32_t n_thre
         const int j = (int)(std::upper_bound(first.begin(), first.end(), task) - first.begin()) - 1;
         const ddm_fit_job& jb = jobs[j];
         if (tb_call != call || tb_job != j) {
-            builder_init(tb, jb.X, jb.n, jb.n_features, jb.y_idx, jb.n_classes, jb.max_features);
+            builder_init(tb, jb.X, jb.n, jb.n_features, jb.y_idx, jb.n_classes, jb.max_features, orders[j].data());
             tb_call = call;
             tb_job = j;
         }
@@ -577,9 +634,9 @@ extern "C" int ddm_rf_fit_many(ddm_fit_job* jobs, int32_t n_jobs, int32_t n_thre
         ddm_fit_job& jb = jobs[j];
         if (jb.status) return;
         bool pure = jb.n_trees <= 255;
-        for (const Tree& t : trees[j]) pure = pure && tree_is_pure(t, jb.n_classes);
-        jb.status = pack_trees(trees[j], jb.n_classes, pure, jb.nodes, jb.roots, jb.leaf_value, jb.leaf_rows_cap,
-                               jb.info);
+        for (int t = 0; t < jb.n_trees; ++t) pure = pure && tree_is_pure(trees[j][t], jb.n_classes);
+        jb.status = pack_trees(trees[j].data(), jb.n_trees, jb.n_classes, pure, jb.nodes, jb.roots, jb.leaf_value,
+                               jb.leaf_rows_cap, jb.info);
         if (jb.status || !jb.blob) return;
         int64_t bytes = 0;
         const int rc = ddm_forest_compile(jb.nodes, (int32_t)jb.info[0], jb.roots, jb.n_trees, jb.classes,

@@ -31,7 +31,7 @@ from . import kernels
 from .forest import upload_forests
 from .params import OUTPUT_COLUMNS, DDMSettings, infer_x_features
 from .rng import MTStream
-from .shuffle import GpuShuffle, expected_draws_per_batch, fy_from_words, randint31_from_words
+from .shuffle import GpuShuffle, expected_draws_per_batch, perm_seeds_from_words
 from .trainer import BatchForestTrainer
 
 def _round_up(n, m):
@@ -291,14 +291,14 @@ class BatchRunner:
             sh = self.shuffles[ps.i]
             words = self.words_h[k].numpy().view(np.uint32)
             L = ps.blen(ps.j)
-            r = fy_from_words(words, L)
-            seeds = None if r is None else randint31_from_words(words[r[1]:], T)
-            if r is None or seeds is None:                      # rejections ran past the read-back
+            r = perm_seeds_from_words(words, L, T)
+            if r is None:                                       # rejections ran past the read-back
                 permj, P1 = sh.host_perm(ps.P, L)
                 seeds, P2 = sh.host_seeds(P1, T)
             else:
-                permj, P1 = r[0], ps.P + r[1]
-                seeds, P2 = seeds[0], P1 + seeds[1]
+                permj, seeds = r[0], r[1]
+                P1 = ps.P + r[2]
+                P2 = P1 + r[3]
             self._upload_perm(ps.i, ps.j, permj, 0)             # batch_b.sample before the fit (:190, :194)
             P_seeds, ps.P = P1, P2                              # 100 tree seeds follow the shuffle
             ps.P_after_first = ps.P

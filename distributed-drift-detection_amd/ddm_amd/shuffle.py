@@ -83,6 +83,20 @@ def randint31_from_words(words, T):
     return out, k
 
 
+def perm_seeds_from_words(words, L, T):
+    """permutation(L) then T randint(2**31-1) seeds from tempered words (native) ->
+    (perm uint8, seeds int64, draws used by the perm, draws used by the seeds) or None."""
+    words = np.ascontiguousarray(words, dtype=np.uint32)
+    perm = np.empty(max(L, 1), dtype=np.uint8)
+    seeds = np.empty(max(T, 1), dtype=np.int64)
+    used = np.zeros(2, dtype=np.int64)
+    rc = lib.ddm_words_perm_seeds(words.ctypes.data, words.size, int(L), int(T), perm.ctypes.data, seeds.ctypes.data,
+                                  used.ctypes.data)
+    if rc != 0:
+        return None
+    return perm[:L], seeds[:T], int(used[0]), int(used[1])
+
+
 class GpuShuffle:
     """One partition's MT19937 stream resident in HBM, with FSM tables for batch length L.
 

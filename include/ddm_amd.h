@@ -224,6 +224,12 @@ int ddm_mt_randint31(uint32_t* key, int32_t* pos, int64_t count, int64_t* out);
 /* Advance the generator by n_draws 32-bit words. */
 int ddm_mt_skip(uint32_t* key, int32_t* pos, int64_t n_draws);
 
+/* One batch's permutation(L) then T randint(2**31-1) seeds from already tempered words
+ * of the stream (e.g. read back from the device copy); used[0], used[1] = words each
+ * consumed.  DDM_E_ARG when the words run out. */
+int ddm_words_perm_seeds(const uint32_t* words, int64_t n_words, int32_t L, int32_t T,
+                         uint8_t* perm_out, int64_t* seeds_out, int64_t* used);
+
 /* ---- batch shuffles on the GPU (csrc/shuffle.hip) -------------------------------- */
 /* The partition's MT19937 stream as raw tempered words R[0..), generated on the device,
  * plus interval-FSM tables that make the Fisher-Yates draws of many batches parallel.
