@@ -1,0 +1,117 @@
+// Epoch read-back staging: everything the host needs after an epoch, gathered on the
+// device so that ONE device->host copy and ONE synchronisation close the epoch.
+//
+// After the batched shuffle / predict / scan of an epoch the controller has to learn,
+// per partition (run_DDM_loop, DDM_Process.py:170-213):
+//   * the batches with a warning or a change (DDM_Process.py:147-152, :204): compacted
+//     here into (window batch, warning, change) records instead of copying every row;
+//   * on a change in batch d (:207-210): the new training batch = batch d in its shuffled
+//     order (`batch_a = batch_b`, :208), i.e. X rows d*pb + perm[d*pb + k] and labels, and
+//     the stream words from the draw after batch d's shuffle, where batch d+1's shuffle
+//     and then the refit's 100 tree seeds are drawn (:190, :102).
+// One workgroup per partition; nothing here decides anything, it only moves bytes.
+#include "common.h"
+
+namespace {
+
+constexpr int kStageThreads = 256;
+
+struct Job {
+    const float* X;
+    int64_t ld;
+    const int32_t* y;
+    const uint8_t* perm;
+    int64_t base;
+    const int32_t* ev;
+    const int32_t* stop;
+    const int64_t* pick;
+    const uint32_t* R;
+    int64_t j, g0, nb, b_end, p_after_first, p_tail_after;
+    int32_t pb, last_len, n_features, n_words, tail, max_events;
+    float* x_out;
+    int32_t* y_out;
+    uint32_t* w_out;
+    int64_t* info_out;
+    int32_t* ev_out;
+};
+static_assert(sizeof(Job) == sizeof(ddm_stage_job), "Job must mirror ddm_stage_job");
+
+__global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__ jobs) {
+    __shared__ int counts[kStageThreads];
+    const Job jb = jobs[blockIdx.x];
+    const int t = threadIdx.x;
+    const int32_t stop = *jb.stop;
+    const int64_t last = stop >= 0 ? jb.j + stop : jb.b_end - 1;   // last batch the scan covered
+    const int64_t nrows = last - jb.j + 1;                         // window rows of ev to look at
+    // ---- compact the event rows: each thread a contiguous slice, block prefix of counts
+    const int64_t per = (nrows + kStageThreads - 1) / kStageThreads;
+    const int64_t r0 = t * per, r1 = min(nrows, r0 + per);
+    int c = 0;
+    for (int64_t r = r0; r < r1; ++r) c += (jb.ev[2 * r] >= 0 || jb.ev[2 * r + 1] >= 0) ? 1 : 0;
+    counts[t] = c;
+    __syncthreads();
+    for (int s = 1; s < kStageThreads; s <<= 1) {      // inclusive scan (Hillis-Steele)
+        const int v = t >= s ? counts[t - s] : 0;
+        __syncthreads();
+        counts[t] += v;
+        __syncthreads();
+    }
+    const int total = counts[kStageThreads - 1];
+    int k = counts[t] - c;
+    for (int64_t r = r0; r < r1 && k < jb.max_events; ++r) {
+        const int32_t w = jb.ev[2 * r], ch = jb.ev[2 * r + 1];
+        if (w >= 0 || ch >= 0) {
+            jb.ev_out[3 * k] = (int32_t)r;
+            jb.ev_out[3 * k + 1] = w;
+            jb.ev_out[3 * k + 2] = ch;
+            ++k;
+        }
+    }
+    if (t == 0) {
+        jb.info_out[1] = total;
+        jb.info_out[2] = total > jb.max_events ? 1 : 0;
+    }
+    if (stop < 0) {
+        if (t == 0) {
+            jb.info_out[0] = -1;
+            jb.info_out[3] = -1;
+        }
+        return;
+    }
+    // ---- a change in batch d: its rows in shuffled order and the words after its shuffle
+    const int64_t d = jb.j + stop;
+    const int L = d == jb.nb - 1 ? jb.last_len : jb.pb;
+    int64_t P;
+    if (d < jb.g0) P = jb.p_after_first;                        // the refit batch itself
+    else if (jb.tail && d == jb.nb - 1) P = jb.p_tail_after;    // the short last batch
+    else P = *jb.pick + 1;
+    if (t == 0) {
+        jb.info_out[0] = P;
+        jb.info_out[3] = d;
+    }
+    const int F = jb.n_features;
+    for (int e = t; e < L * F; e += kStageThreads) {
+        const int kk = e / F, f = e % F;
+        const int64_t row = d * jb.pb + jb.perm[jb.base + d * jb.pb + kk];
+        jb.x_out[e] = jb.X[(int64_t)f * jb.ld + row];
+    }
+    for (int kk = t; kk < L; kk += kStageThreads) {
+        const int64_t row = d * jb.pb + jb.perm[jb.base + d * jb.pb + kk];
+        jb.y_out[kk] = jb.y[row];
+    }
+    if (jb.R)
+        for (int w = t; w < jb.n_words; w += kStageThreads) jb.w_out[w] = jb.R[P + w];
+}
+
+}  // namespace
+
+extern "C" int ddm_epoch_stage(const ddm_stage_job* jobs_dev, int32_t n_jobs, ddm_stream_t stream) {
+    if (!jobs_dev || n_jobs < 0) {
+        ddm::set_error("ddm_epoch_stage: invalid argument");
+        return DDM_E_ARG;
+    }
+    if (n_jobs == 0) return 0;
+    hipLaunchKernelGGL(k_stage, dim3((unsigned)n_jobs), dim3(kStageThreads), 0, ddm::as_hip(stream),
+                       reinterpret_cast<const Job*>(jobs_dev));
+    return ddm::launch_status("ddm_epoch_stage");
+}

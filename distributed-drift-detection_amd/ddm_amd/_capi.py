@@ -70,6 +70,7 @@ SIGNATURES = {
     "ddm_forest_compile": (ctypes.c_int, [_vp, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _i64,
                                           ctypes.POINTER(ctypes.c_int64)]),
     "ddm_rf_fit_many": (ctypes.c_int, [_vp, _i32, _i32]),
+    "ddm_epoch_stage": (ctypes.c_int, [_vp, _i32, _vp]),
     "ddm_words_perm_seeds": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _vp]),
     "ddm_rf_fit": (ctypes.c_int, [_vp, _i32, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp]),
     "ddm_synth_block_labels": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i32, _vp]),

@@ -38,6 +38,10 @@ def _round_up(n, m):
     return (n + m - 1) // m * m
 
 
+def ps_feats(part):
+    return part.X.shape[0]
+
+
 class DevicePartition:
     """One partition's rows resident in HBM: X float32 [F, ld] (column f contiguous), y int32."""
 
@@ -117,7 +121,7 @@ class _Part:
     """Host-side epoch state of one partition in a BatchRunner."""
     __slots__ = ("i", "nb", "last_len", "n_full", "max_win", "base", "ev_base", "j", "P", "retrain", "train_rows",
                  "state", "win", "forest", "out", "done", "P_after_first", "g0", "b_end", "Wg", "tail",
-                 "P_tail_after", "seg_start", "pb")
+                 "P_tail_after", "seg_start", "pb", "staged")
 
     def blen(self, b):
         return self.last_len if b == self.nb - 1 else self.pb
@@ -210,11 +214,34 @@ class BatchRunner:
         for part, nb, mw in zip(self.parts, self.nbs, self.max_wins):
             cap = int(nb * expected_draws_per_batch(pb) * 1.2) + 64 * 1024
             self.shuffles.append(GpuShuffle(dev, pb, cap, mw, self.stream, self.gen_stream))
+        # epoch read-back staging (csrc/stage.hip): per partition the compacted events and,
+        # on a change, the training batch and the stream words after its shuffle; copied
+        # back together with the control block, so an epoch costs ONE synchronisation
+        self.n_words = 3 * pb + self.s.n_estimators + 64
+        self.max_events = 64
+        F = max(p.X.shape[0] for p in self.parts)
+        sz = {"x": 4 * 256 * F, "y": 4 * 256, "w": 4 * self.n_words, "info": 32, "ev": 12 * self.max_events}
+        self.stage_off = {}
+        o = 0
+        for key, nbytes in sz.items():
+            self.stage_off[key] = o
+            o += _round_up(nbytes, 256) * n
+        self.stage_stride = {k: _round_up(v, 256) for k, v in sz.items()}
+        self.stage_d = torch.zeros(o, dtype=torch.uint8, device=dev)
+        self.stage_h = torch.zeros(o, dtype=torch.uint8, pin_memory=True)
+        self.stage_jobs = kernels.PinnedTable(kernels.STAGE_DTYPE, n, dev)
         self.stats = RunStats()
 
     # -- helpers
     def _dptr(self, off, i, size):
         return self.ctrl_d.data_ptr() + off + size * i
+
+    def _sptr(self, key, i):
+        return self.stage_d.data_ptr() + self.stage_off[key] + self.stage_stride[key] * i
+
+    def _sview(self, key, i, dtype, count):
+        a = self.stage_off[key] + self.stage_stride[key] * i
+        return self.stage_h.numpy()[a:a + np.dtype(dtype).itemsize * count].view(dtype)
 
     def _ensure_all(self, wants, wait=True):
         """wants: [(partition index, draws needed)].  Partitions whose enqueued stream falls
@@ -265,11 +292,15 @@ class BatchRunner:
         n_words = 3 * pb + T + 64
         if self.words_h is None or self.words_h.shape[0] < len(need):
             self.words_h = torch.empty((len(self.parts), n_words), dtype=torch.int32, pin_memory=True)
-        for ps in need:
-            self.shuffles[ps.i].ensure(ps.P + n_words)
         rows_dev = []
+        unstaged = [ps for ps in need if ps.staged is None]
+        for ps in unstaged:
+            self.shuffles[ps.i].ensure(ps.P + n_words)
         with torch.cuda.stream(self.stream):
             for k, ps in enumerate(need):
+                if ps.staged is not None:           # everything came back with the epoch
+                    rows_dev.append(None)
+                    continue
                 sh = self.shuffles[ps.i]
                 self.words_h[k].copy_(sh.R[ps.P:ps.P + n_words], non_blocking=True)
                 part = self.parts[ps.i]
@@ -283,13 +314,14 @@ class BatchRunner:
                     rows_dev.append((xh, yh, idx_h))
                 else:
                     rows_dev.append(None)
-        self.stream.synchronize()
+        if unstaged:
+            self.stream.synchronize()
         t1 = time.perf_counter()
         st.refit_readback_s += t1 - t0
         work = []
         for k, ps in enumerate(need):
             sh = self.shuffles[ps.i]
-            words = self.words_h[k].numpy().view(np.uint32)
+            words = ps.staged[2] if ps.staged is not None else self.words_h[k].numpy().view(np.uint32)
             L = ps.blen(ps.j)
             r = perm_seeds_from_words(words, L, T)
             if r is None:                                       # rejections ran past the read-back
@@ -302,7 +334,10 @@ class BatchRunner:
             self._upload_perm(ps.i, ps.j, permj, 0)             # batch_b.sample before the fit (:190, :194)
             P_seeds, ps.P = P1, P2                              # 100 tree seeds follow the shuffle
             ps.P_after_first = ps.P
-            if rows_dev[k] is None:
+            if ps.staged is not None:
+                X32, y = ps.staged[0], ps.staged[1]
+                ps.staged = None
+            elif rows_dev[k] is None:
                 X32, y = self.parts[ps.i].rows(ps.train_rows, self.stream)
             else:
                 X32, y = rows_dev[k][0].numpy(), rows_dev[k][1].numpy().astype(np.int64)
@@ -402,6 +437,7 @@ class BatchRunner:
                 ps.out = np.full((ps.nb - 1, 2), -1, dtype=np.int64)
                 ps.state = kernels.fresh_states(1)
                 ps.forest, ps.retrain, ps.j, ps.done = None, True, 1, False
+                ps.staged = None
                 ps.win = max(1, s.window_batches)
                 ps.seg_start = 1
             while True:
@@ -435,8 +471,10 @@ class BatchRunner:
             ps.tail = ps.b_end == ps.nb and ps.last_len != pb and ps.nb - 1 >= ps.g0
             ps.P_tail_after = None
         shuf = [ps for ps in live if ps.Wg]
+        # stream coverage: the window's shuffles, and the words the staging reads after a
+        # change (from at most the window's last draw)
+        self._ensure_all([(ps.i, ps.P + self.shuffles[ps.i].window_draws(ps.Wg) + self.n_words) for ps in live])
         if shuf:
-            self._ensure_all([(ps.i, ps.P + self.shuffles[ps.i].window_draws(ps.Wg)) for ps in shuf])
             max_W = max(ps.Wg for ps in shuf)
             max_pieces = max(2 + self.shuffles[ps.i].window_draws(ps.Wg) // 8192 for ps in shuf)
         tails = [ps for ps in live if ps.tail]
@@ -493,16 +531,34 @@ class BatchRunner:
                                  self.perm_all.data_ptr(), base + self.o_end)
         if shuf:
             kernels.shuffle_pick_batch(self.jobs, len(shuf), stream)
+        # stage what the host needs next, then one copy back and one synchronisation
+        srec = self.stage_jobs.rec
+        for k, ps in enumerate(live):
+            part, r = self.parts[ps.i], srec[k]
+            r["X"], r["ld"], r["y"] = part.X.data_ptr(), part.X.shape[1], part.y.data_ptr()
+            r["perm"], r["base"] = self.perm_all.data_ptr(), ps.base
+            r["ev"] = self.ev_d.data_ptr() + 8 * ps.ev_base
+            r["stop"], r["pick"] = self._dptr(self.o_stop, ps.i, 4), self._dptr(self.o_pick, ps.i, 8)
+            r["R"] = self.shuffles[ps.i].R.data_ptr()
+            r["j"], r["g0"], r["nb"], r["b_end"] = ps.j, ps.g0, ps.nb, ps.b_end
+            r["p_after_first"] = -1 if ps.P_after_first is None else ps.P_after_first
+            r["p_tail_after"] = -1 if ps.P_tail_after is None else ps.P_tail_after
+            r["pb"], r["last_len"], r["n_features"] = pb, ps.last_len, part.X.shape[0]
+            r["n_words"], r["tail"], r["max_events"] = self.n_words, int(bool(ps.tail)), self.max_events
+            r["x_out"], r["y_out"], r["w_out"] = self._sptr("x", ps.i), self._sptr("y", ps.i), self._sptr("w", ps.i)
+            r["info_out"], r["ev_out"] = self._sptr("info", ps.i), self._sptr("ev", ps.i)
+        kernels.epoch_stage(self.stage_jobs, len(live), stream)
         with torch.cuda.stream(stream):
             self.ctrl_h[:self.o_off].copy_(self.ctrl_d[:self.o_off], non_blocking=True)
             self.ctrl_h[self.o_state:].copy_(self.ctrl_d[self.o_state:], non_blocking=True)
+            self.stage_h.copy_(self.stage_d, non_blocking=True)
         stream.synchronize()
         if self.timing:
             st.predict_ms += self.t_pred.elapsed_ms()
             st.scan_ms += self.t_scan.elapsed_ms()
             if shuf:
                 st.shuffle_ms += self.t_shuf.elapsed_ms()
-        # read-backs that depend on the results: event rows and drift batches' shuffles
+        # read-backs beyond the staging (more events than it holds): rare
         pending = False
         for ps in live:
             stop, nev = int(self.stop_h[ps.i]), int(self.nev_h[ps.i])
@@ -512,16 +568,12 @@ class BatchRunner:
             if self.timing:
                 st.predict_bytes += (p1 - p0) * (4 * ps.forest.features_read + 6)
                 st.scan_rows += min(p1, ps.base + (ps_last + 1) * pb) - p0
-            with torch.cuda.stream(stream):
-                if nev:
-                    k, e0 = ps_last - ps.j + 1, ps.ev_base
+            info = self._sview("info", ps.i, np.int64, 4)
+            if nev and info[2]:
+                k, e0 = ps_last - ps.j + 1, ps.ev_base
+                with torch.cuda.stream(stream):
                     self.ev_h[e0:e0 + k].copy_(self.ev_d[e0:e0 + k], non_blocking=True)
-                    pending = True
-                if stop >= 0:
-                    d = ps.j + stop
-                    at = ps.base + d * pb
-                    self.small_h[ps.i][2][:ps.blen(d)].copy_(self.perm_all[at:at + ps.blen(d)], non_blocking=True)
-                    pending = True
+                pending = True
         if pending:
             stream.synchronize()
         t2 = time.perf_counter()
@@ -530,13 +582,20 @@ class BatchRunner:
         for ps in live:
             stop, nev = int(self.stop_h[ps.i]), int(self.nev_h[ps.i])
             last = ps.j + stop if stop >= 0 else ps.b_end - 1
-            if nev:
+            info = self._sview("info", ps.i, np.int64, 4)
+            if nev and info[2]:                     # overflowed the staging: full rows
                 k, e0 = last - ps.j + 1, ps.ev_base
                 ev = self.ev_h[e0:e0 + k].numpy()
                 for c in range(2):
                     hit = np.nonzero(ev[:, c] >= 0)[0]
                     b = ps.j + hit
                     ps.out[b - 1, c] = b * pb + ev[hit, c].astype(np.int64)
+            elif nev:
+                rec = self._sview("ev", ps.i, np.int32, 3 * self.max_events)[:3 * int(info[1])].reshape(-1, 3)
+                b = ps.j + rec[:, 0].astype(np.int64)
+                for c in range(2):
+                    hit = rec[:, 1 + c] >= 0
+                    ps.out[b[hit] - 1, c] = b[hit] * pb + rec[hit, 1 + c].astype(np.int64)
             picked = int(self.pick_h[ps.i]) if ps.Wg else -1
             # RNG position right after the last consumed batch shuffle
             if stop >= 0:
@@ -547,7 +606,13 @@ class BatchRunner:
                     ps.P = ps.P_tail_after
                 else:
                     ps.P = picked + 1
-                ps.train_rows = d * pb + self.small_h[ps.i][2][:ps.blen(d)].numpy().astype(np.int64)
+                if int(info[0]) != ps.P or int(info[3]) != d:
+                    raise RuntimeError(f"partition {ps.i}: staging disagrees (P {int(info[0])} vs {ps.P}, "
+                                       f"batch {int(info[3])} vs {d})")
+                L = ps.blen(d)
+                ps.staged = (self._sview("x", ps.i, np.float32, L * ps_feats(self.parts[ps.i])).reshape(L, -1).copy(),
+                             self._sview("y", ps.i, np.int32, L).astype(np.int64),
+                             self._sview("w", ps.i, np.uint32, self.n_words).copy())
                 ps.retrain = True
                 # adaptive speculation: the next concept likely lasts about as long as this one
                 seg = d - ps.seg_start + 1

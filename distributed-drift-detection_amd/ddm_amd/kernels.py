@@ -29,6 +29,13 @@ JOB_DTYPE = np.dtype([("R", "<u8"), ("Tsub", "<u8"), ("Tchunk", "<u8"), ("avail"
                       ("stop", "<u8"), ("pick_offset", "<i8"), ("pick_last", "<i8"), ("pick_out", "<u8")])
 assert JOB_DTYPE.itemsize == 120
 GEN_DTYPE = np.dtype([("state", "<u8"), ("R", "<u8"), ("n", "<i8")])
+STAGE_DTYPE = np.dtype([("X", "<u8"), ("ld", "<i8"), ("y", "<u8"), ("perm", "<u8"), ("base", "<i8"), ("ev", "<u8"),
+                        ("stop", "<u8"), ("pick", "<u8"), ("R", "<u8"), ("j", "<i8"), ("g0", "<i8"), ("nb", "<i8"),
+                        ("b_end", "<i8"), ("p_after_first", "<i8"), ("p_tail_after", "<i8"), ("pb", "<i4"),
+                        ("last_len", "<i4"), ("n_features", "<i4"), ("n_words", "<i4"), ("tail", "<i4"),
+                        ("max_events", "<i4"), ("x_out", "<u8"), ("y_out", "<u8"), ("w_out", "<u8"),
+                        ("info_out", "<u8"), ("ev_out", "<u8")])
+assert STAGE_DTYPE.itemsize == 184
 
 
 class PinnedTable:
@@ -53,6 +60,13 @@ def forest_predict_batch(table, n_segs, per_batch, stream, timer=None):
     the C-ABI assigns blocks and copies the table itself."""
     check(lib.ddm_forest_predict_batch(table.h.data_ptr(), table.d.data_ptr(), int(n_segs), int(per_batch),
                                        ctypes.c_void_p(stream.cuda_stream), *_evs(timer)), "ddm_forest_predict_batch")
+
+
+def epoch_stage(table, n_jobs, stream):
+    """ddm_epoch_stage over the first n_jobs records of a PinnedTable of STAGE_DTYPE."""
+    table.upload(n_jobs, stream)
+    check(lib.ddm_epoch_stage(table.d.data_ptr(), int(n_jobs), ctypes.c_void_p(stream.cuda_stream)),
+          "ddm_epoch_stage")
 
 
 def shuffle_generate_batch(table, n_jobs, stream):

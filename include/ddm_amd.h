@@ -280,6 +280,25 @@ int ddm_shuffle_pick_batch(const ddm_shuffle_job* jobs_dev, int32_t n_jobs, ddm_
 int ddm_shuffle_pick(const int32_t* stop, const int64_t* E, int64_t W, int64_t offset, int64_t last,
                      int64_t* out, ddm_stream_t stream);
 
+/* ---- epoch read-back staging (csrc/stage.hip) ------------------------------------ */
+/* After an epoch's kernels, per partition: the event rows of the scanned batches
+ * compacted into ev_out[max_events][3] = (window batch, warning pos, change pos) and,
+ * when the scan stopped at a change in batch d = j + *stop, batch d's rows in shuffled
+ * order (x_out [L][n_features] float32, y_out [L]) and n_words stream words from the draw
+ * P after batch d's shuffle (P = p_after_first if d < g0, p_tail_after for the host-
+ * shuffled short last batch when tail, else *pick + 1).  info_out = {P or -1, event
+ * count, overflow (count > max_events), d or -1}.  ev holds the partition's window rows
+ * [(b - j)][2] as ddm_scan_streams wrote them. */
+typedef struct ddm_stage_job {
+    const float* X; int64_t ld; const int32_t* y; const uint8_t* perm; int64_t base;
+    const int32_t* ev; const int32_t* stop; const int64_t* pick; const uint32_t* R;
+    int64_t j, g0, nb, b_end, p_after_first, p_tail_after;
+    int32_t pb, last_len, n_features, n_words, tail, max_events;
+    float* x_out; int32_t* y_out; uint32_t* w_out; int64_t* info_out; int32_t* ev_out;
+} ddm_stage_job;
+
+int ddm_epoch_stage(const ddm_stage_job* jobs_dev, int32_t n_jobs, ddm_stream_t stream);
+
 /* ---- host forest refit ------------------------------------------------------------ */
 
 /* RandomForestClassifier(n_estimators=n_trees).fit(X, y) exactly as scikit-learn 1.7.2
