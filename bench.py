@@ -112,7 +112,7 @@ def run_c3(args, world, rank, dev, torch, dist):
         kernels.synth_features(part.X, part.y[:n], gid, instances, args.seed, 0.04)
         parts.append((gid, part))
     # all partitions of this GPU in lockstep: one batched launch per kernel per epoch
-    runner = BatchRunner([p for _, p in parts], settings, torch.cuda.Stream(dev), refit=args.refit, timing=True,
+    runner = BatchRunner([p for _, p in parts], settings, torch.cuda.Stream(dev, priority=-1), refit=args.refit, timing=True,
                          fit_threads=args.fit_threads)
     torch.cuda.synchronize()
 

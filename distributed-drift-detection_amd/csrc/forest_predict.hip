@@ -73,7 +73,7 @@ struct Seg {
     int64_t row_base;            // rows are (g / per_batch) * per_batch + perm[g] - row_base
     int64_t block0, nblocks;     // this segment's blocks in the launch grid
     const uint8_t* cforest;      // compiled forest or NULL
-    int32_t cf_slots, cf_vote_regs, cf_leaves, cf_pad;
+    int32_t cf_slots, cf_vote_regs, cf_leaves, flags;
 };
 static_assert(sizeof(Seg) == sizeof(ddm_predict_segment) && sizeof(Seg) == 168, "Seg must mirror ddm_predict_segment");
 
@@ -539,7 +539,7 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
             ddm::set_error("ddm_forest_predict_batch: invalid segment %d", i);
             return DDM_E_ARG;
         }
-        if (g.first_err)
+        if (g.first_err && !(g.flags & DDM_SEG_FIRST_ERR_PRESET))
             if (int rc = ddm::hip_status(hipMemsetAsync(g.first_err, 0xff, sizeof(uint64_t), s), "predict_batch memset"))
                 return rc;
     }

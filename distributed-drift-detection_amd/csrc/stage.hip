@@ -9,12 +9,16 @@
 //     order (`batch_a = batch_b`, :208), i.e. X rows d*pb + perm[d*pb + k] and labels, and
 //     the stream words from the draw after batch d's shuffle, where batch d+1's shuffle
 //     and then the refit's 100 tree seeds are drawn (:190, :102).
-// One workgroup per partition; nothing here decides anything, it only moves bytes.
+// It also draws what the reference draws next from the same stream: batch d+1's
+// shuffle (written into the partition's perm array, DDM_Process.py:190) and the T tree
+// seeds of the refit (:102), from words staged in LDS (one lane runs Fisher-Yates).
+// One workgroup per partition; nothing here decides anything, the host still does.
 #include "common.h"
 
 namespace {
 
 constexpr int kStageThreads = 256;
+constexpr int kStageWords = 1024;   // stream words in LDS for one shuffle + the seeds
 
 struct Job {
     const float* X;
@@ -33,6 +37,9 @@ struct Job {
     uint32_t* w_out;
     int64_t* info_out;
     int32_t* ev_out;
+    uint8_t* perm_w;
+    int64_t* seeds_out;
+    int32_t n_trees, pad;
 };
 static_assert(sizeof(Job) == sizeof(ddm_stage_job), "Job must mirror ddm_stage_job");
 
@@ -101,6 +108,58 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     }
     if (jb.R)
         for (int w = t; w < jb.n_words; w += kStageThreads) jb.w_out[w] = jb.R[P + w];
+    // ---- batch j = d + 1: its shuffle, then the refit's tree seeds
+    __shared__ uint32_t words[kStageWords];
+    __shared__ uint8_t perm[256];
+    __shared__ int64_t pos[2];
+    __shared__ int ok;
+    const int64_t j = d + 1;
+    if (!jb.R || !jb.perm_w || !jb.seeds_out || j >= jb.nb) {
+        if (t == 0) jb.info_out[6] = 0;
+        return;
+    }
+    const int Lj = j == jb.nb - 1 ? jb.last_len : jb.pb;
+    for (int w = t; w < kStageWords; w += kStageThreads) words[w] = jb.R[P + w];
+    __syncthreads();
+    if (t == 0) {
+        int k = 0;
+        bool good = true;
+        for (int i = 0; i < Lj; ++i) perm[i] = (uint8_t)i;
+        for (int i = Lj - 1; i >= 1 && good; --i) {         // legacy permutation(Lj)
+            const uint32_t mask = 0xffffffffu >> __builtin_clz((uint32_t)i);
+            uint32_t v;
+            do {
+                if (k >= kStageWords) { good = false; break; }
+                v = words[k++] & mask;
+            } while (v > (uint32_t)i);
+            if (!good) break;
+            const uint8_t tmp = perm[i];
+            perm[i] = perm[v];
+            perm[v] = tmp;
+        }
+        pos[0] = P + k;
+        for (int tr = 0; tr < jb.n_trees && good; ++tr) {  // randint(2**31 - 1) x n_trees
+            uint32_t v;
+            do {
+                if (k >= kStageWords) { good = false; break; }
+                v = words[k++] & 0x7fffffffu;
+            } while (v > 0x7ffffffeu);
+            if (good) jb.seeds_out[tr] = (int64_t)v;
+        }
+        pos[1] = P + k;
+        ok = good ? 1 : 0;
+    }
+    __syncthreads();
+    if (!ok) {
+        if (t == 0) jb.info_out[6] = 0;
+        return;
+    }
+    for (int i = t; i < Lj; i += kStageThreads) jb.perm_w[jb.base + j * jb.pb + i] = perm[i];
+    if (t == 0) {
+        jb.info_out[4] = pos[0];
+        jb.info_out[5] = pos[1];
+        jb.info_out[6] = 1;
+    }
 }
 
 }  // namespace

@@ -148,7 +148,7 @@ class BatchRunner:
             raise ValueError("a BatchRunner drives the partitions of one device")
         self.device = dev
         self.s = settings or DDMSettings()
-        self.stream = stream or torch.cuda.Stream(dev)
+        self.stream = stream or torch.cuda.Stream(dev, priority=-1)   # epochs ahead of the generation
         self.refit_kind = refit
         self.fit_threads = max(1, int(fit_threads))
         pb = self.s.per_batch
@@ -188,7 +188,24 @@ class BatchRunner:
         k = _round_up(n, 2)
         self.o_first, self.o_nev, self.o_stop, self.o_pick = 0, 8 * k, 16 * k, 20 * k
         self.o_off, self.o_end, self.o_bbase, self.o_state = 28 * k, 36 * k, 44 * k, 52 * k
-        self.ctrl_bytes = _round_up(self.o_state + 56 * k, 64)
+        # one slab holds the control block, the shuffle-job and staging tables and the
+        # staging outputs: an epoch is one host->device copy of [0, o_stage) and one
+        # device->host copy of the whole slab
+        F = max(p.X.shape[0] for p in self.parts)
+        self.n_words = max(3 * pb + self.s.n_estimators + 64, 1024)   # >= the stage kernel's LDS words
+        self.max_events = 64
+        self.o_jobs = _round_up(self.o_state + 56 * k, 256)
+        self.o_stage_tab = self.o_jobs + _round_up(n * kernels.JOB_DTYPE.itemsize, 256)
+        self.o_stage = self.o_stage_tab + _round_up(n * kernels.STAGE_DTYPE.itemsize, 256)
+        sz = {"x": 4 * 256 * F, "y": 4 * 256, "w": 4 * self.n_words, "info": 64, "ev": 12 * self.max_events,
+              "seeds": 8 * self.s.n_estimators}
+        self.stage_off, self.stage_stride = {}, {}
+        o = self.o_stage
+        for key, nbytes in sz.items():
+            self.stage_off[key] = o
+            self.stage_stride[key] = _round_up(nbytes, 256)
+            o += self.stage_stride[key] * n
+        self.ctrl_bytes = o
         self.ctrl_h = torch.zeros(self.ctrl_bytes, dtype=torch.uint8, pin_memory=True)
         self.ctrl_d = torch.zeros(self.ctrl_bytes, dtype=torch.uint8, device=dev)
         c = self.ctrl_h.numpy()
@@ -202,7 +219,10 @@ class BatchRunner:
         self.state_h = c[self.o_state:self.o_state + 56 * n].view(kernels.STATE_DTYPE)
         self.bbase_h[:] = self.ev_bases
         self.segs = kernels.PinnedTable(kernels.SEG_DTYPE, n, dev)
-        self.jobs = kernels.PinnedTable(kernels.JOB_DTYPE, n, dev)
+        self.jobs = kernels.PinnedTable(kernels.JOB_DTYPE, n, dev, self.ctrl_h[self.o_jobs:],
+                                        self.ctrl_d[self.o_jobs:])
+        self.stage_jobs = kernels.PinnedTable(kernels.STAGE_DTYPE, n, dev, self.ctrl_h[self.o_stage_tab:],
+                                              self.ctrl_d[self.o_stage_tab:])
         # the partitions' MT19937 streams are generated and tabulated on a side stream, in
         # pieces, while the epochs run (GpuShuffle.wait_for orders the consumers)
         self.gen_stream = torch.cuda.Stream(dev)
@@ -214,22 +234,6 @@ class BatchRunner:
         for part, nb, mw in zip(self.parts, self.nbs, self.max_wins):
             cap = int(nb * expected_draws_per_batch(pb) * 1.2) + 64 * 1024
             self.shuffles.append(GpuShuffle(dev, pb, cap, mw, self.stream, self.gen_stream))
-        # epoch read-back staging (csrc/stage.hip): per partition the compacted events and,
-        # on a change, the training batch and the stream words after its shuffle; copied
-        # back together with the control block, so an epoch costs ONE synchronisation
-        self.n_words = 3 * pb + self.s.n_estimators + 64
-        self.max_events = 64
-        F = max(p.X.shape[0] for p in self.parts)
-        sz = {"x": 4 * 256 * F, "y": 4 * 256, "w": 4 * self.n_words, "info": 32, "ev": 12 * self.max_events}
-        self.stage_off = {}
-        o = 0
-        for key, nbytes in sz.items():
-            self.stage_off[key] = o
-            o += _round_up(nbytes, 256) * n
-        self.stage_stride = {k: _round_up(v, 256) for k, v in sz.items()}
-        self.stage_d = torch.zeros(o, dtype=torch.uint8, device=dev)
-        self.stage_h = torch.zeros(o, dtype=torch.uint8, pin_memory=True)
-        self.stage_jobs = kernels.PinnedTable(kernels.STAGE_DTYPE, n, dev)
         self.stats = RunStats()
 
     # -- helpers
@@ -237,11 +241,11 @@ class BatchRunner:
         return self.ctrl_d.data_ptr() + off + size * i
 
     def _sptr(self, key, i):
-        return self.stage_d.data_ptr() + self.stage_off[key] + self.stage_stride[key] * i
+        return self.ctrl_d.data_ptr() + self.stage_off[key] + self.stage_stride[key] * i
 
     def _sview(self, key, i, dtype, count):
         a = self.stage_off[key] + self.stage_stride[key] * i
-        return self.stage_h.numpy()[a:a + np.dtype(dtype).itemsize * count].view(dtype)
+        return self.ctrl_h.numpy()[a:a + np.dtype(dtype).itemsize * count].view(dtype)
 
     def _ensure_all(self, wants, wait=True):
         """wants: [(partition index, draws needed)].  Partitions whose enqueued stream falls
@@ -321,17 +325,21 @@ class BatchRunner:
         work = []
         for k, ps in enumerate(need):
             sh = self.shuffles[ps.i]
-            words = ps.staged[2] if ps.staged is not None else self.words_h[k].numpy().view(np.uint32)
-            L = ps.blen(ps.j)
-            r = perm_seeds_from_words(words, L, T)
-            if r is None:                                       # rejections ran past the read-back
-                permj, P1 = sh.host_perm(ps.P, L)
-                seeds, P2 = sh.host_seeds(P1, T)
+            if ps.staged is not None and ps.staged[3] is not None:
+                # batch j's shuffle is already in perm_all and the seeds came back staged
+                seeds, P1, P2 = ps.staged[3], ps.staged[4], ps.staged[5]
             else:
-                permj, seeds = r[0], r[1]
-                P1 = ps.P + r[2]
-                P2 = P1 + r[3]
-            self._upload_perm(ps.i, ps.j, permj, 0)             # batch_b.sample before the fit (:190, :194)
+                words = ps.staged[2] if ps.staged is not None else self.words_h[k].numpy().view(np.uint32)
+                L = ps.blen(ps.j)
+                r = perm_seeds_from_words(words, L, T)
+                if r is None:                                   # rejections ran past the read-back
+                    permj, P1 = sh.host_perm(ps.P, L)
+                    seeds, P2 = sh.host_seeds(P1, T)
+                else:
+                    permj, seeds = r[0], r[1]
+                    P1 = ps.P + r[2]
+                    P2 = P1 + r[3]
+                self._upload_perm(ps.i, ps.j, permj, 0)         # batch_b.sample before the fit (:190, :194)
             P_seeds, ps.P = P1, P2                              # 100 tree seeds follow the shuffle
             ps.P_after_first = ps.P
             if ps.staged is not None:
@@ -376,7 +384,28 @@ class BatchRunner:
             ex.shutdown(wait=True)
             self._executor = None
 
-    def _jobs_for(self, live, with_stop):
+    def _stage_table(self, live):
+        """ddm_stage_job records of this epoch (csrc/stage.hip)."""
+        srec = self.stage_jobs.rec
+        pb = self.s.per_batch
+        for k, ps in enumerate(live):
+            part, r = self.parts[ps.i], srec[k]
+            r["X"], r["ld"], r["y"] = part.X.data_ptr(), part.X.shape[1], part.y.data_ptr()
+            r["perm"], r["base"] = self.perm_all.data_ptr(), ps.base
+            r["ev"] = self.ev_d.data_ptr() + 8 * ps.ev_base
+            r["stop"], r["pick"] = self._dptr(self.o_stop, ps.i, 4), self._dptr(self.o_pick, ps.i, 8)
+            r["R"] = self.shuffles[ps.i].R.data_ptr()
+            r["j"], r["g0"], r["nb"], r["b_end"] = ps.j, ps.g0, ps.nb, ps.b_end
+            r["p_after_first"] = -1 if ps.P_after_first is None else ps.P_after_first
+            r["p_tail_after"] = -1 if ps.P_tail_after is None else ps.P_tail_after
+            r["pb"], r["last_len"], r["n_features"] = pb, ps.last_len, part.X.shape[0]
+            r["n_words"], r["tail"], r["max_events"] = self.n_words, int(bool(ps.tail)), self.max_events
+            r["x_out"], r["y_out"], r["w_out"] = self._sptr("x", ps.i), self._sptr("y", ps.i), self._sptr("w", ps.i)
+            r["info_out"], r["ev_out"] = self._sptr("info", ps.i), self._sptr("ev", ps.i)
+            r["perm_w"], r["seeds_out"] = self.perm_all.data_ptr(), self._sptr("seeds", ps.i)
+            r["n_trees"] = self.s.n_estimators
+
+    def _jobs_for(self, live, with_stop, upload=True):
         """Fill the job table for partitions with device shuffles this epoch."""
         rec = self.jobs.rec
         for k, ps in enumerate(live):
@@ -388,7 +417,8 @@ class BatchRunner:
             else:                                # end of the window's GPU batches (tail epochs)
                 self.shuffles[ps.i].fill_job(rec[k], ps.P, ps.Wg, out_ptr, 0, 0, ps.Wg - 1,
                                              self._dptr(self.o_pick, ps.i, 8))
-        self.jobs.upload(len(live), self.stream)
+        if upload:
+            self.jobs.upload(len(live), self.stream)
 
     def run(self, rngs):
         """Returns, per partition, int64 [n_batches-1, 2]: partition rows of (first warning,
@@ -512,18 +542,20 @@ class BatchRunner:
             sg["nodes"], sg["roots"], sg["leaf_value"], sg["classes"] = d.nodes, d.roots, d.leaf_value or 0, d.classes
             sg["n_trees"], sg["n_classes"], sg["n_nodes"], sg["pure"] = d.n_trees, d.n_classes, d.n_nodes, d.pure
             sg["cforest"], sg["cf_slots"], sg["cf_vote_regs"] = d.cforest or 0, d.cf_slots, d.cf_vote_regs
-            sg["cf_leaves"] = d.cf_leaves
+            sg["cf_leaves"], sg["flags"] = d.cf_leaves, kernels.SEG_FIRST_ERR_PRESET
         t2 = time.perf_counter()
         host += t2 - t1
         t1 = t2
         n = len(self.parts)
         base = self.ctrl_d.data_ptr()
-        with torch.cuda.stream(stream):
-            self.ctrl_d[self.o_off:].copy_(self.ctrl_h[self.o_off:], non_blocking=True)
         if shuf:
-            self._jobs_for(shuf, with_stop=True)
-            if not shuffled:
-                kernels.shuffle_window_batch(self.jobs, len(shuf), max_W, max_pieces, pb, stream, self.t_shuf)
+            self._jobs_for(shuf, with_stop=True, upload=False)
+        self._stage_table(live)
+        self.first_h[:] = -1                    # the predict kernels' first-error slots
+        with torch.cuda.stream(stream):
+            self.ctrl_d[:self.o_stage].copy_(self.ctrl_h[:self.o_stage], non_blocking=True)
+        if shuf and not shuffled:
+            kernels.shuffle_window_batch(self.jobs, len(shuf), max_W, max_pieces, pb, stream, self.t_shuf)
         kernels.forest_predict_batch(self.segs, len(live), pb, stream, self.t_pred)
         kernels.scan_streams_raw(self.err_all.data_ptr(), base + self.o_off, n, self.params, base + self.o_state,
                                  base + self.o_bbase, self.ev_total, self.ev_d.data_ptr(), base + self.o_first,
@@ -532,26 +564,9 @@ class BatchRunner:
         if shuf:
             kernels.shuffle_pick_batch(self.jobs, len(shuf), stream)
         # stage what the host needs next, then one copy back and one synchronisation
-        srec = self.stage_jobs.rec
-        for k, ps in enumerate(live):
-            part, r = self.parts[ps.i], srec[k]
-            r["X"], r["ld"], r["y"] = part.X.data_ptr(), part.X.shape[1], part.y.data_ptr()
-            r["perm"], r["base"] = self.perm_all.data_ptr(), ps.base
-            r["ev"] = self.ev_d.data_ptr() + 8 * ps.ev_base
-            r["stop"], r["pick"] = self._dptr(self.o_stop, ps.i, 4), self._dptr(self.o_pick, ps.i, 8)
-            r["R"] = self.shuffles[ps.i].R.data_ptr()
-            r["j"], r["g0"], r["nb"], r["b_end"] = ps.j, ps.g0, ps.nb, ps.b_end
-            r["p_after_first"] = -1 if ps.P_after_first is None else ps.P_after_first
-            r["p_tail_after"] = -1 if ps.P_tail_after is None else ps.P_tail_after
-            r["pb"], r["last_len"], r["n_features"] = pb, ps.last_len, part.X.shape[0]
-            r["n_words"], r["tail"], r["max_events"] = self.n_words, int(bool(ps.tail)), self.max_events
-            r["x_out"], r["y_out"], r["w_out"] = self._sptr("x", ps.i), self._sptr("y", ps.i), self._sptr("w", ps.i)
-            r["info_out"], r["ev_out"] = self._sptr("info", ps.i), self._sptr("ev", ps.i)
-        kernels.epoch_stage(self.stage_jobs, len(live), stream)
+        kernels.epoch_stage(self.stage_jobs, len(live), stream, upload=False)
         with torch.cuda.stream(stream):
-            self.ctrl_h[:self.o_off].copy_(self.ctrl_d[:self.o_off], non_blocking=True)
-            self.ctrl_h[self.o_state:].copy_(self.ctrl_d[self.o_state:], non_blocking=True)
-            self.stage_h.copy_(self.stage_d, non_blocking=True)
+            self.ctrl_h.copy_(self.ctrl_d, non_blocking=True)
         stream.synchronize()
         if self.timing:
             st.predict_ms += self.t_pred.elapsed_ms()
@@ -568,7 +583,7 @@ class BatchRunner:
             if self.timing:
                 st.predict_bytes += (p1 - p0) * (4 * ps.forest.features_read + 6)
                 st.scan_rows += min(p1, ps.base + (ps_last + 1) * pb) - p0
-            info = self._sview("info", ps.i, np.int64, 4)
+            info = self._sview("info", ps.i, np.int64, 7)
             if nev and info[2]:
                 k, e0 = ps_last - ps.j + 1, ps.ev_base
                 with torch.cuda.stream(stream):
@@ -582,7 +597,7 @@ class BatchRunner:
         for ps in live:
             stop, nev = int(self.stop_h[ps.i]), int(self.nev_h[ps.i])
             last = ps.j + stop if stop >= 0 else ps.b_end - 1
-            info = self._sview("info", ps.i, np.int64, 4)
+            info = self._sview("info", ps.i, np.int64, 7)
             if nev and info[2]:                     # overflowed the staging: full rows
                 k, e0 = last - ps.j + 1, ps.ev_base
                 ev = self.ev_h[e0:e0 + k].numpy()
@@ -610,13 +625,18 @@ class BatchRunner:
                     raise RuntimeError(f"partition {ps.i}: staging disagrees (P {int(info[0])} vs {ps.P}, "
                                        f"batch {int(info[3])} vs {d})")
                 L = ps.blen(d)
+                drawn = int(info[6]) == 1           # batch d+1's shuffle and the seeds, on the device
                 ps.staged = (self._sview("x", ps.i, np.float32, L * ps_feats(self.parts[ps.i])).reshape(L, -1).copy(),
                              self._sview("y", ps.i, np.int32, L).astype(np.int64),
-                             self._sview("w", ps.i, np.uint32, self.n_words).copy())
+                             None if drawn else self._sview("w", ps.i, np.uint32, self.n_words).copy(),
+                             self._sview("seeds", ps.i, np.int64, self.s.n_estimators).copy() if drawn else None,
+                             int(info[4]), int(info[5]))
                 ps.retrain = True
-                # adaptive speculation: the next concept likely lasts about as long as this one
+                # adaptive speculation: the next concept likely lasts about as long as this
+                # one, so the next window covers it with 1/8 to spare (one epoch per drift
+                # when concepts repeat their length; windows still double after a miss)
                 seg = d - ps.seg_start + 1
-                ps.win = max(max(1, s.window_batches), seg // 2)
+                ps.win = max(max(1, s.window_batches), seg + seg // 8)
                 ps.j = d + 1
             else:
                 if ps.tail:

@@ -22,7 +22,8 @@ SEG_DTYPE = np.dtype([("X", "<u8"), ("ld", "<i8"), ("y", "<u8"), ("perm", "<u8")
                       ("roots", "<u8"), ("leaf_value", "<u8"), ("classes", "<u8"), ("n_trees", "<i4"),
                       ("n_classes", "<i4"), ("n_nodes", "<i4"), ("pure", "<i4"), ("row_base", "<i8"),
                       ("block0", "<i8"), ("nblocks", "<i8"), ("cforest", "<u8"), ("cf_slots", "<i4"),
-                      ("cf_vote_regs", "<i4"), ("cf_leaves", "<i4"), ("cf_pad", "<i4")])
+                      ("cf_vote_regs", "<i4"), ("cf_leaves", "<i4"), ("flags", "<i4")])
+SEG_FIRST_ERR_PRESET = 1
 assert SEG_DTYPE.itemsize == 168
 JOB_DTYPE = np.dtype([("R", "<u8"), ("Tsub", "<u8"), ("Tchunk", "<u8"), ("avail", "<i8"), ("P", "<i8"), ("W", "<i8"),
                       ("pieces", "<u8"), ("info", "<u8"), ("J", "<u8"), ("E", "<u8"), ("perm_out", "<u8"),
@@ -34,18 +35,20 @@ STAGE_DTYPE = np.dtype([("X", "<u8"), ("ld", "<i8"), ("y", "<u8"), ("perm", "<u8
                         ("b_end", "<i8"), ("p_after_first", "<i8"), ("p_tail_after", "<i8"), ("pb", "<i4"),
                         ("last_len", "<i4"), ("n_features", "<i4"), ("n_words", "<i4"), ("tail", "<i4"),
                         ("max_events", "<i4"), ("x_out", "<u8"), ("y_out", "<u8"), ("w_out", "<u8"),
-                        ("info_out", "<u8"), ("ev_out", "<u8")])
-assert STAGE_DTYPE.itemsize == 184
+                        ("info_out", "<u8"), ("ev_out", "<u8"), ("perm_w", "<u8"), ("seeds_out", "<u8"),
+                        ("n_trees", "<i4"), ("pad", "<i4")])
+assert STAGE_DTYPE.itemsize == 208
 
 
 class PinnedTable:
-    """A pinned host table of `dtype` records mirrored by a device buffer."""
+    """A pinned host table of `dtype` records mirrored by a device buffer (its own, or
+    byte views h / d of a larger pair of buffers that are copied as a whole)."""
 
-    def __init__(self, dtype, n, device):
+    def __init__(self, dtype, n, device, h=None, d=None):
         self.dtype, self.n = dtype, int(n)
         nbytes = max(1, self.n) * dtype.itemsize
-        self.h = torch.zeros(nbytes, dtype=torch.uint8, pin_memory=True)
-        self.d = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+        self.h = torch.zeros(nbytes, dtype=torch.uint8, pin_memory=True) if h is None else h[:nbytes]
+        self.d = torch.zeros(nbytes, dtype=torch.uint8, device=device) if d is None else d[:nbytes]
         self.rec = self.h.numpy().view(dtype)
 
     def upload(self, count, stream):
@@ -62,9 +65,11 @@ def forest_predict_batch(table, n_segs, per_batch, stream, timer=None):
                                        ctypes.c_void_p(stream.cuda_stream), *_evs(timer)), "ddm_forest_predict_batch")
 
 
-def epoch_stage(table, n_jobs, stream):
-    """ddm_epoch_stage over the first n_jobs records of a PinnedTable of STAGE_DTYPE."""
-    table.upload(n_jobs, stream)
+def epoch_stage(table, n_jobs, stream, upload=True):
+    """ddm_epoch_stage over the first n_jobs records of a PinnedTable of STAGE_DTYPE
+    (upload=False: the caller already copied the table to the device)."""
+    if upload:
+        table.upload(n_jobs, stream)
     check(lib.ddm_epoch_stage(table.d.data_ptr(), int(n_jobs), ctypes.c_void_p(stream.cuda_stream)),
           "ddm_epoch_stage")
 

@@ -170,8 +170,12 @@ typedef struct ddm_predict_segment {
     int64_t block0, nblocks;
     const uint8_t* cforest; /* compiled forest (device) or NULL                              */
     int32_t cf_slots, cf_vote_regs;   /* its n_slots, vote_regs, n_leaves                   */
-    int32_t cf_leaves, cf_pad;
+    int32_t cf_leaves, flags;         /* flags: DDM_SEG_FIRST_ERR_PRESET                     */
 } ddm_predict_segment;
+
+/* ddm_predict_segment.flags: the caller already set *first_err to UINT64_MAX (e.g. in
+ * the same host->device copy as its other inputs), so the call does not reset it. */
+#define DDM_SEG_FIRST_ERR_PRESET 1
 
 int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, ddm_predict_segment* segs_dev,
                              int32_t n_segs, int32_t per_batch, ddm_stream_t stream,
@@ -286,15 +290,21 @@ int ddm_shuffle_pick(const int32_t* stop, const int64_t* E, int64_t W, int64_t o
  * when the scan stopped at a change in batch d = j + *stop, batch d's rows in shuffled
  * order (x_out [L][n_features] float32, y_out [L]) and n_words stream words from the draw
  * P after batch d's shuffle (P = p_after_first if d < g0, p_tail_after for the host-
- * shuffled short last batch when tail, else *pick + 1).  info_out = {P or -1, event
- * count, overflow (count > max_events), d or -1}.  ev holds the partition's window rows
- * [(b - j)][2] as ddm_scan_streams wrote them. */
+ * shuffled short last batch when tail, else *pick + 1).  Then, if batch d+1 exists, its
+ * shuffle is drawn from P into perm_w (at base + (d+1)*pb) and the n_trees refit seeds
+ * after it into seeds_out.  info_out = {P or -1, event count, overflow (count >
+ * max_events), d or -1, draw after batch d+1's shuffle, draw after the seeds, 1 if those
+ * two were drawn}.  ev holds the partition's window rows [(b - j)][2] as
+ * ddm_scan_streams wrote them. */
 typedef struct ddm_stage_job {
     const float* X; int64_t ld; const int32_t* y; const uint8_t* perm; int64_t base;
     const int32_t* ev; const int32_t* stop; const int64_t* pick; const uint32_t* R;
     int64_t j, g0, nb, b_end, p_after_first, p_tail_after;
     int32_t pb, last_len, n_features, n_words, tail, max_events;
     float* x_out; int32_t* y_out; uint32_t* w_out; int64_t* info_out; int32_t* ev_out;
+    uint8_t* perm_w;        /* perm array to receive batch d+1's shuffle (may be NULL)   */
+    int64_t* seeds_out;     /* [n_trees] refit seeds drawn after it (may be NULL)        */
+    int32_t n_trees, pad;
 } ddm_stage_job;
 
 int ddm_epoch_stage(const ddm_stage_job* jobs_dev, int32_t n_jobs, ddm_stream_t stream);
