@@ -126,6 +126,12 @@ class _Part:
     def blen(self, b):
         return self.last_len if b == self.nb - 1 else self.pb
 
+    def b_end_is_tail(self, pb):
+        """This epoch's window reaches a short last batch (shuffled on the host)."""
+        g0 = self.j + 1 if self.retrain else self.j
+        b_end = min(self.nb, self.j + min(self.win, self.max_win))
+        return b_end == self.nb and self.last_len != pb and self.nb - 1 >= g0
+
 
 class BatchRunner:
     """Runs the speculative shuffle+predict+scan epochs of many partitions in lockstep on
@@ -284,8 +290,8 @@ class BatchRunner:
         with torch.cuda.stream(self.stream):
             self.perm_all[at:at + len(perm)].copy_(h[:len(perm)], non_blocking=True)
 
-    def _refits(self, need):
-        """Refit every partition in `need` on its drift batch (train_rows, shuffled order).
+    def _refit_prep(self, need):
+        """Inputs of the refit of every partition in `need` on its drift batch (shuffled order).
 
         One read-back serves all of them: the stream words from each P (batch j's shuffle,
         then the T tree seeds, DDM_Process.py:190,:102) and the drift batches' rows; the
@@ -350,6 +356,15 @@ class BatchRunner:
             else:
                 X32, y = rows_dev[k][0].numpy(), rows_dev[k][1].numpy().astype(np.int64)
             work.append((ps, X32, y, seeds, P_seeds))
+            ps.g0 = ps.j + 1
+            ps.seg_start = ps.j
+        st.refit_s += time.perf_counter() - t0
+        return work
+
+    def _refit_fit(self, work):
+        """The refits themselves (all partitions in one native call) and the forests' upload."""
+        st = self.stats
+        t0 = time.perf_counter()
         fits = [None] * len(work)
         if self.refit_kind == "native":
             t2 = time.perf_counter()
@@ -367,8 +382,6 @@ class BatchRunner:
             ps.forest = f
             ps.retrain = False
             ps.state = kernels.fresh_states(1)                  # ddm = None -> new DDM (:136-139)
-            ps.g0 = ps.j + 1
-            ps.seg_start = ps.j
         st.refits += len(work)
         st.refit_s += time.perf_counter() - t0
 
@@ -384,39 +397,53 @@ class BatchRunner:
             ex.shutdown(wait=True)
             self._executor = None
 
-    def _stage_table(self, live):
-        """ddm_stage_job records of this epoch (csrc/stage.hip)."""
-        srec = self.stage_jobs.rec
+    def _segment_table(self, live):
+        """ddm_predict_segment records (forest predict) of this epoch."""
         pb = self.s.per_batch
-        for k, ps in enumerate(live):
-            part, r = self.parts[ps.i], srec[k]
-            r["X"], r["ld"], r["y"] = part.X.data_ptr(), part.X.shape[1], part.y.data_ptr()
-            r["perm"], r["base"] = self.perm_all.data_ptr(), ps.base
-            r["ev"] = self.ev_d.data_ptr() + 8 * ps.ev_base
-            r["stop"], r["pick"] = self._dptr(self.o_stop, ps.i, 4), self._dptr(self.o_pick, ps.i, 8)
-            r["R"] = self.shuffles[ps.i].R.data_ptr()
-            r["j"], r["g0"], r["nb"], r["b_end"] = ps.j, ps.g0, ps.nb, ps.b_end
-            r["p_after_first"] = -1 if ps.P_after_first is None else ps.P_after_first
-            r["p_tail_after"] = -1 if ps.P_tail_after is None else ps.P_tail_after
-            r["pb"], r["last_len"], r["n_features"] = pb, ps.last_len, part.X.shape[0]
-            r["n_words"], r["tail"], r["max_events"] = self.n_words, int(bool(ps.tail)), self.max_events
-            r["x_out"], r["y_out"], r["w_out"] = self._sptr("x", ps.i), self._sptr("y", ps.i), self._sptr("w", ps.i)
-            r["info_out"], r["ev_out"] = self._sptr("info", ps.i), self._sptr("ev", ps.i)
-            r["perm_w"], r["seeds_out"] = self.perm_all.data_ptr(), self._sptr("seeds", ps.i)
-            r["n_trees"] = self.s.n_estimators
+        rows = []
+        perm, err = self.perm_all.data_ptr(), self.err_all.data_ptr()
+        for ps in live:
+            part, d = self.parts[ps.i], ps.forest.desc
+            p0 = ps.base + ps.j * pb
+            p1 = ps.base + (ps.b_end - 1) * pb + ps.blen(ps.b_end - 1)
+            rows.append((part.X.data_ptr(), part.X.shape[1], part.y.data_ptr(), perm, err, 0,
+                         self._dptr(self.o_first, ps.i, 8), p0, p1, d.nodes, d.roots, d.leaf_value or 0, d.classes,
+                         d.n_trees, d.n_classes, d.n_nodes, d.pure, ps.base, 0, 0, d.cforest or 0, d.cf_slots,
+                         d.cf_vote_regs, d.cf_leaves, kernels.SEG_FIRST_ERR_PRESET))
+        self.segs.rec[:len(rows)] = np.array(rows, dtype=kernels.SEG_DTYPE)
+
+    def _stage_table(self, live):
+        """ddm_stage_job records of this epoch (csrc/stage.hip), built as tuples and
+        stored with one structured-array assignment."""
+        pb, T = self.s.per_batch, self.s.n_estimators
+        perm, ev = self.perm_all.data_ptr(), self.ev_d.data_ptr()
+        rows = []
+        for ps in live:
+            part = self.parts[ps.i]
+            rows.append((part.X.data_ptr(), part.X.shape[1], part.y.data_ptr(), perm, ps.base, ev + 8 * ps.ev_base,
+                         self._dptr(self.o_stop, ps.i, 4), self._dptr(self.o_pick, ps.i, 8),
+                         self.shuffles[ps.i].R.data_ptr(), ps.j, ps.g0, ps.nb, ps.b_end,
+                         -1 if ps.P_after_first is None else ps.P_after_first,
+                         -1 if ps.P_tail_after is None else ps.P_tail_after, pb, ps.last_len, part.X.shape[0],
+                         self.n_words, int(bool(ps.tail)), self.max_events, self._sptr("x", ps.i),
+                         self._sptr("y", ps.i), self._sptr("w", ps.i), self._sptr("info", ps.i),
+                         self._sptr("ev", ps.i), perm, self._sptr("seeds", ps.i), T, 0))
+        self.stage_jobs.rec[:len(rows)] = np.array(rows, dtype=kernels.STAGE_DTYPE)
 
     def _jobs_for(self, live, with_stop, upload=True):
         """Fill the job table for partitions with device shuffles this epoch."""
-        rec = self.jobs.rec
-        for k, ps in enumerate(live):
-            pb = self.s.per_batch
+        rows = []
+        pb = self.s.per_batch
+        for ps in live:
             out_ptr = self.perm_all.data_ptr() + self.bases[ps.i] + ps.g0 * pb
             if with_stop:
-                self.shuffles[ps.i].fill_job(rec[k], ps.P, ps.Wg, out_ptr, self._dptr(self.o_stop, ps.i, 4),
-                                             ps.g0 - ps.j, ps.b_end - 1 - ps.j, self._dptr(self.o_pick, ps.i, 8))
+                rows.append(self.shuffles[ps.i].job_tuple(ps.P, ps.Wg, out_ptr, self._dptr(self.o_stop, ps.i, 4),
+                                                          ps.g0 - ps.j, ps.b_end - 1 - ps.j,
+                                                          self._dptr(self.o_pick, ps.i, 8)))
             else:                                # end of the window's GPU batches (tail epochs)
-                self.shuffles[ps.i].fill_job(rec[k], ps.P, ps.Wg, out_ptr, 0, 0, ps.Wg - 1,
-                                             self._dptr(self.o_pick, ps.i, 8))
+                rows.append(self.shuffles[ps.i].job_tuple(ps.P, ps.Wg, out_ptr, 0, 0, ps.Wg - 1,
+                                                          self._dptr(self.o_pick, ps.i, 8)))
+        self.jobs.rec[:len(rows)] = np.array(rows, dtype=kernels.JOB_DTYPE)
         if upload:
             self.jobs.upload(len(live), self.stream)
 
@@ -489,8 +516,10 @@ class BatchRunner:
         need = [ps for ps in live if ps.retrain]
         for ps in live:
             ps.P_after_first = None
-        if need:
-            self._refits(need)
+        work = self._refit_prep(need) if need else []
+        late_fit = bool(work) and not any(ps.b_end_is_tail(pb) for ps in live)
+        if work and not late_fit:
+            self._refit_fit(work)
         t1 = time.perf_counter()
         host = t1 - t0 - (self.stats.refit_s - refit_before)
         for ps in live:
@@ -523,26 +552,17 @@ class BatchRunner:
                 P_tail = int(self.pick_h[ps.i]) + 1 if ps.Wg else ps.P
                 permT, ps.P_tail_after = self.shuffles[ps.i].host_perm(P_tail, ps.last_len)
                 self._upload_perm(ps.i, ps.nb - 1, permT, 1)
-        # segment table (predict), scan ranges and carried DDM states
-        segs = self.segs.rec
+        # scan ranges and carried DDM states (the control block), segment table (predict)
         self.off_h[:] = 0
         self.end_h[:] = 0
-        for k, ps in enumerate(live):
-            part, f = self.parts[ps.i], ps.forest
+        for ps in live:
             p0 = ps.base + ps.j * pb
             p1 = ps.base + (ps.b_end - 1) * pb + ps.blen(ps.b_end - 1)
             self.off_h[ps.i], self.end_h[ps.i] = p0, p1
-            self.state_h[ps.i] = ps.state[0]
-            sg = segs[k]
-            sg["X"], sg["ld"], sg["y"] = part.X.data_ptr(), part.X.shape[1], part.y.data_ptr()
-            sg["perm"], sg["err"], sg["pred"] = self.perm_all.data_ptr(), self.err_all.data_ptr(), 0
-            sg["first_err"] = self._dptr(self.o_first, ps.i, 8)
-            sg["pos_begin"], sg["pos_end"], sg["row_base"] = p0, p1, ps.base
-            d = f.desc
-            sg["nodes"], sg["roots"], sg["leaf_value"], sg["classes"] = d.nodes, d.roots, d.leaf_value or 0, d.classes
-            sg["n_trees"], sg["n_classes"], sg["n_nodes"], sg["pure"] = d.n_trees, d.n_classes, d.n_nodes, d.pure
-            sg["cforest"], sg["cf_slots"], sg["cf_vote_regs"] = d.cforest or 0, d.cf_slots, d.cf_vote_regs
-            sg["cf_leaves"], sg["flags"] = d.cf_leaves, kernels.SEG_FIRST_ERR_PRESET
+            # a refitting partition starts a fresh DDM (:136-139), whenever its fit runs
+            self.state_h[ps.i] = kernels.fresh_states(1)[0] if ps.retrain else ps.state[0]
+        if not late_fit:
+            self._segment_table(live)
         t2 = time.perf_counter()
         host += t2 - t1
         t1 = t2
@@ -556,6 +576,11 @@ class BatchRunner:
             self.ctrl_d[:self.o_stage].copy_(self.ctrl_h[:self.o_stage], non_blocking=True)
         if shuf and not shuffled:
             kernels.shuffle_window_batch(self.jobs, len(shuf), max_W, max_pieces, pb, stream, self.t_shuf)
+        if late_fit:
+            # the window shuffles do not depend on the new forests: they run on the GPU
+            # while the host fits them
+            self._refit_fit(work)
+            self._segment_table(live)
         kernels.forest_predict_batch(self.segs, len(live), pb, stream, self.t_pred)
         kernels.scan_streams_raw(self.err_all.data_ptr(), base + self.o_off, n, self.params, base + self.o_state,
                                  base + self.o_bbase, self.ev_total, self.ev_d.data_ptr(), base + self.o_first,

@@ -12,6 +12,7 @@ reset from) and produces:
   * numpy_state(X)      numpy's exact (key, pos) after X draws (tempering is invertible)
 """
 import ctypes
+import functools
 
 import numpy as np
 import torch
@@ -21,6 +22,7 @@ from ._capi import check, lib
 SUB, CHUNK = 128, 8192
 
 
+@functools.lru_cache(maxsize=None)
 def expected_draws_per_batch(L):
     """Mean 32-bit draws of `permutation(L)`: interval i takes (mask(i)+1)/(i+1) draws."""
     return sum(((1 << int(i).bit_length()) / (i + 1)) for i in range(1, L))
@@ -215,6 +217,13 @@ class GpuShuffle:
             ev.record(self.gen_stream)
             self.mark_ready(ev)
         self.wait_for(upto)
+
+    def job_tuple(self, P, W, perm_out_ptr, stop_ptr=0, pick_offset=0, pick_last=0, pick_out_ptr=0):
+        """fill_job's record as a tuple in kernels.JOB_DTYPE field order."""
+        assert 0 <= W <= self.max_window
+        return (self.R.data_ptr(), self.Tsub.data_ptr(), self.Tchunk.data_ptr(), self.waited * CHUNK, int(P), int(W),
+                self.pieces.data_ptr(), self.info.data_ptr(), self.J.data_ptr(), self.E.data_ptr(), int(perm_out_ptr),
+                int(stop_ptr), int(pick_offset), int(pick_last), int(pick_out_ptr))
 
     def fill_job(self, rec, P, W, perm_out_ptr, stop_ptr=0, pick_offset=0, pick_last=0, pick_out_ptr=0):
         """One ddm_shuffle_job record (kernels.JOB_DTYPE) for a window of W batches from draw P;
