@@ -169,7 +169,49 @@ extern "C" int ddm_forest_compile(const ddm_node* nodes, int32_t n_nodes, const 
     const int64_t trees_off = align16(stumps_off + 4 * (int64_t)S * sw);
     const int64_t nodes_off = align16(trees_off + (int64_t)sizeof(ddm_cforest_tree) * trees.size());
     const int64_t leafcls_off = align16(nodes_off + (int64_t)sizeof(ddm_cforest_node) * gnodes.size());
-    const int64_t total = align16(leafcls_off + (int64_t)leaf_cls.size());
+    // per-slot rank thresholds and prefix-vote tables (ddm_cforest_slot)
+    std::vector<std::vector<int>> by_slot(cols.size());
+    for (int k = 0; k < S; ++k) by_slot[stumps[k].slot].push_back(k);
+    // records padded with empty slots (n4 = 0) to a multiple of 8: the kernel walks slots
+    // eight at a time
+    std::vector<ddm_cforest_slot> srec((cols.size() + 7) & ~(size_t)7);
+    for (ddm_cforest_slot& rs : srec) {
+        memset(&rs, 0, sizeof(rs));
+        rs.col = cols.empty() ? 0 : cols.back();
+    }
+    std::vector<float> xthr;
+    std::vector<uint32_t> rtab;
+    for (size_t sl = 0; sl < cols.size(); ++sl) {
+        std::vector<int>& ks = by_slot[sl];
+        std::stable_sort(ks.begin(), ks.end(), [&](int a, int b) { return stumps[a].thr < stumps[b].thr; });
+        const int m = (int)ks.size();
+        ddm_cforest_slot& rs = srec[sl];
+        rs.col = cols[sl];
+        rs.n4 = m ? m / 4 + 1 : 0;
+        rs.tab = (int32_t)(rtab.size() / vr);
+        rs.xthr = (int32_t)(xthr.size() / 4);
+        for (int q = 0; q < 4; ++q) rs.thr[q] = q < m ? stumps[ks[q]].thr : INFINITY;
+        for (int q = 4; q < 4 * rs.n4; ++q) xthr.push_back(q < m ? stumps[ks[q]].thr : INFINITY);
+        if (!m) continue;
+        uint32_t acc[4] = {0, 0, 0, 0}, nan_acc[4] = {0, 0, 0, 0};
+        for (int q = 0; q < 4 * rs.n4; ++q) {       // entry q = deltas of the min(q, m) lowest
+            for (int j = 0; j < vr; ++j) rtab.push_back(acc[j]);
+            if (q >= m) continue;
+            const Stump& st = stumps[ks[q]];
+            uint32_t vl[4] = {0, 0, 0, 0}, vrr[4] = {0, 0, 0, 0};
+            inc(st.cl, vl);
+            inc(st.cr, vrr);
+            for (int j = 0; j < vr; ++j) {
+                acc[j] += vrr[j] - vl[j];
+                if (!st.nanleft) nan_acc[j] += vrr[j] - vl[j];
+            }
+        }
+        for (int j = 0; j < vr; ++j) rtab.push_back(nan_acc[j]);   // entry 4*n4: x is NaN
+    }
+    const int64_t slots_off = align16(leafcls_off + (int64_t)leaf_cls.size());
+    const int64_t xthr_off = align16(slots_off + (int64_t)sizeof(ddm_cforest_slot) * srec.size());
+    const int64_t rank_tab_off = align16(xthr_off + 4 * (int64_t)xthr.size());
+    const int64_t total = align16(rank_tab_off + 4 * (int64_t)rtab.size());
     *out_bytes = total;
     if (!out || cap == 0) return 0;
     if (cap < total) {
@@ -193,7 +235,8 @@ extern "C" int ddm_forest_compile(const ddm_node* nodes, int32_t n_nodes, const 
     h.nodes_off = (int)nodes_off;
     h.leafcls_off = (int)leafcls_off;
     for (int k = 0; k < 4; ++k) h.base_votes[k] = base[k];
-    for (size_t s = 0; s < cols.size(); ++s) h.cols[s] = cols[s];
+    for (int s = 0; s < kMaxSlots; ++s)               // past n_slots: the last column (the
+        h.cols[s] = cols.empty() ? 0 : cols[std::min<int>(s, (int)cols.size() - 1)];   // kernel loads 8 at a time)
     int n_right = 0;
     while (n_right < S && stumps[n_right].nanleft == 0) ++n_right;
     h.n_stumps_right = n_right;
@@ -211,5 +254,13 @@ extern "C" int ddm_forest_compile(const ddm_node* nodes, int32_t n_nodes, const 
     if (!trees.empty()) memcpy(out + trees_off, trees.data(), sizeof(ddm_cforest_tree) * trees.size());
     if (!gnodes.empty()) memcpy(out + nodes_off, gnodes.data(), sizeof(ddm_cforest_node) * gnodes.size());
     if (!leaf_cls.empty()) memcpy(out + leafcls_off, leaf_cls.data(), leaf_cls.size());
+    ddm_cforest_head* hp = reinterpret_cast<ddm_cforest_head*>(out);
+    hp->slots_off = (int)slots_off;
+    hp->xthr_off = (int)xthr_off;
+    hp->rank_tab_off = (int)rank_tab_off;
+    hp->rank_tab_entries = (int)(rtab.size() / vr);
+    if (!srec.empty()) memcpy(out + slots_off, srec.data(), sizeof(ddm_cforest_slot) * srec.size());
+    if (!xthr.empty()) memcpy(out + xthr_off, xthr.data(), 4 * xthr.size());
+    if (!rtab.empty()) memcpy(out + rank_tab_off, rtab.data(), 4 * rtab.size());
     return 0;
 }

@@ -74,8 +74,9 @@ struct Seg {
     int64_t block0, nblocks;     // this segment's blocks in the launch grid
     const uint8_t* cforest;      // compiled forest or NULL
     int32_t cf_slots, cf_vote_regs, cf_leaves, flags;
+    int32_t cf_tab_words, pad;
 };
-static_assert(sizeof(Seg) == sizeof(ddm_predict_segment) && sizeof(Seg) == 168, "Seg must mirror ddm_predict_segment");
+static_assert(sizeof(Seg) == sizeof(ddm_predict_segment) && sizeof(Seg) == 176, "Seg must mirror ddm_predict_segment");
 
 template <bool kPure, int kK, bool kLdsForest>
 __device__ __forceinline__ void predict_segment(const Seg& sg, int64_t blk, int64_t nblk, int64_t per_batch,
@@ -208,131 +209,177 @@ __device__ __forceinline__ T ldu(const T* p) {
     }
 }
 
-// Stump record {float32 threshold, slot, delta[kVR]} padded to 16 / 32 bytes
-// (ddm_forest_compile: stump_words).
-template <int kVR>
-struct StumpRec {
-    float thr;
-    int32_t slot;
-    uint32_t delta[kVR];
-    uint32_t pad[(kVR <= 2 ? 4 : 8) - 2 - kVR];
-};
-template <>
-struct StumpRec<2> {
-    float thr;
-    int32_t slot;
-    uint32_t delta[2];
-};
-template <int kVR>
-struct StumpChunk {
-    StumpRec<kVR> r[8];
-};
-
-template <bool kNanLeft, int kVR>
-__device__ __forceinline__ void stump_one(const StumpRec<kVR>& rec, const float* xl, uint32_t (&votes)[kVR]) {
-    const float v = xl[rec.slot * kCfThreads];
-    const bool right = kNanLeft ? (v > rec.thr) : !(v <= rec.thr);
-#pragma unroll
-    for (int j = 0; j < kVR; ++j) votes[j] += right ? rec.delta[j] : 0u;
+// Stumps are evaluated per feature slot through the blob's rank tables
+// (ddm_cforest_slot): r = #{k : !(x <= t_k)} over the slot's padded ascending thresholds
+// (2 VALU per threshold against uniform operands; NaN counts every entry), then one LDS
+// read of the table entry and vote_regs adds, instead of a compare and masked adds per
+// stump.
+__device__ __forceinline__ int rank4(const float x, const float* t) {
+    return (!(x <= t[0]) ? 1 : 0) + (!(x <= t[1]) ? 1 : 0) + (!(x <= t[2]) ? 1 : 0) + (!(x <= t[3]) ? 1 : 0);
 }
 
-// vote += right ? delta : 0 over stumps [k0, k1); right = !(x <= thr) (kNanLeft false:
-// NaN goes right) or x > thr.  x comes from the thread's LDS column (xl[slot * 512]).
-// Records are uniform scalar loads, eight per trip.
-template <bool kNanLeft, int kVR>
-__device__ __forceinline__ void stump_range(const StumpRec<kVR>* recs, int k0, int k1, const float* xl,
-                                            uint32_t (&votes)[kVR]) {
-    const StumpRec<kVR>* p = recs + k0;
-    const StumpRec<kVR>* e = recs + k1;
-    for (; p + 8 <= e; p += 8) {                // 8 records per trip: wide scalar loads
-        const StumpChunk<kVR> c = ldu(reinterpret_cast<const StumpChunk<kVR>*>(p));
-#pragma unroll
-        for (int i = 0; i < 8; ++i) stump_one<kNanLeft, kVR>(c.r[i], xl, votes);
+template <int kVR>
+__device__ __forceinline__ void add_votes(const uint32_t* e, uint32_t (&votes)[kVR]) {
+    if constexpr (kVR == 4) {
+        const uint4 d = *reinterpret_cast<const uint4*>(e);
+        votes[0] += d.x;
+        votes[1] += d.y;
+        votes[2] += d.z;
+        votes[3] += d.w;
+    } else if constexpr (kVR == 2) {
+        const uint2 d = *reinterpret_cast<const uint2*>(e);
+        votes[0] += d.x;
+        votes[1] += d.y;
+    } else {
+        votes[0] += e[0];
     }
-    for (; p < e; ++p) stump_one<kNanLeft, kVR>(ldu(p), xl, votes);
 }
 
-template <int kU, int kVR>
+// A thread evaluates kRows rows (2 for stump forests: one in each half of a double
+// tile; 1 with general trees, whose LDS row columns grow with kRows), so every
+// scalar instruction of the slot walk (records, thresholds, loop control: the scalar
+// unit is shared by the CU's four SIMDs) serves 128 rows of a wave.  Feature values are
+// loaded 8 slots at a time, one chunk ahead of the chunk being evaluated (and the next
+// double tile's first chunk during the current one's last), so a row's loads stay in
+// flight behind the compares.  Column pointers X + col*ld come from LDS (no 64-bit
+// scalar multiplies per load).
+constexpr int kChunk = 8;
+
+template <int kVR, int kRows>
 __device__ __forceinline__ void cf_segment(const Seg& sg, int64_t blk, int64_t nblk, int pb, unsigned char* smem) {
     const uint8_t* blob = sg.cforest;
     const ddm_cforest_head* H = reinterpret_cast<const ddm_cforest_head*>(blob);
     const int U = ldu(&H->n_slots), K = ldu(&H->n_classes), n_general = ldu(&H->n_general);
-    const int n_leaves = ldu(&H->n_leaves), S = ldu(&H->n_stumps), n_right = ldu(&H->n_stumps_right);
-    const StumpRec<kVR>* recs = reinterpret_cast<const StumpRec<kVR>*>(blob + ldu(&H->stumps_off));
+    const int n_leaves = ldu(&H->n_leaves);
+    const int tab_words = ldu(&H->rank_tab_entries) * kVR;
+    const ddm_cforest_slot* slots = reinterpret_cast<const ddm_cforest_slot*>(blob + ldu(&H->slots_off));
+    const float4* xthr = reinterpret_cast<const float4*>(blob + ldu(&H->xthr_off));
     const ddm_cforest_tree* trees = reinterpret_cast<const ddm_cforest_tree*>(blob + ldu(&H->trees_off));
     const ddm_cforest_node* gnodes = reinterpret_cast<const ddm_cforest_node*>(blob + ldu(&H->nodes_off));
     const uint8_t* leafcls = blob + ldu(&H->leafcls_off);
+    const int U8 = (U + kChunk - 1) & ~(kChunk - 1);
 
     const int tid = threadIdx.x;
-    // LDS: row slots [U][512] | err [512] | label [512] | classes [16] | leaf classes
-    float* s_x = reinterpret_cast<float*>(smem);
-    uint8_t* s_e = reinterpret_cast<uint8_t*>(s_x + (size_t)U * kCfThreads);
-    int32_t* s_pred = reinterpret_cast<int32_t*>(s_e + kCfThreads);
-    int32_t* s_cls = s_pred + kCfThreads;
-    uint8_t* s_leaf = reinterpret_cast<uint8_t*>(s_cls + 16);
+    // LDS (cf_lds_bytes): column pointers [32] | rank tables | labels [2][512] |
+    // classes [16] | err [2][512] | leaf classes | row slots [kRows][U8][512] (only with
+    // general trees, which index x by a node's slot at run time)
+    const float** s_colp = reinterpret_cast<const float**>(smem);
+    uint32_t* s_tab = reinterpret_cast<uint32_t*>(s_colp + 32);
+    int32_t* s_pred = reinterpret_cast<int32_t*>(s_tab + ((tab_words + 3) & ~3));
+    int32_t* s_cls = s_pred + kRows * kCfThreads;
+    uint8_t* s_e = reinterpret_cast<uint8_t*>(s_cls + 16);
+    uint8_t* s_leaf = s_e + kRows * kCfThreads;
+    float* s_x = reinterpret_cast<float*>(s_leaf + ((n_leaves + 15) & ~15));
+    {
+        const uint32_t* gt = reinterpret_cast<const uint32_t*>(blob + ldu(&H->rank_tab_off));
+        for (int k = tid; k < tab_words; k += kCfThreads) s_tab[k] = gt[k];
+    }
     for (int k = tid; k < n_leaves; k += kCfThreads) s_leaf[k] = leafcls[k];
     if (tid < 16) s_cls[tid] = H->classes[tid];
+    if (tid < 32) s_colp[tid] = sg.X + (int64_t)H->cols[tid] * sg.ld;
     uint32_t base_votes[kVR];
 #pragma unroll
     for (int j = 0; j < kVR; ++j) base_votes[j] = ldu(&H->base_votes[j]);
 
     const int tile = (kCfThreads / pb) * pb;
     const int tb = (tid / pb) * pb;
-    const float* __restrict__ X = sg.X;
-    const int64_t ld = sg.ld;
-    int64_t colbase[kU];
-#pragma unroll
-    for (int s = 0; s < kU; ++s) colbase[s] = U > 0 ? (int64_t)ldu(&H->cols[s < U ? s : U - 1]) * ld : 0;
-    const float* xl = s_x + tid;
-    float* xw = s_x + tid;
     const int lane = tid & 63;
     bool wave_done = false;
-    // Register double buffering: the next tile's slots and label are loaded while the
-    // current tile is evaluated out of LDS.
-    const int64_t step = nblk * tile;
+    const int64_t step = nblk * kRows * tile;
+    // every lane runs the row phase, on a clamped row, so the forest loops stay
+    // wave-uniform and their records stay in SGPRs
     auto row_of = [&](int64_t gt0) -> int64_t {
         const int64_t gg = gt0 + tid;
         return ((tid < tile && gg < sg.pos_end) ? gg : min(gt0, sg.pos_end - 1)) - sg.row_base;
     };
-    float vnext[kU];
-    int32_t ynext = 0;
-    int64_t g0 = sg.pos_begin + blk * tile;
-    if (g0 < sg.pos_end) {
-        const int64_t row = row_of(g0);
-        if (U > 0) {
+    auto load_chunk = [&](int c, const int64_t (&row)[kRows], float (&xc)[kRows][kChunk]) {
+        const float* p[kChunk];
 #pragma unroll
-            for (int s = 0; s < kU; ++s) vnext[s] = X[colbase[s] + row];
-        }
-        ynext = sg.y[row];
+        for (int k = 0; k < kChunk; ++k) p[k] = s_colp[c + k];
+#pragma unroll
+        for (int i = 0; i < kRows; ++i)
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) xc[i][k] = p[k][row[i]];
+    };
+    float xa[kRows][kChunk], xb[kRows][kChunk];
+#pragma unroll
+    for (int i = 0; i < kRows; ++i)
+#pragma unroll
+        for (int k = 0; k < kChunk; ++k) xa[i][k] = xb[i][k] = 0.f;
+    int32_t ynext[kRows];
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) ynext[i] = 0;
+    int64_t g0 = sg.pos_begin + blk * kRows * tile;
+    __syncthreads();                            // column pointers, tables
+    if (g0 < sg.pos_end) {
+        int64_t row[kRows];
+#pragma unroll
+        for (int i = 0; i < kRows; ++i) row[i] = row_of(g0 + i * tile);
+        if (U > 0) load_chunk(0, row, xa);
+#pragma unroll
+        for (int i = 0; i < kRows; ++i) ynext[i] = sg.y[row[i]];
     }
     for (; g0 < sg.pos_end; g0 += step) {
-        __syncthreads();                        // LDS tables ready / previous tile consumed
-        const int64_t g = g0 + tid;
-        const bool valid = tid < tile && g < sg.pos_end;
-        // ---- row phase (every lane runs it, on a clamped row, so that the forest loops
-        // stay wave-uniform and their records stay in SGPRs).  Each thread only reads the
-        // LDS column it wrote itself, so no barrier is needed before the forest.
-        {
-            if (U > 0) {
+        int64_t row[kRows], nrow[kRows];
+        const bool has_next = g0 + step < sg.pos_end;
 #pragma unroll
-                for (int s = 0; s < kU; ++s)
-                    if (s < U) xw[s * kCfThreads] = vnext[s];
-            }
-            const int32_t yv = ynext;
-            if (g0 + step < sg.pos_end) {       // prefetch (slots past U re-read the last column)
-                const int64_t row = row_of(g0 + step);
-                if (U > 0) {
+        for (int i = 0; i < kRows; ++i) {
+            row[i] = row_of(g0 + i * tile);
+            nrow[i] = has_next ? row_of(g0 + step + i * tile) : row[i];
+        }
+        int32_t yv[kRows];
 #pragma unroll
-                    for (int s = 0; s < kU; ++s) vnext[s] = X[colbase[s] + row];
+        for (int i = 0; i < kRows; ++i) {
+            yv[i] = ynext[i];
+            if (has_next) ynext[i] = sg.y[nrow[i]];
+        }
+        uint32_t votes[kRows][kVR];
+#pragma unroll
+        for (int i = 0; i < kRows; ++i)
+#pragma unroll
+            for (int j = 0; j < kVR; ++j) votes[i][j] = base_votes[j];
+        // ---- row phase.  Each thread only reads the LDS columns it wrote itself, so no
+        // barrier is needed before the general trees.
+        for (int c = 0; c < U; c += kChunk) {
+            if (c + kChunk < U) load_chunk(c + kChunk, row, xb);
+            else if (has_next) load_chunk(0, nrow, xb);
+            const ddm_cforest_slot* sc = slots + c;
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) {
+                if (n_leaves > 0) {
+#pragma unroll
+                    for (int i = 0; i < kRows; ++i) s_x[((i * U8) + c + k) * kCfThreads + tid] = xa[i][k];
                 }
-                ynext = sg.y[row];
-            }
-            uint32_t votes[kVR];
+                const int n4 = ldu(&sc[k].n4);
+                if (n4 > 0) {
+                    const float4 t0 = ldu(reinterpret_cast<const float4*>(sc[k].thr));
+                    const float tt0[4] = {t0.x, t0.y, t0.z, t0.w};
+                    int r[kRows];
 #pragma unroll
-            for (int j = 0; j < kVR; ++j) votes[j] = base_votes[j];
-            stump_range<false, kVR>(recs, 0, n_right, xl, votes);
-            if (n_right < S) stump_range<true, kVR>(recs, n_right, S, xl, votes);
+                    for (int i = 0; i < kRows; ++i) r[i] = rank4(xa[i][k], tt0);
+                    if (n4 > 1) {
+                        const float4* xt = xthr + ldu(&sc[k].xthr);
+                        for (int q = 0; q < n4 - 1; ++q) {
+                            const float4 t = ldu(xt + q);
+                            const float tt[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+                            for (int i = 0; i < kRows; ++i) r[i] += rank4(xa[i][k], tt);
+                        }
+                    }
+                    const uint32_t* tab = s_tab + ldu(&sc[k].tab) * kVR;
+#pragma unroll
+                    for (int i = 0; i < kRows; ++i) add_votes<kVR>(tab + r[i] * kVR, votes[i]);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < kRows; ++i)
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) xa[i][k] = xb[i][k];
+        }
+#pragma unroll
+        for (int i = 0; i < kRows; ++i) {
             // deeper trees: QuickScorer exit-leaf masks
+            const float* xl = s_x + (size_t)i * U8 * kCfThreads + tid;
             for (int t = 0; t < n_general; ++t) {
                 const ddm_cforest_tree T = ldu(trees + t);
                 uint32_t mlo = 0xffffffffu, mhi = 0xffffffffu;
@@ -347,44 +394,48 @@ __device__ __forceinline__ void cf_segment(const Seg& sg, int64_t blk, int64_t n
                 const int c = s_leaf[T.leaf_begin + leaf];
                 const uint32_t inc = 1u << (8 * (c & 3));
 #pragma unroll
-                for (int j = 0; j < kVR; ++j) votes[j] += (c >> 2) == j ? inc : 0u;
+                for (int j = 0; j < kVR; ++j) votes[i][j] += (c >> 2) == j ? inc : 0u;
             }
             // first argmax over the vote counters
             int best = 0, bestv = -1;
 #pragma unroll
             for (int c = 0; c < 4 * kVR; ++c) {
-                const int v = (int)((votes[c >> 2] >> (8 * (c & 3))) & 0xffu);
-                if (c < K && v > bestv) {
-                    bestv = v;
-                    best = c;
-                }
+                const int v = (int)((votes[i][c >> 2] >> (8 * (c & 3))) & 0xffu);
+                const bool better = c < K && v > bestv;
+                bestv = better ? v : bestv;
+                best = better ? c : best;
             }
             const int32_t label = s_cls[best];
-            if (valid) {
-                s_e[tid] = (uint8_t)(label != yv);
-                if (sg.pred) s_pred[tid] = label;
+            if (tid < tile) {
+                s_e[i * kCfThreads + tid] = (uint8_t)(label != yv[i]);
+                if (sg.pred) s_pred[i * kCfThreads + tid] = label;
             }
         }
         __syncthreads();
         // ---- position phase
-        int e = 0;
-        if (valid) {
-            const int k = tb + (int)sg.perm[g];
-            e = s_e[k];
-            sg.err[g] = (uint8_t)e;
-            if (sg.pred) sg.pred[g] = s_pred[k];
+#pragma unroll
+        for (int i = 0; i < kRows; ++i) {
+            const int64_t g = g0 + i * tile + tid;
+            int e = 0;
+            if (tid < tile && g < sg.pos_end) {
+                const int k = i * kCfThreads + tb + (int)sg.perm[g];
+                e = s_e[k];
+                sg.err[g] = (uint8_t)e;
+                if (sg.pred) sg.pred[g] = s_pred[k];
+            }
+            if (sg.first_err) note_first_error(sg.first_err, e, g, lane, wave_done);
         }
-        if (sg.first_err) note_first_error(sg.first_err, e, g, lane, wave_done);
+        __syncthreads();                        // s_e / s_pred / s_x consumed
     }
 }
 
-template <int kU, int kVR>
+template <int kVR, int kRows>
 __global__ __launch_bounds__(kCfThreads) void k_cforest_predict(Seg sg, int pb) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    cf_segment<kU, kVR>(sg, blockIdx.x, gridDim.x, pb, smem);
+    cf_segment<kVR, kRows>(sg, blockIdx.x, gridDim.x, pb, smem);
 }
 
-template <int kU, int kVR>
+template <int kVR, int kRows>
 __global__ __launch_bounds__(kCfThreads) void k_cforest_predict_batch(const Seg* __restrict__ segs, int n_segs,
                                                                       int64_t block_base, int pb) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -393,40 +444,42 @@ __global__ __launch_bounds__(kCfThreads) void k_cforest_predict_batch(const Seg*
     while (s < n_segs && !(ldu(&segs[s].block0) <= gb && gb < ldu(&segs[s].block0) + ldu(&segs[s].nblocks))) ++s;
     if (s == n_segs) return;
     const Seg sg = ldu(segs + s);
-    cf_segment<kU, kVR>(sg, gb - sg.block0, sg.nblocks, pb, smem);
+    cf_segment<kVR, kRows>(sg, gb - sg.block0, sg.nblocks, pb, smem);
 }
 
 using cf_fn = void (*)(Seg, int);
 using cf_batch_fn = void (*)(const Seg*, int, int64_t, int);
 
-int cf_ukind(int slots) { return slots <= 8 ? 0 : slots <= 16 ? 1 : 2; }
 int cf_vkind(int vr) { return vr <= 1 ? 0 : vr <= 2 ? 1 : 2; }
+int cf_rows(int leaves) { return leaves > 0 ? 1 : 2; }
+template <int kRows>
+cf_fn pick_cf_r(int vk) {
+    return vk == 0 ? k_cforest_predict<1, kRows> : vk == 1 ? k_cforest_predict<2, kRows> : k_cforest_predict<4, kRows>;
+}
+cf_fn pick_cf(int vk, int rows) { return rows == 1 ? pick_cf_r<1>(vk) : pick_cf_r<2>(vk); }
+template <int kRows>
+cf_batch_fn pick_cf_batch_r(int vk) {
+    return vk == 0 ? k_cforest_predict_batch<1, kRows>
+                   : vk == 1 ? k_cforest_predict_batch<2, kRows> : k_cforest_predict_batch<4, kRows>;
+}
+cf_batch_fn pick_cf_batch(int vk, int rows) { return rows == 1 ? pick_cf_batch_r<1>(vk) : pick_cf_batch_r<2>(vk); }
 
-template <int kU>
-cf_fn pick_cf_u(int vk) {
-    return vk == 0 ? k_cforest_predict<kU, 1> : vk == 1 ? k_cforest_predict<kU, 2> : k_cforest_predict<kU, 4>;
-}
-cf_fn pick_cf(int uk, int vk) {
-    return uk == 0 ? pick_cf_u<8>(vk) : uk == 1 ? pick_cf_u<16>(vk) : pick_cf_u<32>(vk);
-}
-template <int kU>
-cf_batch_fn pick_cf_batch_u(int vk) {
-    return vk == 0 ? k_cforest_predict_batch<kU, 1>
-                   : vk == 1 ? k_cforest_predict_batch<kU, 2> : k_cforest_predict_batch<kU, 4>;
-}
-cf_batch_fn pick_cf_batch(int uk, int vk) {
-    return uk == 0 ? pick_cf_batch_u<8>(vk) : uk == 1 ? pick_cf_batch_u<16>(vk) : pick_cf_batch_u<32>(vk);
+// LDS of the compiled path (cf_segment): column pointers + rank tables + labels +
+// classes + err + leaf classes + row slots [kRows][slots rounded to 8][512] when the
+// forest has general trees (leaves > 0).
+size_t cf_lds_bytes(int leaves, int slots, int tab_words) {
+    const int kRows = cf_rows(leaves);
+    const size_t slots8 = (size_t)((slots + kChunk - 1) & ~(kChunk - 1));
+    return 8 * 32 + (size_t)4 * ((tab_words + 3) & ~3) + (size_t)4 * kRows * kCfThreads + 64 +
+           (size_t)kRows * kCfThreads + (size_t)((leaves + 15) & ~15) +
+           (leaves > 0 ? (size_t)4 * kRows * kCfThreads * slots8 : 0);
 }
 
-// LDS of the compiled path: row slots [slots][512] + err + labels + classes + leaf classes.
-size_t cf_lds_bytes(int leaves, int slots) {
-    return (size_t)4 * kCfThreads * slots + kCfThreads + 4 * kCfThreads + 64 + (size_t)((leaves + 15) & ~15);
-}
-
-size_t cf_lds_bound(const Seg& g) { return cf_lds_bytes(g.cf_leaves, g.cf_slots); }
+size_t cf_lds_bound(const Seg& g) { return cf_lds_bytes(g.cf_leaves, g.cf_slots, g.cf_tab_words); }
 
 bool cf_usable(const Seg& g, int pb) {
     return g.cforest && g.cf_slots >= 0 && g.cf_slots <= 32 && g.cf_vote_regs >= 1 && g.cf_vote_regs <= 4 &&
+           g.cf_tab_words >= 0 &&
            g.pos_begin % pb == 0 && cf_lds_bound(g) <= 80 * 1024;
 }
 
@@ -494,13 +547,14 @@ extern "C" int ddm_forest_predict(const float* X, int64_t ld, int32_t n_features
     Seg sg{X, ld, y, perm, err_out, pred_out, reinterpret_cast<unsigned long long*>(first_err), pos_begin, pos_end,
            forest->nodes, forest->roots, forest->leaf_value, forest->classes, forest->n_trees, forest->n_classes,
            forest->n_nodes, forest->pure, 0, 0, 0, forest->cforest, forest->cf_slots, forest->cf_vote_regs,
-           forest->cf_leaves, 0};
+           forest->cf_leaves, 0, forest->cf_tab_words, 0};
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
     if (cf_usable(sg, per_batch)) {
-        const int tile = (kCfThreads / per_batch) * per_batch;
+        const int rows = cf_rows(sg.cf_leaves);
+        const int tile = rows * ((kCfThreads / per_batch) * per_batch);
         sg.nblocks = std::min<int64_t>(ddm::ceil_div(n, tile), kMaxBlocks);
-        hipLaunchKernelGGL(pick_cf(cf_ukind(sg.cf_slots), cf_vkind(sg.cf_vote_regs)), dim3((unsigned)sg.nblocks),
+        hipLaunchKernelGGL(pick_cf(cf_vkind(sg.cf_vote_regs), rows), dim3((unsigned)sg.nblocks),
                            dim3(kCfThreads), cf_lds_bound(sg), s, sg, (int)per_batch);
     } else {
         const size_t lds = forest_lds_bytes(forest->n_nodes, forest->n_trees);
@@ -529,7 +583,7 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
     hipStream_t s = ddm::as_hip(stream);
     // One launch per kernel variant; every launch walks the whole device table and only
     // the blocks assigned to its segments work.  Variants: 16 node-walk kinds (pure x
-    // classes x LDS-resident forest) and 9 compiled kinds (slots x vote registers).
+    // classes x LDS-resident forest) and 6 compiled kinds (vote registers x rows/lane).
     Seg* hs = reinterpret_cast<Seg*>(const_cast<ddm_predict_segment*>(segs_host));
     for (int i = 0; i < n_segs; ++i) {
         const Seg& g = hs[i];
@@ -545,25 +599,25 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
     }
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
-    constexpr int kNV = 16 + 9;
+    constexpr int kNV = 16 + 6;
     std::vector<int> variant(n_segs);
     for (int i = 0; i < n_segs; ++i) {
         const Seg& g = hs[i];
         if (cf_usable(g, per_batch)) {
-            variant[i] = 16 + 3 * cf_ukind(g.cf_slots) + cf_vkind(g.cf_vote_regs);
+            variant[i] = 16 + 3 * (cf_rows(g.cf_leaves) - 1) + cf_vkind(g.cf_vote_regs);
         } else {
             const bool lds = forest_lds_bytes(g.n_nodes, g.n_trees) <= (size_t)kMaxLdsForest;
             const int kc = g.n_classes <= 4 ? 0 : g.n_classes <= 8 ? 1 : g.n_classes <= 16 ? 2 : 3;
             variant[i] = (g.pure ? 1 : 0) * 8 + (lds ? 4 : 0) + kc;
         }
     }
-    const int tile = (kCfThreads / per_batch) * per_batch;
+    const int tile = (kCfThreads / per_batch) * per_batch;   // positions per block step (x rows)
     int64_t vbase[kNV + 1] = {0};
     size_t vlds[kNV] = {0};
     int64_t b0 = 0;
     for (int v = 0; v < kNV; ++v) {
         vbase[v] = b0;
-        const int unit = v >= 16 ? tile : kThreads;
+        const int unit = v >= 16 ? (1 + (v - 16) / 3) * tile : kThreads;
         int64_t rows = 0;
         for (int i = 0; i < n_segs; ++i)
             if (variant[i] == v) {
@@ -590,8 +644,7 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
         const int64_t nb = vbase[v + 1] - vbase[v];
         if (nb == 0) continue;
         if (v >= 16) {
-            const int uk = (v - 16) / 3, vk = (v - 16) % 3;
-            hipLaunchKernelGGL(pick_cf_batch(uk, vk), dim3((unsigned)nb), dim3(kCfThreads), vlds[v], s,
+            hipLaunchKernelGGL(pick_cf_batch((v - 16) % 3, 1 + (v - 16) / 3), dim3((unsigned)nb), dim3(kCfThreads), vlds[v], s,
                                reinterpret_cast<const Seg*>(segs_dev), n_segs, vbase[v], (int)per_batch);
         } else {
             const bool lds = (v & 4) != 0;

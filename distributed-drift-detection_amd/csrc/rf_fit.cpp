@@ -647,6 +647,7 @@ extern "C" int ddm_rf_fit_many(ddm_fit_job* jobs, int32_t n_jobs, int32_t n_thre
             jb.cf_slots = h->n_slots;
             jb.cf_vote_regs = h->vote_regs;
             jb.cf_leaves = h->n_leaves;
+            jb.cf_tab_words = h->rank_tab_entries * h->vote_regs;
         }
     });
     for (int j = 0; j < n_jobs; ++j)

@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
@@ -36,7 +36,7 @@ class DdmForest(ctypes.Structure):
                 ("classes", ctypes.c_void_p), ("n_trees", ctypes.c_int32), ("n_classes", ctypes.c_int32),
                 ("n_nodes", ctypes.c_int32), ("pure", ctypes.c_int32), ("cforest", ctypes.c_void_p),
                 ("cf_slots", ctypes.c_int32), ("cf_vote_regs", ctypes.c_int32), ("cf_leaves", ctypes.c_int32),
-                ("cf_pad", ctypes.c_int32)]
+                ("cf_tab_words", ctypes.c_int32)]
 
 
 assert ctypes.sizeof(DdmState) == 56 and ctypes.sizeof(DdmParams) == 24 and ctypes.sizeof(DdmForest) == 72

@@ -409,7 +409,7 @@ class BatchRunner:
             rows.append((part.X.data_ptr(), part.X.shape[1], part.y.data_ptr(), perm, err, 0,
                          self._dptr(self.o_first, ps.i, 8), p0, p1, d.nodes, d.roots, d.leaf_value or 0, d.classes,
                          d.n_trees, d.n_classes, d.n_nodes, d.pure, ps.base, 0, 0, d.cforest or 0, d.cf_slots,
-                         d.cf_vote_regs, d.cf_leaves, kernels.SEG_FIRST_ERR_PRESET))
+                         d.cf_vote_regs, d.cf_leaves, kernels.SEG_FIRST_ERR_PRESET, d.cf_tab_words, 0))
         self.segs.rec[:len(rows)] = np.array(rows, dtype=kernels.SEG_DTYPE)
 
     def _stage_table(self, live):

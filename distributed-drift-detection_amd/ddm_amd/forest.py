@@ -15,6 +15,7 @@ from .treepack import MAX_CLASSES, MISSING_LEFT_BIT, NODE_DTYPE, PackedForest, p
 # ddm_cforest_head (include/ddm_amd.h): the leading int32 fields
 _HEAD_FIELDS = ("n_slots", "n_classes", "vote_regs", "n_stumps", "n_general", "n_leaves", "total_bytes",
                 "any_nanleft")
+_RANK_TAB_ENTRIES = 71          # int32 index of ddm_cforest_head.rank_tab_entries
 
 
 def compile_forest(packed):
@@ -34,6 +35,7 @@ def compile_forest(packed):
     blob = np.zeros(size.value, dtype=np.uint8)
     check(lib.ddm_forest_compile(*args, blob.ctypes.data, blob.size, ctypes.byref(size)), "ddm_forest_compile")
     head = dict(zip(_HEAD_FIELDS, blob[:4 * len(_HEAD_FIELDS)].view(np.int32).tolist()))
+    head["tab_words"] = int(blob[:4 * (_RANK_TAB_ENTRIES + 1)].view(np.int32)[_RANK_TAB_ENTRIES]) * head["vote_regs"]
     return blob, head
 
 
@@ -55,7 +57,7 @@ class DeviceForest:
                               packed.n_trees, packed.n_classes, packed.n_nodes, 1 if packed.pure else 0,
                               0 if blob is None else self.cforest.data_ptr(),
                               head["n_slots"] if head else 0, head["vote_regs"] if head else 0,
-                              head["n_leaves"] if head else 0, 0)
+                              head["n_leaves"] if head else 0, head["tab_words"] if head else 0)
 
     @classmethod
     def from_buffer(cls, packed, blob, head, dev, off, host_keepalive=None):
@@ -69,7 +71,7 @@ class DeviceForest:
                            base + off["classes"], packed.n_trees, packed.n_classes, packed.n_nodes,
                            1 if packed.pure else 0, 0 if blob is None else base + off["blob"],
                            head["n_slots"] if head else 0, head["vote_regs"] if head else 0,
-                           head["n_leaves"] if head else 0, 0)
+                           head["n_leaves"] if head else 0, head["tab_words"] if head else 0)
         return f
 
     @property

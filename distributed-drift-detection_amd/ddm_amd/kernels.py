@@ -22,9 +22,10 @@ SEG_DTYPE = np.dtype([("X", "<u8"), ("ld", "<i8"), ("y", "<u8"), ("perm", "<u8")
                       ("roots", "<u8"), ("leaf_value", "<u8"), ("classes", "<u8"), ("n_trees", "<i4"),
                       ("n_classes", "<i4"), ("n_nodes", "<i4"), ("pure", "<i4"), ("row_base", "<i8"),
                       ("block0", "<i8"), ("nblocks", "<i8"), ("cforest", "<u8"), ("cf_slots", "<i4"),
-                      ("cf_vote_regs", "<i4"), ("cf_leaves", "<i4"), ("flags", "<i4")])
+                      ("cf_vote_regs", "<i4"), ("cf_leaves", "<i4"), ("flags", "<i4"),
+                      ("cf_tab_words", "<i4"), ("pad", "<i4")])
 SEG_FIRST_ERR_PRESET = 1
-assert SEG_DTYPE.itemsize == 168
+assert SEG_DTYPE.itemsize == 176
 JOB_DTYPE = np.dtype([("R", "<u8"), ("Tsub", "<u8"), ("Tchunk", "<u8"), ("avail", "<i8"), ("P", "<i8"), ("W", "<i8"),
                       ("pieces", "<u8"), ("info", "<u8"), ("J", "<u8"), ("E", "<u8"), ("perm_out", "<u8"),
                       ("stop", "<u8"), ("pick_offset", "<i8"), ("pick_last", "<i8"), ("pick_out", "<u8")])

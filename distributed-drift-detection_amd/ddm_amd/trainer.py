@@ -73,7 +73,7 @@ class FitJob(ctypes.Structure):
                 ("roots", ctypes.c_void_p), ("leaf_value", ctypes.c_void_p), ("leaf_rows_cap", ctypes.c_int64),
                 ("info", ctypes.c_int64 * 3), ("blob", ctypes.c_void_p), ("blob_cap", ctypes.c_int64),
                 ("blob_bytes", ctypes.c_int64), ("cf_slots", ctypes.c_int32), ("cf_vote_regs", ctypes.c_int32),
-                ("cf_leaves", ctypes.c_int32), ("pad", ctypes.c_int32)]
+                ("cf_leaves", ctypes.c_int32), ("cf_tab_words", ctypes.c_int32)]
 
 
 class BatchForestTrainer:
@@ -136,7 +136,8 @@ class BatchForestTrainer:
             pf = PackedForest(b["nodes"][:n_nodes].copy(), b["roots"].copy(), lv, cls32, bool(pure))
             if j.blob_bytes:
                 blob = b["blob"][:j.blob_bytes].copy()
-                head = {"n_slots": j.cf_slots, "vote_regs": j.cf_vote_regs, "n_leaves": j.cf_leaves}
+                head = {"n_slots": j.cf_slots, "vote_regs": j.cf_vote_regs, "n_leaves": j.cf_leaves,
+                        "tab_words": j.cf_tab_words}
                 out.append((pf, blob, head))
             else:
                 out.append((pf, None, None))

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 5
+#define DDM_AMD_ABI_VERSION 6
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -89,10 +89,10 @@ typedef struct ddm_forest {
     int32_t pure;                /* 1: every leaf is one-hot and n_trees <= 255    */
     const uint8_t*  cforest;     /* device blob of ddm_forest_compile, or NULL: then the
                                     node walk above is used                         */
-    int32_t cf_slots;            /* the blob's n_slots, vote_regs and n_leaves            */
-    int32_t cf_vote_regs;        /* (kernel choice and LDS size without reading the blob) */
-    int32_t cf_leaves;
-    int32_t cf_pad;
+    int32_t cf_slots;            /* the blob's n_slots, vote_regs, n_leaves and rank-table */
+    int32_t cf_vote_regs;        /* words (kernel choice and LDS size without reading the  */
+    int32_t cf_leaves;           /* blob)                                                   */
+    int32_t cf_tab_words;
 } ddm_forest;
 
 /* ---- compiled forests (the fast predict path) -------------------------------------
@@ -112,7 +112,11 @@ typedef struct ddm_forest {
  * Layout (byte offsets from the blob start, 16-byte aligned sections):
  *   ddm_cforest_head | stumps u32[S][stump_words] ({float32 thr bits, slot, delta[vote_regs]},
  *                                                  stump_words = 4 (vote_regs <= 2) or 8)
- *   | trees ddm_cforest_tree[n_general] | nodes ddm_cforest_node[] | leaf class u8[n_leaves] */
+ *   | trees ddm_cforest_tree[n_general] | nodes ddm_cforest_node[] | leaf class u8[n_leaves]
+ *   | slot records ddm_cforest_slot[n_slots] | extra thresholds float4[]
+ *   | rank tables u32[entries][vote_regs]
+ * The stump records are the forest's plain form (tests, tools); the kernel evaluates the
+ * stumps through the per-slot rank tables (ddm_cforest_slot). */
 typedef struct ddm_cforest_head {
     int32_t n_slots, n_classes, vote_regs, n_stumps;
     int32_t n_general, n_leaves, total_bytes, any_nanleft;
@@ -122,7 +126,23 @@ typedef struct ddm_cforest_head {
     uint32_t base_votes[4];
     int32_t cols[32];            /* feature column of each slot                          */
     int32_t classes[16];         /* classes_ labels                                      */
+    int32_t slots_off, xthr_off, rank_tab_off, rank_tab_entries;  /* byte offsets, entries */
 } ddm_cforest_head;
+
+/* Per-slot stump ranks.  The m stumps on slot s have ascending thresholds t_0..t_{m-1},
+ * stored as n4 = m/4 + 1 float4 groups padded with +inf (so at least one pad).  With
+ * r = #{k : !(x <= t_k)} over the 4*n4 entries, r = #{t_k < x} <= m for every non-NaN x
+ * (no pad counts) and r = 4*n4 for NaN (every compare counts).  The slot's votes are then
+ * table[tab + r]: P[r] = the deltas of the r lowest stumps for r <= m, and entry 4*n4 the
+ * deltas of the stumps that send NaN right.  Group 0 is inline, groups 1.. are at
+ * extra thresholds[xthr..]. */
+typedef struct ddm_cforest_slot {
+    int32_t col;                 /* feature column                                       */
+    int32_t n4;                  /* threshold groups (0: no stump reads this slot)       */
+    int32_t tab;                 /* first table entry                                    */
+    int32_t xthr;                /* first extra group                                    */
+    float thr[4];                /* group 0                                              */
+} ddm_cforest_slot;
 
 typedef struct ddm_cforest_tree { int32_t node_begin, n_nodes, leaf_begin, n_leaves; } ddm_cforest_tree;
 typedef struct ddm_cforest_node {
@@ -169,8 +189,9 @@ typedef struct ddm_predict_segment {
     int64_t row_base;       /* row = (g / per_batch) * per_batch + perm[g] - row_base (g: position) */
     int64_t block0, nblocks;
     const uint8_t* cforest; /* compiled forest (device) or NULL                              */
-    int32_t cf_slots, cf_vote_regs;   /* its n_slots, vote_regs, n_leaves                   */
+    int32_t cf_slots, cf_vote_regs;   /* its n_slots, vote_regs, n_leaves, rank-table words */
     int32_t cf_leaves, flags;         /* flags: DDM_SEG_FIRST_ERR_PRESET                     */
+    int32_t cf_tab_words, pad;
 } ddm_predict_segment;
 
 /* ddm_predict_segment.flags: the caller already set *first_err to UINT64_MAX (e.g. in
@@ -335,7 +356,7 @@ typedef struct ddm_fit_job {
     ddm_node* nodes; int64_t nodes_cap; int32_t* roots; double* leaf_value; int64_t leaf_rows_cap;
     int64_t info[3];                   /* out: n_nodes, pure, n_leaf_rows */
     uint8_t* blob; int64_t blob_cap; int64_t blob_bytes;
-    int32_t cf_slots, cf_vote_regs, cf_leaves, pad;
+    int32_t cf_slots, cf_vote_regs, cf_leaves, cf_tab_words;
 } ddm_fit_job;
 
 int ddm_rf_fit_many(ddm_fit_job* jobs, int32_t n_jobs, int32_t n_threads);

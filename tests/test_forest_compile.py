@@ -10,13 +10,17 @@ HEAD = np.dtype([("n_slots", "<i4"), ("n_classes", "<i4"), ("vote_regs", "<i4"),
                  ("stumps_off", "<i4"), ("stump_words", "<i4"), ("n_stumps_right", "<i4"), ("trees_off", "<i4"),
                  ("nodes_off", "<i4"), ("leafcls_off", "<i4"), ("pad0", "<i4"), ("pad1", "<i4"),
                  ("base_votes", "<u4", 4), ("cols", "<i4", 32),
-                 ("classes", "<i4", 16)])
+                 ("classes", "<i4", 16), ("slots_off", "<i4"), ("xthr_off", "<i4"), ("rank_tab_off", "<i4"),
+                 ("rank_tab_entries", "<i4")])
+SLOT = np.dtype([("col", "<i4"), ("n4", "<i4"), ("tab", "<i4"), ("xthr", "<i4"), ("thr", "<f4", 4)])
 TREE = np.dtype([("node_begin", "<i4"), ("n_nodes", "<i4"), ("leaf_begin", "<i4"), ("n_leaves", "<i4")])
 NODE = np.dtype([("threshold", "<f4"), ("slot_nanleft", "<i4"), ("left_lo", "<u4"), ("left_hi", "<u4")])
 
 
-def eval_blob(blob, X32):
-    """Row-by-row model of k_cforest_predict's row phase: returns predicted labels."""
+def eval_blob(blob, X32, ranks=False):
+    """Row-by-row model of k_cforest_predict's row phase: returns predicted labels.
+    ranks=True evaluates the stumps through the per-slot rank tables (what the kernel
+    does), False through the stump records."""
     h = blob[:HEAD.itemsize].view(HEAD)[0]
     U, K, vr = int(h["n_slots"]), int(h["n_classes"]), int(h["vote_regs"])
     S = int(h["n_stumps"])
@@ -32,11 +36,25 @@ def eval_blob(blob, X32):
         for r, row in enumerate(X32):
             x = row[h["cols"][:U]]
             votes = h["base_votes"][:vr].astype(np.uint64)
-            for k in range(S):
-                v = x[recs[k, 1]]
-                right = (not (v <= thr[k])) if k < h["n_stumps_right"] else (v > thr[k])
-                if right:
-                    votes = (votes + recs[k, 2:]) % (1 << 32)
+            if ranks:
+                slots = blob[h["slots_off"]:h["slots_off"] + SLOT.itemsize * U].view(SLOT)
+                xthr = blob[h["xthr_off"]:h["rank_tab_off"]].view(np.float32)
+                rtab = blob[h["rank_tab_off"]:h["rank_tab_off"] + 4 * vr * h["rank_tab_entries"]].view(
+                    np.uint32).reshape(-1, vr)
+                for sl, rs in enumerate(slots):
+                    assert rs["col"] == h["cols"][sl]
+                    if rs["n4"] == 0:
+                        continue
+                    t = np.concatenate([rs["thr"], xthr[4 * rs["xthr"]:4 * (rs["xthr"] + rs["n4"] - 1)]])
+                    assert len(t) == 4 * rs["n4"] and np.isinf(t[-1])
+                    rank = int((~(x[sl] <= t)).sum())          # NaN: every entry counts
+                    votes = (votes + rtab[rs["tab"] + rank]) % (1 << 32)
+            else:
+                for k in range(S):
+                    v = x[recs[k, 1]]
+                    right = (not (v <= thr[k])) if k < h["n_stumps_right"] else (v > thr[k])
+                    if right:
+                        votes = (votes + recs[k, 2:]) % (1 << 32)
             for t in trees:
                 m = (1 << 64) - 1
                 for nd in nodes[t["node_begin"]:t["node_begin"] + t["n_nodes"]]:
@@ -70,7 +88,9 @@ def test_compiled_blob_predicts_like_sklearn(n_classes, nan, F):
     if nan:
         X[rs.rand(400, F) < 0.05] = np.nan
     X32 = X.astype(np.float32)
-    assert np.array_equal(eval_blob(blob, X32), rf.predict(X32))
+    want = rf.predict(X32)
+    assert np.array_equal(eval_blob(blob, X32), want)
+    assert np.array_equal(eval_blob(blob, X32, ranks=True), want)
 
 
 def test_compile_rejects_unsupported_forests():
@@ -96,3 +116,4 @@ def test_stump_forest_has_no_general_trees():
     assert head["n_general"] == 0 and head["n_stumps"] == 100
     Xt = (0.05 + 0.1 * ((np.array([0, 1])[:, None] * 7 + np.arange(27) * 3) % 10)).astype(np.float32)
     assert np.array_equal(eval_blob(blob, Xt), rf.predict(Xt))
+    assert np.array_equal(eval_blob(blob, Xt, ranks=True), rf.predict(Xt))
