@@ -208,8 +208,10 @@ __device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restr
     const int n_subrows = (int)max((int64_t)0, (chunk_end - sub_end) / kSub);
     uint32_t* a_draws = tab;
     uint16_t* a_sub = reinterpret_cast<uint16_t*>(tab + kSub);
+#pragma unroll 2
     for (int k = threadIdx.x; k < n_draws; k += 64) a_draws[k] = R[P + k];
-    for (int64_t e = threadIdx.x; e < (int64_t)n_subrows * S; e += 64) a_sub[e] = Tsub[first_sub * S + e];
+#pragma unroll 8
+    for (int e = threadIdx.x; e < n_subrows * S; e += 64) a_sub[e] = Tsub[first_sub * S + e];
     __syncthreads();
     if (threadIdx.x == 0) {
         int64_t pos = P, batch = 0, k = 0;
@@ -245,7 +247,8 @@ __device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restr
         const int64_t c0 = pos0 / kChunk;
         const int nload = (int)min((int64_t)64, (avail - pos0) / kChunk);
         __syncthreads();
-        for (int64_t e = threadIdx.x; e < (int64_t)nload * S; e += 64) tab[e] = Tchunk[c0 * S + e];
+#pragma unroll 8
+        for (int e = threadIdx.x; e < nload * S; e += 64) tab[e] = Tchunk[c0 * S + e];
         __syncthreads();
         if (threadIdx.x == 0) {
             int64_t pos = pos0, batch = sh_batch, k = sh_k;
@@ -281,16 +284,20 @@ __global__ __launch_bounds__(64) void k_fsm_walk_batch(const Job* __restrict__ j
     fsm_walk(j.R, j.Tsub, j.Tchunk, j.P, j.W, L, j.avail, reinterpret_cast<ChunkStart*>(j.pieces), j.info);
 }
 
-// One wave per window piece.  The piece's sub-chunk table rows are staged in LDS, lane 0
-// derives every sub-chunk's start (state, batch); then the lanes replay sub-chunks: for
-// each accepted draw of batch b < W record J[b*L + s] = v & mask(s) and, when s == 1,
-// E[b] = draw index.
+// One wave per window piece.  The chunk's sub-chunk table rows are staged in LDS (16-byte
+// loads) together with the draws of the piece's first and last sub-chunk (the only ones
+// lane 0 may have to step draw by draw); lane 0 derives every sub-chunk's start (state,
+// batch); then each lane replays one sub-chunk straight from HBM, 16 draws per round of
+// loads: for each accepted draw of batch b < W record J[b*L + s] = v & mask(s) and, when
+// s == 1, E[b] = draw index.  (LDS per wave ~13 KB, so a CU holds many pieces at once.)
+constexpr int kReplayBatch = 16;
+
 __device__ void fsm_replay(const uint32_t* __restrict__ R, const uint16_t* __restrict__ Tsub,
                            const ChunkStart* __restrict__ pieces, const int64_t* __restrict__ info, int64_t W, int L,
                            uint8_t* __restrict__ J, int64_t* __restrict__ E, int64_t blk, int64_t nblk) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t rep_lds[];   // [kChunk] draws, then [64][S] rows
-    uint32_t* draws = rep_lds;
-    uint16_t* subtab = reinterpret_cast<uint16_t*>(rep_lds + kChunk);
+    extern __shared__ __attribute__((aligned(16))) uint32_t rep_lds[];   // [64][S] sub-chunk rows (u16)
+    uint16_t* subtab = reinterpret_cast<uint16_t*>(rep_lds);
+    __shared__ uint32_t edge[2][kSub];
     __shared__ int64_t sub_pos[kSubPerChunk + 2];
     __shared__ int32_t sub_state[kSubPerChunk + 2], sub_batch[kSubPerChunk + 2];
     __shared__ int n_subs;
@@ -299,16 +306,22 @@ __device__ void fsm_replay(const uint32_t* __restrict__ R, const uint16_t* __res
     for (int64_t pc = blk; pc < npieces; pc += nblk) {
         const ChunkStart c = pieces[pc];
         const int64_t stop = (pc + 1 < npieces) ? pieces[pc + 1].pos : end;
-        // stage the table rows of the whole sub-chunks of this piece's chunk
+        if (stop <= c.pos) continue;
+        // the chunk's sub-chunk rows: 64 * S u16 = 8 * S uint4, 16-byte aligned (the chunk's
+        // rows start at chunk * 128 * S bytes); rows past the piece are not read below
         const int64_t chunk = c.pos / kChunk;
         const int64_t first_sub = chunk * kSubPerChunk;
-        for (int64_t e = threadIdx.x; e < (int64_t)kSubPerChunk * S; e += 64) {
-            const int64_t sb = first_sub + e / S;
-            if ((sb + 1) * kSub <= stop) subtab[e] = Tsub[first_sub * S + e];
+        {
+            const uint4* src = reinterpret_cast<const uint4*>(Tsub + first_sub * S);
+            uint4* dst = reinterpret_cast<uint4*>(subtab);
+#pragma unroll 4
+            for (int e = threadIdx.x; e < 8 * S; e += 64) dst[e] = src[e];
         }
-        // the piece's draws (a piece lies inside one chunk)
-        const int64_t dbase = chunk * kChunk;
-        for (int64_t q = c.pos + threadIdx.x; q < stop; q += 64) draws[q - dbase] = R[q];
+        const int64_t sA = c.pos / kSub, sB = (stop - 1) / kSub;
+        for (int k = threadIdx.x; k < kSub; k += 64) {
+            edge[0][k] = R[sA * kSub + k];
+            edge[1][k] = R[sB * kSub + k];
+        }
         __syncthreads();
         if (threadIdx.x == 0) {
             int64_t pos = c.pos;
@@ -326,8 +339,9 @@ __device__ void fsm_replay(const uint32_t* __restrict__ R, const uint16_t* __res
                     s = e & 0xffu;
                     b += (int32_t)(e >> 8);
                 } else {
+                    const uint32_t* d = edge[pos / kSub == sA ? 0 : 1] - (pos / kSub) * kSub;
                     for (int64_t q = pos; q < nxt; ++q) {
-                        const uint32_t v = draws[q - dbase];
+                        const uint32_t v = d[q];
                         if ((v & imask(s)) <= s) {
                             if (s == 1) {
                                 s = (uint32_t)S;
@@ -347,17 +361,25 @@ __device__ void fsm_replay(const uint32_t* __restrict__ R, const uint16_t* __res
         for (int t = threadIdx.x; t < n_subs; t += 64) {
             uint32_t s = (uint32_t)sub_state[t];
             int64_t b = sub_batch[t];
-            for (int64_t q = sub_pos[t]; q < sub_pos[t + 1] && b < W; ++q) {
-                const uint32_t v = draws[q - dbase];
-                const uint32_t m = v & imask(s);
-                if (m <= s) {
-                    J[b * L + s] = (uint8_t)m;
-                    if (s == 1) {
-                        E[b] = q;
-                        s = (uint32_t)S;
-                        ++b;
-                    } else {
-                        --s;
+            const int64_t beg = sub_pos[t], fin = sub_pos[t + 1];
+            for (int64_t q0 = beg; q0 < fin && b < W; q0 += kReplayBatch) {
+                uint32_t v[kReplayBatch];
+#pragma unroll
+                for (int k = 0; k < kReplayBatch; ++k) v[k] = R[min(q0 + k, fin - 1)];
+#pragma unroll
+                for (int k = 0; k < kReplayBatch; ++k) {
+                    if (q0 + k < fin && b < W) {
+                        const uint32_t m = v[k] & imask(s);
+                        if (m <= s) {
+                            J[b * L + s] = (uint8_t)m;
+                            if (s == 1) {
+                                E[b] = q0 + k;
+                                s = (uint32_t)S;
+                                ++b;
+                            } else {
+                                --s;
+                            }
+                        }
                     }
                 }
             }
@@ -424,7 +446,7 @@ size_t walk_lds_bytes(int L) {
                     kSub * sizeof(uint32_t) + (size_t)kSubPerChunk * (L - 1) * sizeof(uint16_t));
 }
 
-size_t replay_lds_bytes(int L) { return kChunk * sizeof(uint32_t) + (size_t)kSubPerChunk * (L - 1) * sizeof(uint16_t); }
+size_t replay_lds_bytes(int L) { return (size_t)kSubPerChunk * (L - 1) * sizeof(uint16_t); }
 
 }  // namespace
 
