@@ -42,8 +42,10 @@ def parse():
     ap.add_argument("--rows-per-part", type=int, default=125_000_000)
     ap.add_argument("--block-rows", type=int, default=10_000_037, help="global class-block length (C3)")
     ap.add_argument("--features", type=int, default=27)
-    ap.add_argument("--refit", default="native", choices=["native", "sklearn"],
-                    help="native: ddm_rf_fit (identical trees to sklearn 1.7.2); sklearn: host sklearn")
+    ap.add_argument("--refit", default="device", choices=["device", "native", "sklearn"],
+                    help="device: ddm_rf_fit_device in the epoch that finds the change; native: "
+                         "ddm_rf_fit_many on host threads (both identical trees to sklearn 1.7.2); "
+                         "sklearn: host sklearn")
     ap.add_argument("--fit-threads", type=int, default=16, help="host threads for the tree-parallel native refits")
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--cpu-baseline", type=int, default=1)
@@ -146,7 +148,8 @@ def run_c3(args, world, rank, dev, torch, dist):
     agg = {k: sum(getattr(s, k) for s in st) for k in ("epochs", "refits", "predicted_rows", "refit_s",
                                                         "predict_ms", "predict_bytes", "scan_ms", "scan_rows",
                                                         "shuffle_ms", "host_s", "gpu_s", "refit_fit_s",
-                                                        "refit_readback_s", "prep_s")}
+                                                        "refit_readback_s", "prep_s", "dfit_ms",
+                                                        "device_refits")}
     drifts = int(sum((r[:, 1] >= 0).sum() for r in results.values()))
     warns = int(sum((r[:, 0] >= 0).sum() for r in results.values()))
     rows_rank = n * args.parts * args.steps
@@ -162,9 +165,12 @@ def run_c3(args, world, rank, dev, torch, dist):
                     f"class blocks of {block} global rows, INSTANCES={instances} (row % INSTANCES), "
                     f"{args.parts} partitions x {n} rows per GPU",
         "rows_per_gpu_step": n * args.parts, "partitions_per_gpu": args.parts,
-        "refit": ("native ddm_rf_fit_many (sklearn 1.7.2 RandomForestClassifier restated, identical trees), "
-                  f"all trees of an epoch's refits on {args.fit_threads} host threads") if args.refit == "native" else
-                 "host sklearn RandomForestClassifier(100 trees), in-process",
+        "refit": {"device": "ddm_rf_fit_device (sklearn 1.7.2 RandomForestClassifier restated, identical trees) "
+                            "on the GPU, one wave per tree, in the epoch that finds the change; each partition's "
+                            "first fit on the host",
+                  "native": "native ddm_rf_fit_many (sklearn 1.7.2 RandomForestClassifier restated, identical "
+                            f"trees), all trees of an epoch's refits on {args.fit_threads} host threads",
+                  "sklearn": "host sklearn RandomForestClassifier(100 trees), in-process"}[args.refit],
         "shuffle": "batch shuffles generated on the GPU from the partition's MT19937 stream (ddm_shuffle_*)",
         "execution": "all partitions of the GPU in lockstep epochs: one batched shuffle, predict and scan "
                      "launch per epoch (BatchRunner)",
@@ -179,7 +185,9 @@ def run_c3(args, world, rank, dev, torch, dist):
              "host_s_per_step": agg["host_s"] / args.steps, "gpu_wait_s_per_step": agg["gpu_s"] / args.steps,
              "refit_native_fit_s_per_step": agg["refit_fit_s"] / args.steps,
              "refit_readback_s_per_step": agg["refit_readback_s"] / args.steps,
-             "stream_prep_s_per_step": agg["prep_s"] / args.steps}
+             "stream_prep_s_per_step": agg["prep_s"] / args.steps,
+             "device_refits_per_step": agg["device_refits"] / args.steps,
+             "device_refit_kernels_ms_per_step": agg["dfit_ms"] / args.steps}
     roofline = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_from_profile("ddm_forest_predict", rows_per_launch),
                 "kernel": "ddm_forest_predict", "alg_bytes_per_row": "4*F_used + 6",

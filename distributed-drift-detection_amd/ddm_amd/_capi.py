@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
@@ -71,6 +71,8 @@ SIGNATURES = {
                                           ctypes.POINTER(ctypes.c_int64)]),
     "ddm_rf_fit_many": (ctypes.c_int, [_vp, _i32, _i32]),
     "ddm_epoch_stage": (ctypes.c_int, [_vp, _i32, _vp]),
+    "ddm_rf_device_scratch_bytes": (_i64, [_i32, _i32, _i32, _i32]),
+    "ddm_rf_fit_device": (ctypes.c_int, [_vp, _i32, _i32, _vp]),
     "ddm_words_perm_seeds": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _vp]),
     "ddm_rf_fit": (ctypes.c_int, [_vp, _i32, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp]),
     "ddm_synth_block_labels": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i32, _vp]),

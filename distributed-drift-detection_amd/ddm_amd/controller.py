@@ -27,7 +27,7 @@ import numpy as np
 import pandas as pd
 import torch
 
-from . import kernels
+from . import dfit, kernels
 from .forest import upload_forests
 from .params import OUTPUT_COLUMNS, DDMSettings, infer_x_features
 from .rng import MTStream
@@ -105,13 +105,13 @@ def sklearn_refit(settings):
 class RunStats:
     __slots__ = ("epochs", "refits", "predicted_rows", "refit_s", "gpu_s", "host_s", "predict_ms", "predict_bytes",
                  "scan_ms", "scan_rows", "shuffle_ms", "sklearn_refits", "refit_fit_s", "refit_readback_s",
-                 "prep_s")
+                 "prep_s", "dfit_ms", "device_refits")
 
     def __init__(self):
         self.epochs = self.refits = self.predicted_rows = self.predict_bytes = self.scan_rows = 0
-        self.sklearn_refits = 0
+        self.sklearn_refits = self.device_refits = 0
         self.refit_s = self.gpu_s = self.host_s = self.predict_ms = self.scan_ms = self.shuffle_ms = 0.0
-        self.refit_fit_s = self.refit_readback_s = self.prep_s = 0.0
+        self.refit_fit_s = self.refit_readback_s = self.prep_s = self.dfit_ms = 0.0
 
     def as_dict(self):
         return {k: getattr(self, k) for k in self.__slots__}
@@ -141,11 +141,16 @@ class BatchRunner:
     Partitions are independent (DDM_Process.py:226 groups by device_id), so a partition
     that is done simply drops out of the tables.
 
-    refit: "native" (ddm_rf_fit_many, identical trees to sklearn 1.7.2; sklearn itself for
-    NaN inputs) or "sklearn".  The native refits of all partitions that drifted in an
-    epoch are one call: every tree on a pool of `fit_threads` host threads."""
+    refit: "device" (ddm_rf_fit_device: the refit after a change runs on the GPU in the
+    same epoch, on the rows, labels and seeds the staging kernel gathered; trees
+    identical to the host trainer's), "native" (ddm_rf_fit_many, identical trees to
+    sklearn 1.7.2, on host threads) or "sklearn".  A device refit that reports a status
+    (NaN rows, more classes than its buffers hold) and the first fit of every partition
+    go through "native"; NaN inputs go to sklearn itself.  The native refits of all
+    partitions that drifted in an epoch are one call: every tree on a pool of
+    `fit_threads` host threads."""
 
-    def __init__(self, parts, settings=None, stream=None, refit="native", timing=False, fit_threads=8):
+    def __init__(self, parts, settings=None, stream=None, refit="device", timing=False, fit_threads=8):
         self.parts = list(parts)
         if not self.parts:
             raise ValueError("no partitions")
@@ -202,9 +207,10 @@ class BatchRunner:
         self.max_events = 64
         self.o_jobs = _round_up(self.o_state + 56 * k, 256)
         self.o_stage_tab = self.o_jobs + _round_up(n * kernels.JOB_DTYPE.itemsize, 256)
-        self.o_stage = self.o_stage_tab + _round_up(n * kernels.STAGE_DTYPE.itemsize, 256)
+        self.o_dfit_tab = self.o_stage_tab + _round_up(n * kernels.STAGE_DTYPE.itemsize, 256)
+        self.o_stage = self.o_dfit_tab + _round_up(n * dfit.DFIT_DTYPE.itemsize, 256)
         sz = {"x": 4 * 256 * F, "y": 4 * 256, "w": 4 * self.n_words, "info": 64, "ev": 12 * self.max_events,
-              "seeds": 8 * self.s.n_estimators}
+              "seeds": 8 * self.s.n_estimators, "dfit": 8 * dfit.RESULT_WORDS}
         self.stage_off, self.stage_stride = {}, {}
         o = self.o_stage
         for key, nbytes in sz.items():
@@ -229,6 +235,20 @@ class BatchRunner:
                                         self.ctrl_d[self.o_jobs:])
         self.stage_jobs = kernels.PinnedTable(kernels.STAGE_DTYPE, n, dev, self.ctrl_h[self.o_stage_tab:],
                                               self.ctrl_d[self.o_stage_tab:])
+        # device refits: per partition its output buffers and its (static) job record,
+        # pointing at the partition's staging outputs; gated on a change with device seeds
+        self.dfit_jobs = kernels.PinnedTable(dfit.DFIT_DTYPE, n, dev, self.ctrl_h[self.o_dfit_tab:],
+                                             self.ctrl_d[self.o_dfit_tab:])
+        self.dfit_bufs, self.dfit_rows = [], []
+        if refit == "device":
+            for i, part in enumerate(self.parts):
+                b = dfit.RefitBuffers(pb, part.X.shape[0], self.s.n_estimators, 16, dev)
+                info = self._sptr("info", i)
+                self.dfit_bufs.append(b)
+                self.dfit_rows.append(b.record(self._sptr("x", i), self._sptr("y", i), self._sptr("seeds", i),
+                                               self._sptr("dfit", i), gate=info, gate2=info + 48))
+        self.t_fit = ((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                      if timing and refit == "device" else None)
         # the partitions' MT19937 streams are generated and tabulated on a side stream, in
         # pieces, while the epochs run (GpuShuffle.wait_for orders the consumers)
         self.gen_stream = torch.cuda.Stream(dev)
@@ -331,6 +351,20 @@ class BatchRunner:
         work = []
         for k, ps in enumerate(need):
             sh = self.shuffles[ps.i]
+            if ps.staged is not None and isinstance(ps.staged[0], str):
+                # refit on the GPU in the epoch that found the change (ddm_rf_fit_device)
+                _, P1, P2, res = ps.staged
+                ps.staged = None
+                ps.P = P2
+                ps.P_after_first = ps.P
+                ps.forest = dfit.DeviceFitForest(self.dfit_bufs[ps.i], res)
+                ps.retrain = False
+                ps.state = kernels.fresh_states(1)              # ddm = None -> new DDM (:136-139)
+                ps.g0 = ps.j + 1
+                ps.seg_start = ps.j
+                st.refits += 1
+                st.device_refits += 1
+                continue
             if ps.staged is not None and ps.staged[3] is not None:
                 # batch j's shuffle is already in perm_all and the seeds came back staged
                 seeds, P1, P2 = ps.staged[3], ps.staged[4], ps.staged[5]
@@ -366,7 +400,7 @@ class BatchRunner:
         st = self.stats
         t0 = time.perf_counter()
         fits = [None] * len(work)
-        if self.refit_kind == "native":
+        if self.refit_kind in ("native", "device"):         # host refits of the device mode too
             t2 = time.perf_counter()
             fits = self.batch_trainer.fit_many([(X32, y, seeds) for _, X32, y, seeds, _ in work])
             st.refit_fit_s += time.perf_counter() - t2
@@ -571,6 +605,8 @@ class BatchRunner:
         if shuf:
             self._jobs_for(shuf, with_stop=True, upload=False)
         self._stage_table(live)
+        if self.dfit_rows:
+            self.dfit_jobs.rec[:len(live)] = np.array([self.dfit_rows[ps.i] for ps in live], dtype=dfit.DFIT_DTYPE)
         self.first_h[:] = -1                    # the predict kernels' first-error slots
         with torch.cuda.stream(stream):
             self.ctrl_d[:self.o_stage].copy_(self.ctrl_h[:self.o_stage], non_blocking=True)
@@ -590,6 +626,13 @@ class BatchRunner:
             kernels.shuffle_pick_batch(self.jobs, len(shuf), stream)
         # stage what the host needs next, then one copy back and one synchronisation
         kernels.epoch_stage(self.stage_jobs, len(live), stream, upload=False)
+        if self.dfit_rows:
+            # the refits of the partitions that changed, on the rows the staging gathered
+            if self.t_fit is not None:
+                self.t_fit[0].record(stream)
+            dfit.fit_device(self.dfit_jobs.d, len(live), self.s.n_estimators, stream)
+            if self.t_fit is not None:
+                self.t_fit[1].record(stream)
         with torch.cuda.stream(stream):
             self.ctrl_h.copy_(self.ctrl_d, non_blocking=True)
         stream.synchronize()
@@ -598,6 +641,8 @@ class BatchRunner:
             st.scan_ms += self.t_scan.elapsed_ms()
             if shuf:
                 st.shuffle_ms += self.t_shuf.elapsed_ms()
+            if self.t_fit is not None:
+                st.dfit_ms += self.t_fit[0].elapsed_time(self.t_fit[1])
         # read-backs beyond the staging (more events than it holds): rare
         pending = False
         for ps in live:
@@ -651,11 +696,16 @@ class BatchRunner:
                                        f"batch {int(info[3])} vs {d})")
                 L = ps.blen(d)
                 drawn = int(info[6]) == 1           # batch d+1's shuffle and the seeds, on the device
-                ps.staged = (self._sview("x", ps.i, np.float32, L * ps_feats(self.parts[ps.i])).reshape(L, -1).copy(),
-                             self._sview("y", ps.i, np.int32, L).astype(np.int64),
-                             None if drawn else self._sview("w", ps.i, np.uint32, self.n_words).copy(),
-                             self._sview("seeds", ps.i, np.int64, self.s.n_estimators).copy() if drawn else None,
-                             int(info[4]), int(info[5]))
+                res = self._sview("dfit", ps.i, np.int64, dfit.RESULT_WORDS) if self.dfit_rows else None
+                if drawn and res is not None and int(res[0]) == 0:
+                    ps.staged = ("device", int(info[4]), int(info[5]), res.copy())
+                else:
+                    F_i = ps_feats(self.parts[ps.i])
+                    ps.staged = (self._sview("x", ps.i, np.float32, L * F_i).reshape(L, -1).copy(),
+                                 self._sview("y", ps.i, np.int32, L).astype(np.int64),
+                                 None if drawn else self._sview("w", ps.i, np.uint32, self.n_words).copy(),
+                                 self._sview("seeds", ps.i, np.int64, self.s.n_estimators).copy() if drawn else None,
+                                 int(info[4]), int(info[5]))
                 ps.retrain = True
                 # adaptive speculation: the next concept likely lasts about as long as this
                 # one, so the next window covers it with 1/8 to spare (one epoch per drift
@@ -681,7 +731,7 @@ class BatchRunner:
 class PartitionRunner(BatchRunner):
     """One partition (the reference's per-UDF-call unit) on one HIP stream."""
 
-    def __init__(self, part, settings=None, stream=None, refit="native", timing=False, fit_threads=8):
+    def __init__(self, part, settings=None, stream=None, refit="device", timing=False, fit_threads=8):
         super().__init__([part], settings, stream, refit, timing, fit_threads=fit_threads)
         self.part = part
 
@@ -689,7 +739,7 @@ class PartitionRunner(BatchRunner):
         return super().run([rng])[0]
 
 
-def run_partition_frame(pdf, rng, settings=None, device=None, stream=None, refit="native", stats=None):
+def run_partition_frame(pdf, rng, settings=None, device=None, stream=None, refit="device", stats=None):
     """One partition frame through the GPU path with an explicit MT19937 stream `rng`
     (the RNG a Spark Python worker would hold).  Returns the reference's output frame:
     one row per batch after the first, columns warning_flag_local/global and
@@ -710,7 +760,7 @@ def run_partition_frame(pdf, rng, settings=None, device=None, stream=None, refit
     return events_frame(rows, pdf.index.to_numpy(), pdf[s.row_number].to_numpy())
 
 
-def run_partition_frames(frames, rngs, settings=None, device=None, stream=None, refit="native", stats=None):
+def run_partition_frames(frames, rngs, settings=None, device=None, stream=None, refit="device", stats=None):
     """Many partition frames of ONE device in lockstep (BatchRunner): the output frame of
     each, as run_partition_frame would return it, with rngs[k] consumed by frames[k]."""
     s = settings or DDMSettings()
@@ -741,7 +791,7 @@ def events_frame(rows, local_labels, global_labels):
     return pd.DataFrame(res, columns=OUTPUT_COLUMNS, index=np.zeros(len(res), dtype=np.int64))
 
 
-def run_DDM_loop(pdf, settings=None, device=None, stream=None, refit="native", stats=None):
+def run_DDM_loop(pdf, settings=None, device=None, stream=None, refit="device", stats=None):
     """Drop-in for the grouped-map UDF `run_DDM_loop` (DDM_Process.py:166-213): same input
     frame, same output frame, and it draws from / advances numpy's global RandomState
     exactly as the reference does (so `np.random.seed(k)` before the call reproduces the

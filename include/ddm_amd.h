@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 6
+#define DDM_AMD_ABI_VERSION 7
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -360,6 +360,51 @@ typedef struct ddm_fit_job {
 } ddm_fit_job;
 
 int ddm_rf_fit_many(ddm_fit_job* jobs, int32_t n_jobs, int32_t n_threads);
+
+/* ---- device forest refit ---------------------------------------
+ * train_rf (DDM_Process.py:98-105) on the GPU, tree for tree what ddm_rf_fit builds
+ * (scikit-learn 1.7.2: bootstrap from RandomState(seed), BestSplitter with our_rand_r
+ * feature draws, Gini, fully grown), then packed and compiled as ddm_rf_fit_many does,
+ * so that the refit after a change never leaves the device: the training batch, its
+ * labels and the tree seeds are the ones ddm_epoch_stage gathered and drew.  One wave
+ * builds one tree.  Limits: L <= 256 rows, F <= 256 features, k_cap <= 64 classes;
+ * a job outside them, or with NaN in X, reports a status and is refit on the host. */
+typedef struct ddm_dfit_job {
+    const float* X;          /* device [L][F] float32 row-major (ddm_stage_job.x_out)      */
+    const int32_t* y;        /* device [L] labels (ddm_stage_job.y_out)                      */
+    const int64_t* seeds;    /* device [n_trees] tree seeds (ddm_stage_job.seeds_out)        */
+    const int64_t* gate;     /* device: the job runs only when *gate >= 0 (NULL: always),
+                                e.g. ddm_stage_job.info_out (the change's stream position) */
+    const int64_t* gate2;    /* device: and only when *gate2 == 1 (NULL: no condition),
+                                e.g. info_out + 6 (the seeds were drawn on the device)      */
+    int32_t L, F, n_trees, max_features;
+    int32_t k_cap, pad;      /* classes the job's buffers hold (<= 64)                       */
+    uint8_t* scratch;        /* device, ddm_rf_device_scratch_bytes(L, F, n_trees, k_cap)   */
+    ddm_node* nodes;         /* device outputs, as ddm_rf_fit writes them: [n_trees*(2L-1)] */
+    int32_t* roots;          /* [n_trees]                                                    */
+    double* leaf_value;      /* [n_trees*L][k_cap] (impure forests)                          */
+    int32_t* classes;        /* [k_cap] sorted labels (classes_)                             */
+    uint8_t* blob;           /* the ddm_forest_compile blob, when the forest compiles        */
+    int64_t blob_cap;
+    int64_t* result;         /* device int64[12]: DDM_DFIT_* indices                        */
+} ddm_dfit_job;
+
+#define DDM_DFIT_STATUS    0   /* -1 not run (gate), 0 ok, DDM_E_NAN / DDM_E_FOREST / DDM_E_ARG */
+#define DDM_DFIT_CLASSES   1
+#define DDM_DFIT_NODES     2
+#define DDM_DFIT_PURE      3
+#define DDM_DFIT_LEAF_ROWS 4
+#define DDM_DFIT_BLOB      5   /* blob bytes; 0: not compilable (node walk)                  */
+#define DDM_DFIT_CF_SLOTS  6
+#define DDM_DFIT_CF_VR     7
+#define DDM_DFIT_CF_LEAVES 8
+#define DDM_DFIT_CF_TAB    9
+
+int64_t ddm_rf_device_scratch_bytes(int32_t L, int32_t F, int32_t n_trees, int32_t k_cap);
+
+/* Fits every job (device table of n_jobs records) on `stream`; max_trees bounds the
+ * jobs' n_trees (grid size).  Asynchronous: results land in each job's result[]. */
+int ddm_rf_fit_device(const ddm_dfit_job* jobs_dev, int32_t n_jobs, int32_t max_trees, ddm_stream_t stream);
 
 /* ---- synthetic inputs (benchmark configs) ------------------------- */
 

@@ -93,8 +93,9 @@ def test_synthetic_rialto_stream_vs_oracle():
     assert (want[:, 2] >= 0).sum() >= 3
 
 
-@pytest.mark.parametrize("win,maxwin", [(256, 1 << 16), (1, 8), (7, 64)])
-def test_lockstep_batch_of_unequal_partitions_vs_oracle(win, maxwin):
+@pytest.mark.parametrize("win,maxwin,refit", [(256, 1 << 16, "device"), (1, 8, "device"), (7, 64, "device"),
+                                              (256, 1 << 16, "native"), (7, 64, "native")])
+def test_lockstep_batch_of_unequal_partitions_vs_oracle(win, maxwin, refit):
     """Partitions of different lengths (short tails, one finishing epochs before the
     others) in ONE BatchRunner == the oracle run on each partition alone."""
     from ddm_amd import kernels
@@ -114,7 +115,7 @@ def test_lockstep_batch_of_unequal_partitions_vs_oracle(win, maxwin):
     for part in parts:
         host.append((part.X[:, :part.n].t().contiguous().cpu().numpy().astype(np.float64),
                      part.y[:part.n].cpu().numpy().astype(np.int64)))
-    runner = BatchRunner(parts, DDMSettings(window_batches=win, max_window_batches=maxwin))
+    runner = BatchRunner(parts, DDMSettings(window_batches=win, max_window_batches=maxwin), refit=refit)
     rngs = [MTStream.from_seed(50 + k) for k in range(len(parts))]
     got = runner.run(rngs)
     runner.close()
@@ -127,3 +128,9 @@ def test_lockstep_batch_of_unequal_partitions_vs_oracle(win, maxwin):
         assert np.array_equal(rngs[k].key, after[1]) and rngs[k].pos.value == after[2], k
         drifts += int((want[:, 2] >= 0).sum())
     assert drifts >= 5
+    # every refit after a change ran on the device, the first one of each partition natively
+    if refit == "device":
+        assert runner.stats.device_refits > 0
+        assert runner.stats.device_refits + len(parts) >= runner.stats.refits - 1
+    else:
+        assert runner.stats.device_refits == 0
