@@ -202,10 +202,9 @@ def run_c4(args, world, rank, dev, torch, dist):
     S, L = args.c4_streams, args.c4_len
     err = torch.empty(S * L + 16, dtype=torch.uint8, device=dev)
     kernels.synth_bernoulli_streams(err, S, L, args.seed + rank)
-    off = torch.arange(S + 1, dtype=torch.int64, device=dev) * L
     nb = (L + 99) // 100
-    base = torch.arange(S, dtype=torch.int64, device=dev) * nb
     ev = torch.empty((S * nb, 2), dtype=torch.int32, device=dev)
+    flags = torch.empty(kernels.scan_batches_scratch_size(S, L), dtype=torch.uint8, device=dev)
     state0 = torch.from_numpy(kernels.fresh_states(S).view(np.uint8)).to(dev)
     state = torch.empty_like(state0)
     prm = kernels.params_struct()
@@ -216,7 +215,7 @@ def run_c4(args, world, rank, dev, torch, dist):
         state.copy_(state0)
         if timed:
             e0.record(stream)
-        kernels.scan_streams(err, off, prm, state, base, S * nb, ev, mode=1, stream=stream)
+        kernels.scan_batches(err, S, L, prm, state, ev, flags, stream=stream)
         if timed:
             e1.record(stream)
 
@@ -255,9 +254,10 @@ def run_c4(args, world, rank, dev, torch, dist):
                         f"by U(.05,.3)), DDM only, fresh DDM at the batch after each change"}
     extra = {"changes_per_step": changes, "scan_kernel_ms": avg_ms}
     roofline = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_from_profile("ddm_scan_streams", S * L),
-                "kernel": "ddm_scan_streams", "alg_bytes_per_row": "1 + 8/100",
-                "avg_launch_ms": avg_ms, "note": "fp64-VALU bound: ~45 VALU/row recurrence"}
+                "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_from_profile("ddm_scan_batches", S * L),
+                "kernel": "ddm_scan_batches", "alg_bytes_per_row": "1 + 8/100",
+                "avg_launch_ms": avg_ms,
+                "note": "k_scan_batches_spec + k_scan_batches_fix (batch-parallel speculation, per-stream fix-up)"}
     return rows, elapsed, info, extra, roofline, cpu
 
 

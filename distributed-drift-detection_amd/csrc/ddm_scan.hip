@@ -398,7 +398,516 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Batch-parallel scan for many independent, equal-length, back-to-back streams in mode 1
+// (configs[3]: 1M streams x 4096 rows, reset-heavy).
+//
+// In mode 1 a change drops the detector and the next batch starts fresh
+// (DDM_Process.py:207-210), so every batch whose predecessor changed is independent of
+// everything before it.  On reset-heavy streams that is nearly every batch, so:
+//
+//  * k_scan_batches_spec: every batch of every stream is scanned on its own with a FRESH
+//    detector (speculation).  A batch is one work item; a wave owns a contiguous range of
+//    items and hands them to its lanes dynamically (refill when >= kRefill lanes are idle),
+//    so the short trivial items and the long exact ones even out over the wave and each
+//    wave-iteration is either a refill or an exact row, never both.  Starting an item
+//    loads its <= 128 bytes as 16-byte chunks, folds them into a 128-bit nonzero mask
+//    and resolves the trivial case at once (two leading zeros then the first error is
+//    the change, or no error at all); otherwise the lane runs exact rows, x from the mask,
+//    1/n from a 1 KB LDS table (n <= 129 inside one batch).
+//    It writes the item's (warning, change) pair and a flag byte (bit 0 change, bit 1 any
+//    event).
+//  * k_scan_batches_fix: one lane per stream walks its flag bytes.  A batch whose
+//    detector really is fresh (the carried state for batch 0, a change before it
+//    otherwise) keeps the speculative result; every other batch (the successor of an
+//    unchanged batch) is rescanned exactly with the carried detector, which also
+//    rebuilds the carry through unchanged batches.  It writes the carried state and the
+//    per-stream event count.
+//
+// Decisions are those of k_scan_streams bit for bit: the same recurrence, the same
+// shortcuts (gate 3 only), the same event positions.
+constexpr int kBatchRcp = 160;
+constexpr int kSpecThreads = 256;
+constexpr int kMaxBatch = 128;
+
+// bit k set <=> byte k of w is nonzero
+__device__ __forceinline__ uint32_t nz4(uint32_t w) {
+    const uint32_t t = (((w & 0x7f7f7f7fu) + 0x7f7f7f7fu) | w) & 0x80808080u;
+    return (((t >> 7) * 0x00204081u) >> 21) & 0xfu;
+}
+
+__device__ __forceinline__ uint32_t nz16(uint4 v) {
+    return nz4(v.x) | (nz4(v.y) << 4) | (nz4(v.z) << 8) | (nz4(v.w) << 12);
+}
+
+// 128-bit nonzero mask of the rows [bstart, bstart + blen), blen in 1..128: bit t of
+// (m0, m1) = row bstart + t is an error.  All nine 16-byte loads are issued before any
+// is used (chunk addresses past the batch are clamped to its last chunk, their bits
+// dropped).
+__device__ __forceinline__ void batch_mask(const uint8_t* __restrict__ err, int64_t bstart, int blen,
+                                           uint64_t& m0, uint64_t& m1) {
+    const int64_t c0 = bstart & ~(int64_t)15;
+    const int64_t clast = (bstart + blen - 1) & ~(int64_t)15;
+    const int off = (int)(bstart & 15);
+    const int nch = (off + blen + 15) >> 4;
+    uint4 v[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) v[k] = *reinterpret_cast<const uint4*>(err + min(c0 + 16 * k, clast));
+    uint32_t c[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) c[k] = k < nch ? nz16(v[k]) : 0u;
+    const uint64_t a0 = (uint64_t)c[0] | ((uint64_t)c[1] << 16) | ((uint64_t)c[2] << 32) | ((uint64_t)c[3] << 48);
+    const uint64_t a1 = (uint64_t)c[4] | ((uint64_t)c[5] << 16) | ((uint64_t)c[6] << 32) | ((uint64_t)c[7] << 48);
+    const uint64_t a2 = c[8];
+    m0 = off ? (a0 >> off) | (a1 << (64 - off)) : a0;
+    m1 = off ? (a1 >> off) | (a2 << (64 - off)) : a1;
+    if (blen < 64) {
+        m0 &= (1ull << blen) - 1;
+        m1 = 0;
+    } else if (blen < 128) {
+        m1 &= (1ull << (blen - 64)) - 1;
+    }
+}
+
+__device__ __forceinline__ int mask_bit(uint64_t m0, uint64_t m1, int i) {
+    return (int)((i < 64 ? m0 >> i : m1 >> (i - 64)) & 1ull);
+}
+
+// first set bit at or after i (128 if none)
+__device__ __forceinline__ int mask_next(uint64_t m0, uint64_t m1, int i) {
+    if (i < 64) {
+        const uint64_t t = m0 & (~0ull << i);
+        if (t) return __builtin_ctzll(t);
+        return m1 ? 64 + __builtin_ctzll(m1) : 128;
+    }
+    if (i >= 128) return 128;
+    const uint64_t t = m1 & (~0ull << (i - 64));
+    return t ? 64 + __builtin_ctzll(t) : 128;
+}
+
+struct SmallDet {          // a detector inside one batch: n <= kMaxBatch + 1
+    double p, s, pmin, smin, psmin;
+    int n;
+};
+
+// returns 2 = change, 1 = warning, 0 = neither
+__device__ __forceinline__ int small_add(SmallDet& d, int x, int min_inst, double wl, double cl,
+                                         const double* __restrict__ rcp) {
+    const double n = (double)d.n;
+    const double r = rcp[d.n];
+    const double p = d.p + div_rn((double)x - d.p, n, r);
+    const double s = sqrt(div_rn(p * (1.0 - p), n, r));
+    d.p = p;
+    d.s = s;
+    d.n += 1;
+    if (d.n < min_inst) return 0;
+    const double ps = p + s;
+    if (ps <= d.psmin) {
+        d.pmin = p;
+        d.smin = s;
+        d.psmin = ps;
+    }
+    if (ps > d.pmin + cl * d.smin) return 2;
+    return ps > d.pmin + wl * d.smin ? 1 : 0;
+}
+
+__device__ __forceinline__ bool state_fresh(const ddm_state& st) {
+    return st.in_concept_change || (st.sample_count == 1 && st.miss_prob == 1.0 && st.miss_std == 0.0 &&
+                                    st.miss_prob_sd_min == __builtin_huge_val() &&
+                                    st.miss_prob_min == __builtin_huge_val() && st.miss_sd_min == __builtin_huge_val());
+}
+
+// The fix-up list: streams with an unchanged batch (need[s], stored by the speculative
+// pass) or a carry-in that is not fresh.  Every other stream's speculation is its result:
+// the reset state (its last batch changed) and nb batches with an event.
+__global__ __launch_bounds__(256) void k_scan_batches_list(int64_t n_streams, int64_t nb,
+                                                           ddm_state* __restrict__ state,
+                                                           const uint32_t* __restrict__ need,
+                                                           int64_t* __restrict__ nev_out, int32_t* __restrict__ list,
+                                                           uint32_t* __restrict__ ctr) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    bool fix = false;
+    if (t < n_streams) {
+        fix = need[t] != 0u || !state_fresh(state[t]);
+        if (!fix) {
+            if (nb > 0) {
+                ddm_state st;
+                st.miss_prob = 1.0;
+                st.miss_std = 0.0;
+                st.miss_prob_min = st.miss_sd_min = st.miss_prob_sd_min = __builtin_huge_val();
+                st.sample_count = 1;
+                st.in_concept_change = 0;
+                st.in_warning_zone = 0;
+                state[t] = st;
+            }
+            if (nev_out) nev_out[t] = nb;
+        }
+    }
+    const uint64_t m = __ballot(fix);
+    if (!m) return;
+    const int lane = threadIdx.x & 63, lead = __builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == lead) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = __shfl(base, lead);
+    if (fix) list[base + __popcll(m & ((1ull << lane) - 1))] = (int32_t)t;
+}
+
+__global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
+    const uint8_t* __restrict__ err, int64_t n_items, int64_t L, int64_t nb, int64_t nbp, ddm_params P,
+    int2* __restrict__ ev, uint8_t* __restrict__ flags, const uint8_t* __restrict__ pmap,
+    int64_t items_per_wave, int refill, uint32_t* __restrict__ need) {
+    __shared__ double rcp[kBatchRcp];
+    for (int k = threadIdx.x; k < kBatchRcp; k += kSpecThreads) rcp[k] = 1.0 / (double)(k > 0 ? k : 1);
+    __syncthreads();
+    const int pb = (int)P.per_batch;
+    const int min_inst = P.min_num_instances;
+    const double wl = P.warning_level, cl = P.out_control_level;
+    const bool shortcuts = min_inst == 3;
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1;
+    const int64_t wave = (int64_t)blockIdx.x * (kSpecThreads / 64) + (threadIdx.x >> 6);
+    int64_t cursor = wave * items_per_wave;
+    const int64_t wend = min(cursor + items_per_wave, n_items);
+    const double inv_nb = 1.0 / (double)nb;
+
+    bool busy = false;
+    int64_t item = 0, bstart = 0, fpos = 0, sid = 0;
+    int blen = 0, i = 0, wpos = -1;
+    uint64_t m0 = 0, m1 = 0;
+    SmallDet d;
+    d.p = d.s = d.pmin = d.smin = d.psmin = 0.0;
+    d.n = 1;
+
+    for (;;) {
+        const uint64_t idle_m = __ballot(!busy);
+        const int nidle = __popcll(idle_m);
+        if (cursor >= wend && nidle == 64) break;
+        if (cursor < wend && (nidle >= refill || nidle == 64)) {
+            // refill: idle lanes take the next items of the wave's range, in lane order
+            if (!busy) {
+                item = cursor + __popcll(idle_m & below);
+                if (item < wend) {
+                    int64_t s = (int64_t)((double)item * inv_nb);
+                    if (s * nb > item) --s;
+                    else if ((s + 1) * nb <= item) ++s;
+                    const int64_t j = item - s * nb;
+                    sid = s;
+                    bstart = s * L + j * pb;
+                    fpos = s * nbp + j;
+                    blen = (int)min((int64_t)pb, L - j * pb);
+                    batch_mask(err, bstart, blen, m0, m1);
+                    if (shortcuts && blen >= 2 && (m0 & 3ull) == 0) {
+                        // fresh + two zero rows = trivial state (n = 3); its first error row
+                        // is the change (p + s > 0), and zeros raise nothing
+                        const int t = mask_next(m0, m1, 2);
+                        if (t < blen) {
+                            ev[item] = make_int2(-1, pmap ? (int)pmap[bstart + t] : t);
+                            flags[fpos] = 3;
+                        } else {
+                            ev[item] = make_int2(-1, -1);
+                            flags[fpos] = 0;
+                            need[sid] = 1u;
+                        }
+                    } else {
+                        busy = true;
+                        i = 0;
+                        wpos = -1;
+                        d.p = 1.0;
+                        d.s = 0.0;
+                        d.pmin = d.smin = d.psmin = __builtin_huge_val();
+                        d.n = 1;
+                    }
+                }
+            }
+            cursor += nidle;
+        } else if (busy) {
+            // one exact row of the lane's item
+            const int r = small_add(d, mask_bit(m0, m1, i), min_inst, wl, cl, rcp);
+            if (r == 1 && wpos < 0) wpos = i;
+            ++i;
+            if (r == 2 || i >= blen) {
+                const bool chg = r == 2;
+                const int w = wpos < 0 ? -1 : (pmap ? (int)pmap[bstart + wpos] : wpos);
+                const int cp = chg ? (pmap ? (int)pmap[bstart + i - 1] : i - 1) : -1;
+                ev[item] = make_int2(w, cp);
+                flags[fpos] = (uint8_t)((chg ? 1 : 0) | ((chg || wpos >= 0) ? 2 : 0));
+                if (!chg) need[sid] = 1u;
+                busy = false;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void load_det(Det& d, const ddm_state& st) {
+    d.p = st.miss_prob;
+    d.s = st.miss_std;
+    d.pmin = st.miss_prob_min;
+    d.smin = st.miss_sd_min;
+    d.psmin = st.miss_prob_sd_min;
+    d.n = st.sample_count;
+    d.chg = st.in_concept_change;
+    d.warn = st.in_warning_zone;
+}
+
+__device__ __forceinline__ ddm_state store_det(const Det& d) {
+    ddm_state st;
+    st.miss_prob = d.p;
+    st.miss_std = d.s;
+    st.miss_prob_min = d.pmin;
+    st.miss_sd_min = d.smin;
+    st.miss_prob_sd_min = d.psmin;
+    st.sample_count = d.n;
+    st.in_concept_change = d.chg;
+    st.in_warning_zone = d.warn;
+    return st;
+}
+
+// Fix-up: persistent lanes take the streams of the fix-up list and run each batch after
+// batch through one flat loop.  A lane is idle, waiting to open a batch, or stepping
+// through one; each wave-iteration does one kind of work for the lanes in that state, so
+// memory latency (claiming streams: state + flags; opening a batch: its 128-bit mask) is
+// paid once for many lanes, and stepping never waits on memory:
+//   claim  when >= refill lanes are idle: the next list entries, their carried state and
+//          first 64-batch window of flags;
+//   open   when >= open_thr lanes wait: skip the run of batches whose speculative change
+//          stands (a fresh detector and a change flag: bit operations on the window),
+//          finish the stream at its end, else load the batch mask;
+//   step   one row step of the rescan (k_scan_fast's mode-1 rules, Markstein division).
+constexpr int kFixThreads = 256;
+
+__device__ __forceinline__ uint64_t change_window(const uint8_t* __restrict__ fl, int64_t wbase, int64_t nb) {
+    uint64_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint4 v = *reinterpret_cast<const uint4*>(fl + wbase + 16 * q);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t b = w[k] & 0x01010101u;            // bit 0 of each flag byte
+            m |= (uint64_t)(((b * 0x00204081u) >> 21) & 0xfu) << (16 * q + 4 * k);
+        }
+    }
+    const int64_t valid = nb - wbase;
+    return valid < 64 ? m & ((1ull << valid) - 1) : m;
+}
+
+__global__ __launch_bounds__(kFixThreads) void k_scan_batches_fix(
+    const uint8_t* __restrict__ err, int64_t L, int64_t nb, int64_t nbp, ddm_params P,
+    ddm_state* __restrict__ state, int2* __restrict__ ev, const uint8_t* __restrict__ flags,
+    int64_t* __restrict__ nev_out, const uint8_t* __restrict__ pmap, const int32_t* __restrict__ list,
+    uint32_t* __restrict__ ctr, int refill, int open_thr) {
+    __shared__ double rcp[kRcpN];
+    for (int k = threadIdx.x; k < kRcpN; k += kFixThreads) rcp[k] = 1.0 / (double)(k > 0 ? k : 1);
+    __syncthreads();
+    const int64_t pb = P.per_batch;
+    const int min_inst = P.min_num_instances;
+    const double wl = P.warning_level, cl = P.out_control_level;
+    const bool shortcuts = min_inst == 3;
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1;
+    const uint32_t n_list = __atomic_load_n(ctr, __ATOMIC_RELAXED);
+    uint32_t claimed = 0;                           // wave-uniform: claims exhausted once >= n_list
+
+    enum { IDLE = 0, OPEN = 1, STEP = 2 };
+    Det d;
+    d.p = d.s = d.pmin = d.smin = d.psmin = 0.0;
+    d.n = 1;
+    d.chg = d.warn = 0;
+    int64_t sid = 0, j = 0, wbase = 0, nev = 0, bstart = 0;
+    uint64_t chg_m = 0, m0 = 0, m1 = 0;
+    int blen = 0, i = 0, wpos = -1, mode = IDLE;
+    for (;;) {
+        const uint64_t idle_m = __ballot(mode == IDLE);
+        const uint64_t open_m = __ballot(mode == OPEN);
+        const int nidle = __popcll(idle_m), nopen = __popcll(open_m);
+        const bool stepping = nidle + nopen < 64;
+        if (claimed < n_list && (nidle >= refill || (!stepping && nopen == 0))) {
+            const int lead = __builtin_ctzll(idle_m);
+            uint32_t base = 0;
+            if (lane == lead) base = atomicAdd(ctr + 1, (uint32_t)nidle);
+            base = __shfl(base, lead);
+            claimed = base + (uint32_t)nidle;
+            if (mode == IDLE) {
+                const uint32_t k = base + (uint32_t)__popcll(idle_m & below);
+                if (k < n_list) {
+                    sid = list[k];
+                    load_det(d, state[sid]);
+                    j = 0;
+                    wbase = 0;
+                    chg_m = nb > 0 ? change_window(flags + sid * nbp, 0, nb) : 0;
+                    nev = 0;
+                    mode = OPEN;
+                }
+            }
+            continue;
+        }
+        if (nopen > 0 && (nopen >= open_thr || !stepping)) {
+            if (mode == OPEN) {
+                for (;;) {
+                    if (j >= nb) break;
+                    if (j >= wbase + 64) {          // next 64-batch window (nb > 64 only)
+                        wbase = j & ~(int64_t)63;
+                        chg_m = change_window(flags + sid * nbp, wbase, nb);
+                    }
+                    if (!det_fresh(d)) break;
+                    const uint64_t rel = chg_m >> (j - wbase);
+                    const int run = (int)min((int64_t)(rel == ~0ull ? 64 : __builtin_ctzll(~rel)), wbase + 64 - j);
+                    if (run == 0) break;
+                    nev += run;                     // batches whose speculative change stands
+                    j += run;
+                    det_reset(d);
+                }
+                if (j >= nb) {                      // stream done
+                    state[sid] = store_det(d);
+                    if (nev_out) nev_out[sid] = nev;
+                    mode = IDLE;
+                } else {
+                    bstart = sid * L + j * pb;
+                    blen = (int)min(pb, L - j * pb);
+                    batch_mask(err, bstart, blen, m0, m1);
+                    i = 0;
+                    wpos = -1;
+                    mode = STEP;
+                }
+            }
+            continue;
+        }
+        if (!stepping) break;                       // all idle, claims exhausted
+        if (mode != STEP) continue;
+        // one step of the rescan of batch j
+        const int xi = mask_bit(m0, m1, i);
+        const bool triv = det_trivial(d);
+        int cpos = -1;
+        if (shortcuts && !triv && i + 1 < blen && det_fresh(d) && xi == 0 && mask_bit(m0, m1, i + 1) == 0) {
+            d.p = d.s = d.pmin = d.smin = d.psmin = 0.0;
+            d.n = 3;
+            d.chg = d.warn = 0;
+            i += 2;
+        } else if (triv && xi == 0) {
+            const int t = min(mask_next(m0, m1, i), blen);
+            d.n += t - i;
+            d.warn = 0;
+            i = t;
+        } else if (shortcuts && triv && d.n >= 3) {
+            cpos = i;
+            ++i;
+        } else {
+            // exact rows until a change or the end of the batch, in one tight loop: the long
+            // carried chains (a detector that stays unchanged batch after batch) are the
+            // tail of this kernel, and the shortcuts above are exact equivalents only
+            for (int x = xi;;) {
+                det_add_fast(d, x, min_inst, wl, cl, rcp);
+                if (d.warn && wpos < 0) wpos = i;
+                ++i;
+                if (d.chg) {
+                    cpos = i - 1;
+                    break;
+                }
+                if (i >= blen) break;
+                x = mask_bit(m0, m1, i);
+            }
+        }
+        if (cpos >= 0 || i >= blen) {
+            int w = wpos, c = cpos;
+            if (pmap) {
+                if (w >= 0) w = pmap[bstart + w];
+                if (c >= 0) c = pmap[bstart + c];
+            }
+            ev[sid * nb + j] = make_int2(w, c);
+            nev += (w >= 0 || c >= 0);
+            if (cpos >= 0) det_reset(d);            // DDM dropped (DDM_Process.py:209)
+            ++j;
+            mode = OPEN;
+        }
+    }
+}
+
 }  // namespace
+
+namespace {
+struct BatchScratch {
+    uint32_t* ctr;      // [0] fix-up list length, [1] claim cursor
+    uint32_t* need;     // [n_streams]
+    int32_t* list;      // [n_streams]
+    uint8_t* flags;     // [n_streams * nbp], 64-byte aligned rows
+    int64_t bytes;
+};
+
+BatchScratch batch_scratch(void* base, int64_t n_streams, int64_t nb) {
+    const auto up = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
+    const int64_t nbp = ddm::ceil_div(nb, 64) * 64;
+    const int64_t o_need = 256, o_list = o_need + up(4 * n_streams), o_flags = o_list + up(4 * n_streams);
+    uint8_t* b = static_cast<uint8_t*>(base);
+    return {reinterpret_cast<uint32_t*>(b), reinterpret_cast<uint32_t*>(b + o_need),
+            reinterpret_cast<int32_t*>(b + o_list), b + o_flags, o_flags + up(n_streams * nbp)};
+}
+}  // namespace
+
+extern "C" int64_t ddm_scan_batches_scratch_bytes(int64_t n_streams, int64_t stream_len, int32_t per_batch) {
+    if (n_streams < 0 || stream_len < 0 || per_batch <= 0) return -1;
+    return batch_scratch(nullptr, n_streams, ddm::ceil_div(stream_len, per_batch)).bytes;
+}
+
+extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t stream_len, const ddm_params* prm,
+                                ddm_state* state_io, int32_t* ev_out, int64_t* nev_out, void* scratch,
+                                const uint8_t* perm_map, ddm_stream_t stream, ddm_event_t ev_begin,
+                                ddm_event_t ev_end) {
+    if (!err || !prm || !state_io || !ev_out || !scratch || n_streams < 0 || n_streams >= ((int64_t)1 << 31) ||
+        stream_len < 0 || prm->per_batch <= 0 || prm->per_batch > kMaxBatch) {
+        ddm::set_error("ddm_scan_batches: invalid argument (per_batch must be 1..%d)", kMaxBatch);
+        return DDM_E_ARG;
+    }
+    const int64_t nb = ddm::ceil_div(stream_len, prm->per_batch);
+    const int64_t nbp = ddm::ceil_div(nb, 64) * 64;
+    const int64_t n_items = n_streams * nb;
+    if (n_streams == 0) return 0;
+    const BatchScratch sc = batch_scratch(scratch, n_streams, nb);
+    hipStream_t s = ddm::as_hip(stream);
+    static const int refill = [] {
+        const char* e = getenv("DDM_SCAN_REFILL");
+        return e ? atoi(e) : 40;
+    }();
+    static const int64_t waves_max = [] {
+        const char* e = getenv("DDM_SCAN_WAVES");
+        return e ? atoll(e) : 256 * 4 * 8;
+    }();
+    static const int64_t fix_blocks_max = [] {
+        const char* e = getenv("DDM_FIX_BLOCKS");
+        return e ? atoll(e) : 512;
+    }();
+    static const int fix_refill = [] {
+        const char* e = getenv("DDM_FIX_REFILL");
+        return e ? atoi(e) : 16;
+    }();
+    static const int fix_open = [] {
+        const char* e = getenv("DDM_FIX_OPEN");
+        return e ? atoi(e) : 16;
+    }();
+    if (ev_begin)
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
+    if (int rc = ddm::hip_status(hipMemsetAsync(scratch, 0, (size_t)(256 + ((4 * n_streams + 255) & ~255)), s),
+                                 "ddm_scan_batches: memset"))
+        return rc;
+    if (n_items > 0) {
+        // ~8 waves per SIMD of resident work, each owning a contiguous range of items
+        const int64_t waves = std::max<int64_t>(1, std::min<int64_t>(waves_max, ddm::ceil_div(n_items, 256)));
+        const int64_t per_wave = ddm::ceil_div(n_items, waves);
+        const int64_t blocks = ddm::ceil_div(ddm::ceil_div(n_items, per_wave), kSpecThreads / 64);
+        hipLaunchKernelGGL(k_scan_batches_spec, dim3((unsigned)blocks), dim3(kSpecThreads), 0, s, err, n_items,
+                           stream_len, nb, nbp, *prm, reinterpret_cast<int2*>(ev_out), sc.flags, perm_map, per_wave,
+                           refill, sc.need);
+        if (int rc = ddm::launch_status("ddm_scan_batches")) return rc;
+    }
+    hipLaunchKernelGGL(k_scan_batches_list, dim3((unsigned)ddm::ceil_div(n_streams, 256)), dim3(256), 0, s, n_streams,
+                       nb, state_io, sc.need, nev_out, sc.list, sc.ctr);
+    const int64_t fix_blocks = std::max<int64_t>(1, std::min<int64_t>(fix_blocks_max, ddm::ceil_div(n_streams, kFixThreads)));
+    hipLaunchKernelGGL(k_scan_batches_fix, dim3((unsigned)fix_blocks), dim3(kFixThreads), 0, s, err, stream_len, nb,
+                       nbp, *prm, state_io, reinterpret_cast<int2*>(ev_out), sc.flags, nev_out, perm_map, sc.list,
+                       sc.ctr, fix_refill, fix_open);
+    if (ev_end)
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
+    return ddm::launch_status("ddm_scan_batches");
+}
 
 extern "C" int ddm_scan_streams(const uint8_t* err, const int64_t* stream_off, int64_t n_streams,
                                 const ddm_params* prm, ddm_state* state_io, const uint64_t* first_nz,

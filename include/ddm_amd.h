@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 7
+#define DDM_AMD_ABI_VERSION 8
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -228,6 +228,24 @@ int ddm_scan_streams(const uint8_t* err, const int64_t* stream_off, int64_t n_st
                      int32_t* stop_out, int64_t* nev_out, int32_t mode, double* ps_out,
                      const uint8_t* perm_map, const int64_t* stream_end, ddm_stream_t stream,
                      ddm_event_t ev_begin, ddm_event_t ev_end);
+
+/* run_DDM in mode 1 (fresh DDM at the batch after a change) over n_streams independent
+ * streams of stream_len rows each, back to back: stream s is err[s*stream_len ..
+ * (s+1)*stream_len) (err readable up to the next multiple of 16 bytes past the end).
+ * Replaces the per-row DDM loop of run_DDM (DDM_Process.py:135-159) for DDM-only
+ * streams (SURVEY.md §8 a4/a5, configs[3]); results are those of ddm_scan_streams in
+ * mode 1 with offsets s*stream_len and batch_base s*nb, nb = ceil(stream_len/per_batch).
+ * Batch-parallel: every batch is scanned speculatively with a fresh detector, then one
+ * lane per stream rescans the batches whose carry-in was not fresh.
+ * per_batch must be 1..128.  ev_out: int32 [n_streams*nb][2] (every entry written);
+ * nev_out (may be NULL): batches with an event per stream; scratch: device memory of
+ * ddm_scan_batches_scratch_bytes(...) bytes, 256-byte aligned (n_streams < 2^31);
+ * perm_map: as for ddm_scan_streams. */
+int64_t ddm_scan_batches_scratch_bytes(int64_t n_streams, int64_t stream_len, int32_t per_batch);
+int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t stream_len, const ddm_params* prm,
+                     ddm_state* state_io, int32_t* ev_out, int64_t* nev_out, void* scratch,
+                     const uint8_t* perm_map, ddm_stream_t stream, ddm_event_t ev_begin,
+                     ddm_event_t ev_end);
 
 /* Timing events for the ev_begin / ev_end arguments (hipEventCreate / Destroy /
  * ElapsedTime; elapsed needs both events completed, e.g. after a stream sync). */
