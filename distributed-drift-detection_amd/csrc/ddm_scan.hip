@@ -552,23 +552,30 @@ __global__ __launch_bounds__(256) void k_scan_batches_list(int64_t n_streams, in
     if (fix) list[base + __popcll(m & ((1ull << lane) - 1))] = (int32_t)t;
 }
 
+// Per-wave LDS queue of the batches that need exact rows (mask + batch), see below.
+constexpr int kSpecQ = 256;
+
 __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
     const uint8_t* __restrict__ err, int64_t n_items, int64_t L, int64_t nb, int64_t nbp, ddm_params P,
     int2* __restrict__ ev, uint8_t* __restrict__ flags, const uint8_t* __restrict__ pmap,
-    int64_t items_per_wave, int refill, uint32_t* __restrict__ need) {
+    int64_t items_per_wave, int fill_below, uint32_t* __restrict__ need) {
     __shared__ double rcp[kBatchRcp];
+    __shared__ uint64_t qm0[kSpecThreads / 64][kSpecQ], qm1[kSpecThreads / 64][kSpecQ];
+    __shared__ uint32_t qitem[kSpecThreads / 64][kSpecQ];
     for (int k = threadIdx.x; k < kBatchRcp; k += kSpecThreads) rcp[k] = 1.0 / (double)(k > 0 ? k : 1);
     __syncthreads();
     const int pb = (int)P.per_batch;
     const int min_inst = P.min_num_instances;
     const double wl = P.warning_level, cl = P.out_control_level;
     const bool shortcuts = min_inst == 3;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t below = (1ull << lane) - 1;
-    const int64_t wave = (int64_t)blockIdx.x * (kSpecThreads / 64) + (threadIdx.x >> 6);
-    int64_t cursor = wave * items_per_wave;
-    const int64_t wend = min(cursor + items_per_wave, n_items);
+    const int64_t wave = (int64_t)blockIdx.x * (kSpecThreads / 64) + wv;
+    const int64_t wstart = wave * items_per_wave;
+    const int64_t wend = min(wstart + items_per_wave, n_items);
+    int64_t cursor = wstart;
     const double inv_nb = 1.0 / (double)nb;
+    int qhead = 0, qcount = 0;                      // wave-uniform ring state
 
     bool busy = false;
     int64_t item = 0, bstart = 0, fpos = 0, sid = 0;
@@ -578,50 +585,96 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
     d.p = d.s = d.pmin = d.smin = d.psmin = 0.0;
     d.n = 1;
 
+    auto locate = [&](int64_t it) {                 // item -> stream, batch, rows, flag slot
+        int64_t s = (int64_t)((double)it * inv_nb);
+        if (s * nb > it) --s;
+        else if ((s + 1) * nb <= it) ++s;
+        const int64_t j = it - s * nb;
+        sid = s;
+        bstart = s * L + j * pb;
+        fpos = s * nbp + j;
+        blen = (int)min((int64_t)pb, L - j * pb);
+    };
+
     for (;;) {
         const uint64_t idle_m = __ballot(!busy);
-        const int nidle = __popcll(idle_m);
-        if (cursor >= wend && nidle == 64) break;
-        if (cursor < wend && (nidle >= refill || nidle == 64)) {
-            // refill: idle lanes take the next items of the wave's range, in lane order
+        int nidle = __popcll(idle_m);
+        if (qcount > 0 && nidle > 0) {
+            // pop: idle lanes take queued batches in lane order (LDS only)
+            const int take = min(nidle, qcount);
             if (!busy) {
-                item = cursor + __popcll(idle_m & below);
-                if (item < wend) {
-                    int64_t s = (int64_t)((double)item * inv_nb);
-                    if (s * nb > item) --s;
-                    else if ((s + 1) * nb <= item) ++s;
-                    const int64_t j = item - s * nb;
-                    sid = s;
-                    bstart = s * L + j * pb;
-                    fpos = s * nbp + j;
-                    blen = (int)min((int64_t)pb, L - j * pb);
-                    batch_mask(err, bstart, blen, m0, m1);
-                    if (shortcuts && blen >= 2 && (m0 & 3ull) == 0) {
-                        // fresh + two zero rows = trivial state (n = 3); its first error row
-                        // is the change (p + s > 0), and zeros raise nothing
-                        const int t = mask_next(m0, m1, 2);
-                        if (t < blen) {
-                            ev[item] = make_int2(-1, pmap ? (int)pmap[bstart + t] : t);
-                            flags[fpos] = 3;
-                        } else {
-                            ev[item] = make_int2(-1, -1);
-                            flags[fpos] = 0;
-                            need[sid] = 1u;
-                        }
-                    } else {
-                        busy = true;
-                        i = 0;
-                        wpos = -1;
-                        d.p = 1.0;
-                        d.s = 0.0;
-                        d.pmin = d.smin = d.psmin = __builtin_huge_val();
-                        d.n = 1;
-                    }
+                const int rank = __popcll(idle_m & below);
+                if (rank < take) {
+                    const int q = (qhead + rank) & (kSpecQ - 1);
+                    m0 = qm0[wv][q];
+                    m1 = qm1[wv][q];
+                    item = wstart + qitem[wv][q];
+                    locate(item);
+                    busy = true;
+                    i = 0;
+                    wpos = -1;
+                    d.p = 1.0;
+                    d.s = 0.0;
+                    d.pmin = d.smin = d.psmin = __builtin_huge_val();
+                    d.n = 1;
                 }
             }
-            cursor += nidle;
-        } else if (busy) {
-            // one exact row of the lane's item
+            qhead = (qhead + take) & (kSpecQ - 1);
+            qcount -= take;
+            nidle -= take;
+        }
+        if (cursor < wend && qcount < fill_below) {
+            // fill: the next 64 items, one per lane (all lanes; busy ones pause a step).
+            // Trivial batches are resolved here; the others go to the queue.
+            bool exact = false;
+            uint64_t a0 = 0, a1 = 0;
+            const int64_t it = cursor + lane;
+            if (it < wend) {
+                const int64_t keep_item = item, keep_b = bstart, keep_f = fpos, keep_s = sid;
+                const int keep_len = blen;
+                locate(it);
+                batch_mask(err, bstart, blen, a0, a1);
+                if (shortcuts && blen >= 2 && (a0 & 3ull) == 0) {
+                    // fresh + two zero rows = trivial state (n = 3); its first error row
+                    // is the change (p + s > 0), and zeros raise nothing
+                    const int t = mask_next(a0, a1, 2);
+                    if (t < blen) {
+                        ev[it] = make_int2(-1, pmap ? (int)pmap[bstart + t] : t);
+                        flags[fpos] = 3;
+                    } else {
+                        ev[it] = make_int2(-1, -1);
+                        flags[fpos] = 0;
+                        need[sid] = 1u;
+                    }
+                } else {
+                    exact = true;
+                }
+                item = keep_item;
+                bstart = keep_b;
+                fpos = keep_f;
+                sid = keep_s;
+                blen = keep_len;
+            }
+            const uint64_t ex_m = __ballot(exact);
+            if (exact) {
+                const int q = (qhead + qcount + __popcll(ex_m & below)) & (kSpecQ - 1);
+                qm0[wv][q] = a0;
+                qm1[wv][q] = a1;
+                qitem[wv][q] = (uint32_t)(it - wstart);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            qcount += __popcll(ex_m);
+            cursor += 64;
+            continue;
+        }
+        if (nidle == 64) {
+            if (cursor >= wend && qcount == 0) break;
+            continue;
+        }
+        if (busy) {
+            // one exact row of the lane's batch
             const int r = small_add(d, mask_bit(m0, m1, i), min_inst, wl, cl, rcp);
             if (r == 1 && wpos < 0) wpos = i;
             ++i;
@@ -864,12 +917,12 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
     const BatchScratch sc = batch_scratch(scratch, n_streams, nb);
     hipStream_t s = ddm::as_hip(stream);
     static const int refill = [] {
-        const char* e = getenv("DDM_SCAN_REFILL");
-        return e ? atoi(e) : 40;
+        const char* e = getenv("DDM_SCAN_FILL");
+        return std::max(1, std::min(kSpecQ - 64, e ? atoi(e) : 64));
     }();
     static const int64_t waves_max = [] {
         const char* e = getenv("DDM_SCAN_WAVES");
-        return e ? atoll(e) : 256 * 4 * 8;
+        return e ? atoll(e) : 256 * 4 * 4;
     }();
     static const int64_t fix_blocks_max = [] {
         const char* e = getenv("DDM_FIX_BLOCKS");
@@ -891,7 +944,11 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
     if (n_items > 0) {
         // ~8 waves per SIMD of resident work, each owning a contiguous range of items
         const int64_t waves = std::max<int64_t>(1, std::min<int64_t>(waves_max, ddm::ceil_div(n_items, 256)));
-        const int64_t per_wave = ddm::ceil_div(n_items, waves);
+        const int64_t per_wave = ddm::ceil_div(n_items, waves);   // < 2^32 (queue entries hold an offset)
+        if (per_wave >= ((int64_t)1 << 32)) {
+            ddm::set_error("ddm_scan_batches: too many batches");
+            return DDM_E_ARG;
+        }
         const int64_t blocks = ddm::ceil_div(ddm::ceil_div(n_items, per_wave), kSpecThreads / 64);
         hipLaunchKernelGGL(k_scan_batches_spec, dim3((unsigned)blocks), dim3(kSpecThreads), 0, s, err, n_items,
                            stream_len, nb, nbp, *prm, reinterpret_cast<int2*>(ev_out), sc.flags, perm_map, per_wave,
