@@ -74,6 +74,22 @@ class DevicePartition:
         part.host_X32, part.host_y = X32, y.astype(np.int64)
         return part
 
+    @classmethod
+    def from_columns(cls, Xc, y, device, stream=None):
+        """Xc: float32 [F, n] columnar host array (loader.PartitionArrays.X32), y: int labels."""
+        Xc = np.asarray(Xc, dtype=np.float32)
+        y = np.asarray(y)
+        if y.size and (y.min() < np.iinfo(np.int32).min or y.max() > np.iinfo(np.int32).max):
+            raise ValueError("labels must fit int32 on the device path")
+        F, n = Xc.shape
+        part = cls.allocate(n, F, device)
+        with torch.cuda.stream(stream or torch.cuda.current_stream(device)):
+            if n:
+                part.X[:, :n].copy_(torch.from_numpy(np.ascontiguousarray(Xc)))
+                part.y[:n].copy_(torch.from_numpy(y.astype(np.int32)))
+        part.host_X32, part.host_y = np.ascontiguousarray(Xc.T), y.astype(np.int64)
+        return part
+
     def rows(self, rows, stream):
         """Training rows (features float32 [k, F], labels int64) in the given order."""
         if self.host_X32 is not None:
@@ -780,6 +796,24 @@ def run_partition_frames(frames, rngs, settings=None, device=None, stream=None, 
     if stats is not None:
         stats.update(runner.stats.as_dict())
     return [events_frame(r, *lab) for r, lab in zip(rows, labels)]
+
+
+def run_partition_arrays(parts, rngs, settings=None, device=None, stream=None, refit="device", stats=None):
+    """Columnar partitions of ONE device (loader.PartitionArrays: float32 [F, n], labels,
+    full_df_row_number) in lockstep, without pandas on the way in: the output frame of
+    each, as run_partition_frame would return it for parts[k].frame(...)."""
+    s = settings or DDMSettings()
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    dparts = [DevicePartition.from_columns(p.X32, p.target, device, stream) for p in parts]
+    runner = BatchRunner(dparts, s, stream, refit)
+    try:
+        rows = runner.run(rngs)
+    finally:
+        runner.close()
+    if stats is not None:
+        stats.update(runner.stats.as_dict())
+    return [events_frame(r, np.arange(len(p.target)), p.row_number) for r, p in zip(rows, parts)]
 
 
 def events_frame(rows, local_labels, global_labels):

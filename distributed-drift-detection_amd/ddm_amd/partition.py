@@ -18,7 +18,7 @@ import numpy as np
 import pandas as pd
 import torch
 
-from .controller import run_partition_frames
+from .controller import run_partition_arrays, run_partition_frames
 from .params import OUTPUT_COLUMNS, DDMSettings
 from .rng import MTStream
 
@@ -103,3 +103,41 @@ def apply_in_pandas(df, instances, base_seed, settings=None, devices=None, max_w
     outs = run_partitions(parts, {d: base_seed + d for d, _ in parts}, settings, devices, max_workers)
     frames = [outs[d] for d, _ in parts]
     return pd.concat(frames) if frames else pd.DataFrame(columns=OUTPUT_COLUMNS)
+
+
+def run_stream_file(path, mult, instances, base_seed, data_seed=None, sort_kind="quicksort", settings=None,
+                    devices=None, engine="pyarrow"):
+    """The reference's whole job minus Spark (DDM_Process.py:38-55, :216-258): load and
+    prepare the stream, split it into INSTANCES partitions, run every partition on the GPUs
+    of this process (partition d on GPU d % n_gpus, seeded base_seed + d), and collect the
+    output.  Returns (events frame in device_id order, post-loop record dict with the
+    distances of DDM_Process.py:250-257, the total time of :224-258 and the mean distance)."""
+    import time
+
+    from . import loader, record
+    table, order, parts = loader.load_partitions(path, mult, instances, data_seed, sort_kind, engine)
+    s = settings or DDMSettings()
+    if devices is None:
+        devices = [torch.device("cuda", i) for i in range(torch.cuda.device_count())]
+    if not devices:
+        raise RuntimeError("no GPU visible: the MI355X partition path needs a HIP device")
+    t0 = time.perf_counter()
+    groups = {}
+    for p in parts:
+        groups.setdefault(placement(p.device_id, len(devices)), []).append(p)
+
+    def on_gpu(item):
+        g, items = item
+        outs = run_partition_arrays(items, [MTStream.from_seed(base_seed + p.device_id) for p in items], s,
+                                    devices[g], torch.cuda.Stream(devices[g]))
+        return [(p.device_id, o) for p, o in zip(items, outs)]
+
+    with ThreadPoolExecutor(max(1, len(groups))) as ex:
+        res = dict(kv for pairs in ex.map(on_gpu, sorted(groups.items())) for kv in pairs)
+    frames = [res[p.device_id] for p in parts]
+    events = pd.concat(frames) if frames else pd.DataFrame(columns=OUTPUT_COLUMNS)
+    dist = record.dist_between_changes(len(order), table.target[order])
+    changes = record.change_distances(events, dist)
+    total = time.perf_counter() - t0
+    return events, {"distances": changes, "dist_between_changes": dist, "total_time": total,
+                    "average_distance": float(changes["distance"].mean()) if len(changes) else float("nan")}
