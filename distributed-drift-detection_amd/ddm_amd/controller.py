@@ -21,6 +21,7 @@ shuffle and the refit's 100 tree seeds are read from the stream on the host, the
 forest is refit natively on batch d, and the next window starts at d+1.  Work past d
 is discarded, so total predict work stays within ~2x the rows.
 """
+import os
 import time
 
 import numpy as np
@@ -33,6 +34,12 @@ from .params import OUTPUT_COLUMNS, DDMSettings, infer_x_features
 from .rng import MTStream
 from .shuffle import GpuShuffle, expected_draws_per_batch, perm_seeds_from_words
 from .trainer import BatchForestTrainer
+
+# Largest piece of a partition's MT19937 stream generated per side-stream launch: an epoch
+# waits only for the piece holding the draws it reads, so the generator (one sequential
+# recurrence per partition) runs ahead of the epochs instead of holding them to its end.
+GEN_PIECE_MAX = int(os.environ.get("DDM_GEN_PIECE", 1 << 22))
+
 
 def _round_up(n, m):
     return (n + m - 1) // m * m
@@ -268,6 +275,9 @@ class BatchRunner:
         # the partitions' MT19937 streams are generated and tabulated on a side stream, in
         # pieces, while the epochs run (GpuShuffle.wait_for orders the consumers)
         self.gen_stream = torch.cuda.Stream(dev)
+        # tables on a stream of their own: the generator (8 workgroups, one sequential
+        # recurrence per partition) never waits for a piece's tables before the next piece
+        self.tab_stream = torch.cuda.Stream(dev)
         self.gen_tables = []
         # pinned staging per partition: [0] batch-j shuffle of a refit epoch, [1] short last
         # batch, [2] drift batch's shuffle read back
@@ -275,7 +285,7 @@ class BatchRunner:
         self.shuffles = []
         for part, nb, mw in zip(self.parts, self.nbs, self.max_wins):
             cap = int(nb * expected_draws_per_batch(pb) * 1.2) + 64 * 1024
-            self.shuffles.append(GpuShuffle(dev, pb, cap, mw, self.stream, self.gen_stream))
+            self.shuffles.append(GpuShuffle(dev, pb, cap, mw, self.stream, self.gen_stream, self.tab_stream))
         self.stats = RunStats()
 
     # -- helpers
@@ -308,10 +318,13 @@ class BatchRunner:
             kernels.shuffle_generate_batch(table, len(reqs), self.gen_stream)
             self.gen_tables.append(table)
         if tabs:
+            g = torch.cuda.Event()
+            g.record(self.gen_stream)
+            self.tab_stream.wait_event(g)
             for i, need in tabs:
                 self.shuffles[i].tables_to(need)
             ev = torch.cuda.Event()
-            ev.record(self.gen_stream)
+            ev.record(self.tab_stream)
             for i, _ in tabs:
                 self.shuffles[i].mark_ready(ev)
         if wait:
@@ -532,7 +545,7 @@ class BatchRunner:
                                  wait=False)
                 if upto >= total:
                     break
-                upto = min(total, upto * 4)
+                upto = min(total, upto + min(upto, GEN_PIECE_MAX))
             if self.timing:
                 st.prep_s += time.perf_counter() - tp
             for ps in pss:

@@ -106,11 +106,12 @@ class GpuShuffle:
     itself) in pieces, each closed by an event; consumers on `stream` wait on the event of
     the piece that covers what they read (`wait_for`), so generation overlaps the epochs."""
 
-    def __init__(self, device, L, capacity_draws, max_window, stream, gen_stream=None):
+    def __init__(self, device, L, capacity_draws, max_window, stream, gen_stream=None, tab_stream=None):
         if not 2 <= L <= 256:
             raise ValueError("GPU shuffles need 2 <= batch length <= 256")
         self.device, self.L, self.S, self.stream = device, L, L - 1, stream
         self.gen_stream = gen_stream or stream
+        self.tab_stream = tab_stream or self.gen_stream   # tables (after the words they read)
         self.max_window = int(max_window)
         self.mt = torch.zeros(625, dtype=torch.int32, device=device)
         self._alloc(max(2 * CHUNK, int(capacity_draws)))
@@ -148,6 +149,7 @@ class GpuShuffle:
         st[624] = self.init_pos
         self.stream.synchronize()
         self.gen_stream.synchronize()       # nothing of the previous run may still read R
+        self.tab_stream.synchronize()
         with torch.cuda.stream(self.gen_stream):
             self.mt.copy_(torch.from_numpy(st.view(np.int32)))
         self.gen = self.tab = self.waited = 0
@@ -158,6 +160,9 @@ class GpuShuffle:
 
     def _gp(self):
         return ctypes.c_void_p(self.gen_stream.cuda_stream)
+
+    def _tp(self):
+        return ctypes.c_void_p(self.tab_stream.cuda_stream)
 
     def window_draws(self, W):
         """Draws a window of W batches may need (mean + 15% + slack; windows grow R on demand)."""
@@ -181,15 +186,17 @@ class GpuShuffle:
         return req, need_chunks
 
     def tables_to(self, need_chunks):
-        """Tabulate up to need_chunks on gen_stream (after the words they read)."""
+        """Tabulate up to need_chunks on tab_stream (ordered after the words they read: the
+        caller makes tab_stream wait for gen_stream when they differ)."""
         if need_chunks > self.tab:
             check(lib.ddm_shuffle_tables(self.R.data_ptr(), self.tab, need_chunks - self.tab, self.L,
-                                         self.Tsub.data_ptr(), self.Tchunk.data_ptr(), self._gp()),
+                                         self.Tsub.data_ptr(), self.Tchunk.data_ptr(), self._tp()),
                   "ddm_shuffle_tables")
             self.tab = need_chunks
 
     def mark_ready(self, event):
-        """Everything enqueued on gen_stream so far is complete once `event` fires."""
+        """Everything enqueued on tab_stream (and so on gen_stream) so far is complete once
+        `event` fires."""
         self.ready.append((self.tab, event))
 
     def wait_for(self, upto):
@@ -212,9 +219,13 @@ class GpuShuffle:
             req, need_chunks = self.gen_request(upto)
             if req is not None:
                 check(lib.ddm_shuffle_generate(req[0], req[1], req[2], self._gp()), "ddm_shuffle_generate")
+            if self.tab_stream is not self.gen_stream:
+                g = torch.cuda.Event()
+                g.record(self.gen_stream)
+                self.tab_stream.wait_event(g)
             self.tables_to(need_chunks)
             ev = torch.cuda.Event()
-            ev.record(self.gen_stream)
+            ev.record(self.tab_stream)
             self.mark_ready(ev)
         self.wait_for(upto)
 
