@@ -104,6 +104,85 @@ __global__ __launch_bounds__(256) void k_mt_generate(uint32_t* __restrict__ stat
     mt_generate(state, R, n);
 }
 
+// g(T) * key on the device.  T^i(key) is the window (x_i .. x_{i+623}) of the MT19937
+// word sequence that starts with key (x_{k+624} = f(x_k, x_{k+1}, x_{k+397})), so by
+// linearity g(T) * key = XOR over the set coefficients i of g of those windows:
+//   1. the sequence x_0 .. x_{623 + deg g} (untempered) is generated into scratch, a
+//      624-word block per three barrier phases;
+//   2. thread j accumulates out[j] = XOR_i x_{i+j} over the ~10k set bits of g (coalesced
+//      reads across the threads, the bit scan uniform).
+struct JumpJob {
+    const uint32_t* key;
+    const uint64_t* poly;
+    uint32_t* out;
+    uint32_t* scratch;
+};
+
+__global__ __launch_bounds__(256) void k_mt_jump(const JumpJob* __restrict__ jobs) {
+    __shared__ uint64_t P[DDM_MT_POLY_WORDS];
+    __shared__ uint32_t blk[2][kN];
+    __shared__ int top_s;
+    const JumpJob jb = jobs[blockIdx.x];
+    const int t = threadIdx.x;
+    if (t == 0) top_s = -1;
+    for (int k = t; k < DDM_MT_POLY_WORDS; k += 256) P[k] = jb.poly[k];
+    for (int k = t; k < kN; k += 256) {
+        blk[0][k] = jb.key[k];
+        jb.scratch[k] = jb.key[k];
+    }
+    __syncthreads();
+    for (int k = t; k < DDM_MT_POLY_WORDS; k += 256)
+        if (P[k]) atomicMax(&top_s, 64 * k + 63 - __builtin_clzll(P[k]));
+    __syncthreads();
+    const int top = top_s;
+    // 1. x_624 .. x_{623 + top}: whole blocks
+    int cur = 0;
+    for (int64_t base = kN; base < kN + top; base += kN) {
+        const uint32_t* o = blk[cur];
+        uint32_t* w = blk[cur ^ 1];
+        if (t < 227) {
+            const uint32_t v = mt_word(o[t], o[t + 1], o[t + 397]);
+            w[t] = v;
+            jb.scratch[base + t] = v;
+        }
+        __syncthreads();
+        if (t < 227) {
+            const int i = 227 + t;
+            const uint32_t v = mt_word(o[i], o[i + 1], w[t]);
+            w[i] = v;
+            jb.scratch[base + i] = v;
+        }
+        __syncthreads();
+        if (t < 170) {
+            const int i = 454 + t;
+            const uint32_t v = (i < kN - 1) ? mt_word(o[i], o[i + 1], w[i - 227]) : mt_word(o[kN - 1], w[0], w[396]);
+            w[i] = v;
+            jb.scratch[base + i] = v;
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    __threadfence_block();
+    __syncthreads();
+    // 2. out[j] = XOR over set bits i of x_{i+j}
+    uint32_t a0 = 0, a1 = 0, a2 = 0;
+    const uint32_t* x = jb.scratch;
+    for (int wd = 0; wd * 64 <= top; ++wd) {
+        uint64_t bits = P[wd];
+        while (bits) {
+            const int i = 64 * wd + __builtin_ctzll(bits);
+            bits &= bits - 1;
+            a0 ^= x[i + t];
+            a1 ^= x[i + t + 256];
+            if (t < kN - 512) a2 ^= x[i + t + 512];
+        }
+    }
+    jb.out[t] = top >= 0 ? a0 : 0u;
+    jb.out[t + 256] = top >= 0 ? a1 : 0u;
+    if (t < kN - 512) jb.out[t + 512] = top >= 0 ? a2 : 0u;
+    if (t == 0) jb.out[kN] = kN;
+}
+
 struct GenJob {
     uint32_t* state;
     uint32_t* R;
@@ -521,6 +600,20 @@ extern "C" int ddm_shuffle_generate(uint32_t* mt_state, uint32_t* R, int64_t n, 
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_mt_generate, dim3(1), dim3(256), 0, ddm::as_hip(stream), mt_state, R, n);
     return ddm::launch_status("ddm_shuffle_generate");
+}
+
+extern "C" int ddm_mt_jump(const ddm_jump_job* jobs_dev, int32_t n_jobs, ddm_stream_t stream) {
+    if (!jobs_dev || n_jobs < 0) {
+        ddm::set_error("ddm_mt_jump: invalid argument");
+        return DDM_E_ARG;
+    }
+    if (n_jobs == 0) return 0;
+    static_assert(sizeof(JumpJob) == sizeof(ddm_jump_job), "JumpJob must mirror ddm_jump_job");
+    static_assert(DDM_MT_JUMP_SCRATCH_WORDS >= kN * ((kN + 64 * DDM_MT_POLY_WORDS + kN - 1) / kN + 1),
+                  "jump scratch holds the whole blocks of x_0 .. x_{623 + deg}");
+    hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)n_jobs), dim3(256), 0, ddm::as_hip(stream),
+                       reinterpret_cast<const JumpJob*>(jobs_dev));
+    return ddm::launch_status("ddm_mt_jump");
 }
 
 extern "C" int ddm_shuffle_tables(const uint32_t* R, int64_t chunk0, int64_t nchunk, int32_t batch_len,

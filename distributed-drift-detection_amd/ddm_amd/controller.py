@@ -38,7 +38,7 @@ from .trainer import BatchForestTrainer
 # Largest piece of a partition's MT19937 stream generated per side-stream launch: an epoch
 # waits only for the piece holding the draws it reads, so the generator (one sequential
 # recurrence per partition) runs ahead of the epochs instead of holding them to its end.
-GEN_PIECE_MAX = int(os.environ.get("DDM_GEN_PIECE", 1 << 22))
+GEN_PIECE_MAX = int(os.environ.get("DDM_GEN_PIECE", 1 << 25))
 
 
 def _round_up(n, m):
@@ -308,8 +308,7 @@ class BatchRunner:
             sh = self.shuffles[i]
             if sh.chunks_for(upto) > sh.tab:
                 req, need = sh.gen_request(upto)
-                if req is not None:
-                    reqs.append(req)
+                reqs.extend(req)
                 tabs.append((i, need))
         if reqs:
             table = kernels.PinnedTable(kernels.GEN_DTYPE, len(reqs), self.device)   # read by the async copy

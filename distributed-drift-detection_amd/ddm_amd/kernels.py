@@ -81,6 +81,33 @@ def shuffle_generate_batch(table, n_jobs, stream):
           "ddm_shuffle_generate_batch")
 
 
+JUMP_DTYPE = np.dtype([("key", "<u8"), ("poly", "<u8"), ("out", "<u8"), ("scratch", "<u8")])
+JUMP_SCRATCH_WORDS = 21216
+POLY_WORDS = 312
+_poly_cache = {}
+
+
+def mt_jump_polys(jump, n, device):
+    """Device tensor [n, POLY_WORDS] of x^((k+1)*jump) mod phi (MT19937 jump-ahead), cached
+    per (device, jump) and grown on demand."""
+    key = (str(device), int(jump))
+    held = _poly_cache.setdefault(key, [])
+    if not held or held[-1].shape[0] < n:
+        m = max(int(n), 256, 2 * (held[-1].shape[0] if held else 0))
+        host = np.zeros((m, POLY_WORDS), dtype=np.uint64)
+        check(lib.ddm_mt_jump_polys(int(jump), m, host.ctypes.data), "ddm_mt_jump_polys")
+        t = torch.from_numpy(host.view(np.int64)).to(device)
+        torch.cuda.synchronize(device)      # readers run on other streams
+        held.append(t)                      # earlier tables stay alive for in-flight jumps
+    return held[-1]
+
+
+def mt_jump(table, n_jobs, stream):
+    """ddm_mt_jump over the first n_jobs records of a PinnedTable of JUMP_DTYPE."""
+    table.upload(n_jobs, stream)
+    check(lib.ddm_mt_jump(table.d.data_ptr(), int(n_jobs), ctypes.c_void_p(stream.cuda_stream)), "ddm_mt_jump")
+
+
 def shuffle_window_batch(table, n_jobs, max_W, max_pieces, batch_len, stream, timer=None):
     """Window shuffles of every job in the (already uploaded) job table."""
     check(lib.ddm_shuffle_window_batch(table.d.data_ptr(), int(n_jobs), int(max_W), int(max_pieces), int(batch_len),

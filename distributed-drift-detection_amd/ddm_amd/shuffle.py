@@ -17,9 +17,14 @@ import functools
 import numpy as np
 import torch
 
+from . import kernels
 from ._capi import check, lib
 
 SUB, CHUNK = 128, 8192
+# Segment length of the parallel MT19937 generation: the stream of a partition is cut at
+# draws D_0 = 0, D_s = (624 - pos0) + s * JUMP, and segment s >= 1 starts from the state
+# T^(s * JUMP)(key0) (ddm_mt_jump), so all segments of a piece are generated at once.
+JUMP = 1 << 20
 
 
 @functools.lru_cache(maxsize=None)
@@ -126,6 +131,10 @@ class GpuShuffle:
         self.waited = 0          # chunks the consuming stream has waited for
         self.init_key = None
         self.init_pos = 624
+        self.seg = None
+        self.jump_scratch = None
+        self.n_seg = self.jumped = 0
+        self._keep = []          # pinned job tables read by in-flight async copies
 
     def _alloc(self, cap):
         cap = (cap + CHUNK - 1) // CHUNK * CHUNK
@@ -150,8 +159,14 @@ class GpuShuffle:
         self.stream.synchronize()
         self.gen_stream.synchronize()       # nothing of the previous run may still read R
         self.tab_stream.synchronize()
+        self.n_seg = self._segments_for(self.cap)
+        if getattr(self, "seg", None) is None or self.seg.shape[0] < self.n_seg:
+            self.seg = torch.zeros((self.n_seg, 640), dtype=torch.int32, device=self.device)
         with torch.cuda.stream(self.gen_stream):
             self.mt.copy_(torch.from_numpy(st.view(np.int32)))
+            self.seg[0, :625].copy_(self.mt)
+        self.jumped = 1                     # segments whose start state exists
+        self._keep = []
         self.gen = self.tab = self.waited = 0
         self.ready = []
 
@@ -172,18 +187,56 @@ class GpuShuffle:
     def chunks_for(upto):
         return (int(upto) + CHUNK - 1) // CHUNK + 1
 
+    def seg_start(self, s):
+        return 0 if s == 0 else (624 - self.init_pos) + s * JUMP
+
+    def _segments_for(self, draws):
+        return max(1, (int(draws) - (624 - self.init_pos)) // JUMP + 1)
+
+    def _jump_to(self, n_seg):
+        """Start states of segments [jumped, n_seg) on gen_stream (ddm_mt_jump, one launch)."""
+        if n_seg <= self.jumped:
+            return
+        if n_seg > self.seg.shape[0]:
+            torch.cuda.synchronize(self.device)
+            seg = torch.zeros((2 * n_seg, 640), dtype=torch.int32, device=self.device)
+            seg[:self.seg.shape[0]].copy_(self.seg)
+            self.seg = seg
+        nj = n_seg - self.jumped
+        if self.jump_scratch is None or self.jump_scratch.shape[0] < nj:
+            torch.cuda.synchronize(self.device)
+            self.jump_scratch = torch.empty((nj, kernels.JUMP_SCRATCH_WORDS), dtype=torch.int32, device=self.device)
+        polys = kernels.mt_jump_polys(JUMP, n_seg - 1, self.device)
+        tab = kernels.PinnedTable(kernels.JUMP_DTYPE, nj, self.device)
+        for k, s in enumerate(range(self.jumped, n_seg)):
+            tab.rec[k] = (self.mt.data_ptr(), polys[s - 1].data_ptr(), self.seg[s].data_ptr(),
+                          self.jump_scratch[k].data_ptr())
+        kernels.mt_jump(tab, nj, self.gen_stream)
+        self._keep.append(tab)
+        self.jumped = n_seg
+
     def gen_request(self, upto):
         """Grow R to cover draws [0, upto) plus one chunk; returns the (state, R, n) generate
-        job still to launch on gen_stream (or None) and the chunk count the tables must reach."""
+        jobs still to launch on gen_stream (one per segment the new draws touch; every
+        segment's state slot continues where its previous piece stopped) and the chunk count
+        the tables must reach."""
         need_chunks = self.chunks_for(upto)
         target = need_chunks * CHUNK
         if target > self.cap:
             self._alloc(max(target, int(self.cap * 1.5)))
-        req = None
+        reqs = []
         if target > self.gen:
-            req = (self.mt.data_ptr(), self.R.data_ptr() + 4 * self.gen, target - self.gen)
+            s_last = self._segments_for(target - 1) - 1
+            if s_last >= 1:                 # every segment of the expected stream at once
+                self._jump_to(max(s_last + 1, self.n_seg))
+            s = self._segments_for(self.gen) - 1 if self.gen else 0
+            while s <= s_last:
+                lo, hi = max(self.gen, self.seg_start(s)), min(target, self.seg_start(s + 1))
+                if lo < hi:
+                    reqs.append((self.seg[s].data_ptr(), self.R.data_ptr() + 4 * lo, hi - lo))
+                s += 1
             self.gen = target
-        return req, need_chunks
+        return reqs, need_chunks
 
     def tables_to(self, need_chunks):
         """Tabulate up to need_chunks on tab_stream (ordered after the words they read: the
@@ -216,9 +269,13 @@ class GpuShuffle:
         """Generate R and tabulate chunks so that draws [0, upto) are covered and visible to
         the consuming stream."""
         if self.chunks_for(upto) > self.tab:
-            req, need_chunks = self.gen_request(upto)
-            if req is not None:
-                check(lib.ddm_shuffle_generate(req[0], req[1], req[2], self._gp()), "ddm_shuffle_generate")
+            reqs, need_chunks = self.gen_request(upto)
+            if reqs:
+                table = kernels.PinnedTable(kernels.GEN_DTYPE, len(reqs), self.device)
+                for k, r in enumerate(reqs):
+                    table.rec[k] = r
+                kernels.shuffle_generate_batch(table, len(reqs), self.gen_stream)
+                self._keep.append(table)
             if self.tab_stream is not self.gen_stream:
                 g = torch.cuda.Event()
                 g.record(self.gen_stream)

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 8
+#define DDM_AMD_ABI_VERSION 9
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -313,6 +313,25 @@ typedef struct ddm_shuffle_job {
 } ddm_shuffle_job;
 
 int ddm_shuffle_generate_batch(const ddm_gen_job* jobs_dev, int32_t n_jobs, ddm_stream_t stream);
+
+/* MT19937 jump-ahead, so one partition's stream is generated in parallel segments.
+ * A reduced GF(2) polynomial is DDM_MT_POLY_WORDS uint64 words, bit i = coefficient of x^i.
+ * ddm_mt_charpoly (host): the characteristic polynomial phi of MT19937's transition
+ *   (degree 19937, DDM_MT_POLY_WORDS + 1 words; Berlekamp-Massey, computed once).
+ * ddm_mt_jump_polys (host): out[k] = x^((k+1)*jump) mod phi for k < n (cached per jump).
+ * ddm_mt_jump (device): per job, out[0..623] = the MT19937 state (numpy key layout,
+ *   pos 624) T^e(key) for the polynomial x^e mod phi in poly, and out[624] = 624.  The
+ *   lower 31 bits of out[0] are not part of the state (never read by the generator).
+ *   scratch: DDM_MT_JUMP_SCRATCH_WORDS device words per job.
+ *   Replaces nothing in the reference: the streams are those of DDM_Process.py:187,190,102. */
+#define DDM_MT_POLY_WORDS 312
+#define DDM_MT_JUMP_SCRATCH_WORDS 21216
+typedef struct ddm_jump_job {
+    const uint32_t* key; const uint64_t* poly; uint32_t* out; uint32_t* scratch;
+} ddm_jump_job;
+int ddm_mt_charpoly(uint64_t* out);
+int ddm_mt_jump_polys(int64_t jump, int32_t n, uint64_t* out);
+int ddm_mt_jump(const ddm_jump_job* jobs_dev, int32_t n_jobs, ddm_stream_t stream);
 int ddm_shuffle_window_batch(const ddm_shuffle_job* jobs_dev, int32_t n_jobs, int64_t max_W,
                              int64_t max_pieces, int32_t batch_len, ddm_stream_t stream,
                              ddm_event_t ev_begin, ddm_event_t ev_end);

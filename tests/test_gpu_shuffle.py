@@ -94,3 +94,36 @@ def test_stream_growth():
     sh.window(0, 5000, out)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), host.perms(np.full(5000, 100, np.int32)))
+
+
+@pytest.mark.parametrize("jump", [5000, 1 << 13])
+def test_raw_stream_across_jump_segments(monkeypatch, jump):
+    """Segments after the first start from jumped states (ddm_mt_jump): the whole stream is
+    still numpy's, draw for draw, whatever the start position inside a block."""
+    from ddm_amd import shuffle
+    monkeypatch.setattr(shuffle, "JUMP", jump)
+    sh = _mk(100, cap=400000)
+    for seed, pre in ((21, 0), (22, 5), (23, 623), (24, 624 * 2 + 300)):
+        mt = MTStream.from_seed(seed)
+        mt.skip(pre)
+        sh.reset(mt)
+        got = sh.words(0, 300000).copy()
+        rs = np.random.RandomState(seed)
+        if pre:
+            rs.randint(0, 2**32, pre, dtype=np.uint64)
+        want = rs.randint(0, 2**32, 300000, dtype=np.uint64).astype(np.uint32)
+        assert np.array_equal(got, want), (seed, pre, int(np.argmax(got != want)))
+
+
+def test_raw_stream_default_segments():
+    """The production segment length (2^20 draws): a stream of 2.5M draws spans 3 segments."""
+    sh = _mk(100, cap=3 << 20)
+    mt = MTStream.from_seed(31)
+    mt.skip(77)
+    sh.reset(mt)
+    n = 2_500_000
+    got = sh.words(0, n).copy()
+    rs = np.random.RandomState(31)
+    rs.randint(0, 2**32, 77, dtype=np.uint64)
+    want = rs.randint(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    assert np.array_equal(got, want), int(np.argmax(got != want))
