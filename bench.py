@@ -96,6 +96,15 @@ def cpu_baseline_c3(part, n_rows, seed):
                       f"{dt:.1f} s"}
 
 
+def events_rows(out):
+    """BatchRunner output (rows x [warning pos, change pos]) as the reference's 4 columns."""
+    import numpy as np
+    ev = np.full((len(out), 4), -1, dtype=np.int64)
+    ev[:, 0] = ev[:, 1] = out[:, 0]
+    ev[:, 2] = ev[:, 3] = out[:, 1]
+    return ev
+
+
 def run_c3(args, world, rank, dev, torch, dist):
     import numpy as np
     from ddm_amd import kernels
@@ -120,10 +129,20 @@ def run_c3(args, world, rank, dev, torch, dist):
 
     results = {}
 
+    n_rows = {r * args.parts + p: (n + 99) // 100 - 1 for r in range(world) for p in range(args.parts)}
+
     def step():
         outs = runner.run([MTStream.from_seed(args.seed + gid) for gid, _ in parts])
         for (gid, _), o in zip(parts, outs):
             results[gid] = o
+        if world > 1:
+            # the collect of DDM_Process.py:258: drift/warning positions of every partition
+            # on every rank, one RCCL all_gather of the batches with an event
+            from ddm_amd.dist import gather_events
+            allev = gather_events({gid: events_rows(results[gid]) for gid, _ in parts}, n_rows=n_rows)
+            for gid, _ in parts:
+                if not np.array_equal(allev[gid], events_rows(results[gid])):
+                    raise RuntimeError(f"partition {gid}: gathered events differ")
 
     for _ in range(args.warmup):
         step()
@@ -266,17 +285,24 @@ def main():
     world, rank, local_rank = dist_env()
     import torch
     import torch.distributed as dist
-    dev = torch.device("cuda", local_rank)
+    # DDM_BENCH_BACKEND=gloo with fewer GPUs than ranks rehearses the N>1 path on one box
+    # (ranks share a GPU); the driver's runs use RCCL ("nccl"), one GPU per rank
+    backend = os.environ.get("DDM_BENCH_BACKEND", "nccl")
+    dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     fn = run_c3 if args.workload == "c3" else run_c4
     rows_rank, elapsed, info, extra, roofline, cpu = fn(args, world, rank, dev, torch, dist)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        rdev = dev if backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        r = torch.tensor([rows_rank], dtype=torch.float64, device=dev)
+        r = torch.tensor([rows_rank], dtype=torch.float64, device=rdev)
         dist.all_reduce(r)
         rows_total = float(r.item())
     else:

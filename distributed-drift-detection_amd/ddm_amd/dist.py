@@ -20,26 +20,30 @@ def local_partitions(parts, rank, world):
     return [(d, f) for d, f in parts if d % world == rank]
 
 
-def _records(outputs):
+def _records(outputs, events_only=False):
     recs = []
     for d, ev in sorted(outputs.items()):
         ev = np.asarray(ev, dtype=np.int64).reshape(-1, 4)
-        r = np.empty((len(ev), RECORD), dtype=np.int64)
+        idx = np.nonzero((ev >= 0).any(axis=1))[0] if events_only else np.arange(len(ev))
+        r = np.empty((len(idx), RECORD), dtype=np.int64)
         r[:, 0] = d
-        r[:, 1] = np.arange(len(ev))
-        r[:, 2:] = ev
+        r[:, 1] = idx
+        r[:, 2:] = ev[idx]
         recs.append(r)
     return np.concatenate(recs) if recs else np.empty((0, RECORD), dtype=np.int64)
 
 
-def gather_events(outputs, group=None, device=None):
+def gather_events(outputs, group=None, device=None, n_rows=None):
     """outputs: {device_id: int64 [n_batches-1, 4]} of this rank -> the same dict for ALL
-    partitions of all ranks (on every rank)."""
+    partitions of all ranks (on every rank).  n_rows ({device_id: output rows} of every
+    partition, known to every rank from the stream description): only the batches with an
+    event travel (the drift positions; a few KB instead of every batch row) and the
+    full outputs are rebuilt with -1 elsewhere."""
     world = dist.get_world_size(group)
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
             else torch.device("cpu")
-    recs = torch.from_numpy(_records(outputs)).to(device)
+    recs = torch.from_numpy(_records(outputs, events_only=n_rows is not None)).to(device)
     n = torch.tensor([recs.shape[0]], dtype=torch.int64, device=device)
     counts = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(counts, n, group=group)
@@ -52,8 +56,14 @@ def gather_events(outputs, group=None, device=None):
     allrec = np.concatenate([b[:c].cpu().numpy() for b, c in zip(bufs, counts)]) if cap else \
         np.empty((0, RECORD), dtype=np.int64)
     out = {}
+    if n_rows is not None:
+        for d, n in n_rows.items():
+            out[int(d)] = np.full((int(n), 4), -1, dtype=np.int64)
     for d in np.unique(allrec[:, 0]):
         r = allrec[allrec[:, 0] == d]
         r = r[np.argsort(r[:, 1])]
-        out[int(d)] = r[:, 2:].copy()
+        if n_rows is not None:
+            out[int(d)][r[:, 1]] = r[:, 2:]
+        else:
+            out[int(d)] = r[:, 2:].copy()
     return out

@@ -42,6 +42,11 @@ def _worker(rank, world, port, mult, inst, q):
 
     outs = run_partitions(mine, {d: 1000 + d for d, _ in mine}, devices=[], max_workers=1, fn=oracle_fn)
     allev = ddm_dist.gather_events(outs)
+    n_rows = {d: len(e) for d, _, e in golden_partitions(mult, inst)}
+    compact = ddm_dist.gather_events(outs, n_rows=n_rows)
+    assert sorted(compact) == sorted(allev)
+    for d in allev:
+        assert np.array_equal(compact[d], allev[d]), d
     q.put((rank, {d: v.tolist() for d, v in allev.items()}))
     dist.barrier()
     dist.destroy_process_group()
@@ -71,3 +76,6 @@ def test_records_roundtrip_single_process():
     outs = {3: np.array([[1, 2, -1, -1], [-1, -1, 5, 6]]), 1: np.zeros((0, 4), np.int64)}
     r = _records(outs)
     assert r.shape == (2, RECORD) and (r[:, 0] == 3).all() and list(r[:, 1]) == [0, 1]
+    outs = {2: np.array([[-1, -1, -1, -1], [-1, -1, 5, 6], [-1, -1, -1, -1]])}
+    r = _records(outs, events_only=True)
+    assert r.shape == (1, RECORD) and list(r[0]) == [2, 1, -1, -1, 5, 6]
