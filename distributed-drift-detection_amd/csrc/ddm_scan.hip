@@ -558,10 +558,11 @@ constexpr int kSpecQ = 256;
 __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
     const uint8_t* __restrict__ err, int64_t n_items, int64_t L, int64_t nb, int64_t nbp, ddm_params P,
     int2* __restrict__ ev, uint8_t* __restrict__ flags, const uint8_t* __restrict__ pmap,
-    int64_t items_per_wave, int fill_below, uint32_t* __restrict__ need) {
+    int64_t items_per_wave, int fill_below, int pop_min, uint32_t* __restrict__ need) {
     __shared__ double rcp[kBatchRcp];
     __shared__ uint64_t qm0[kSpecThreads / 64][kSpecQ], qm1[kSpecThreads / 64][kSpecQ];
-    __shared__ uint32_t qitem[kSpecThreads / 64][kSpecQ];
+    __shared__ uint32_t qitem[kSpecThreads / 64][kSpecQ], qsid[kSpecThreads / 64][kSpecQ];
+    __shared__ uint32_t qjl[kSpecThreads / 64][kSpecQ];
     for (int k = threadIdx.x; k < kBatchRcp; k += kSpecThreads) rcp[k] = 1.0 / (double)(k > 0 ? k : 1);
     __syncthreads();
     const int pb = (int)P.per_batch;
@@ -599,8 +600,9 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
     for (;;) {
         const uint64_t idle_m = __ballot(!busy);
         int nidle = __popcll(idle_m);
-        if (qcount > 0 && nidle > 0) {
-            // pop: idle lanes take queued batches in lane order (LDS only)
+        if (qcount > 0 && (nidle >= pop_min || nidle == 64 || (nidle > 0 && cursor >= wend))) {
+            // pop: idle lanes take queued batches in lane order (LDS only; the queue entry
+            // carries the batch's stream and index, so no division here)
             const int take = min(nidle, qcount);
             if (!busy) {
                 const int rank = __popcll(idle_m & below);
@@ -609,7 +611,12 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
                     m0 = qm0[wv][q];
                     m1 = qm1[wv][q];
                     item = wstart + qitem[wv][q];
-                    locate(item);
+                    sid = qsid[wv][q];
+                    const uint32_t jl = qjl[wv][q];
+                    const int64_t j = jl >> 8;
+                    blen = (int)(jl & 0xffu);
+                    bstart = sid * L + j * pb;
+                    fpos = sid * nbp + j;
                     busy = true;
                     i = 0;
                     wpos = -1;
@@ -628,6 +635,7 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
             // Trivial batches are resolved here; the others go to the queue.
             bool exact = false;
             uint64_t a0 = 0, a1 = 0;
+            uint32_t e_sid = 0, e_jl = 0;
             const int64_t it = cursor + lane;
             if (it < wend) {
                 const int64_t keep_item = item, keep_b = bstart, keep_f = fpos, keep_s = sid;
@@ -648,6 +656,8 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
                     }
                 } else {
                     exact = true;
+                    e_sid = (uint32_t)sid;
+                    e_jl = (uint32_t)(((fpos - sid * nbp) << 8) | (int64_t)blen);
                 }
                 item = keep_item;
                 bstart = keep_b;
@@ -661,6 +671,8 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
                 qm0[wv][q] = a0;
                 qm1[wv][q] = a1;
                 qitem[wv][q] = (uint32_t)(it - wstart);
+                qsid[wv][q] = e_sid;
+                qjl[wv][q] = e_jl;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -920,6 +932,10 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
         const char* e = getenv("DDM_SCAN_FILL");
         return std::max(1, std::min(kSpecQ - 64, e ? atoi(e) : 64));
     }();
+    static const int pop_min = [] {
+        const char* e = getenv("DDM_SCAN_POP");
+        return std::max(1, std::min(64, e ? atoi(e) : 16));
+    }();
     static const int64_t waves_max = [] {
         const char* e = getenv("DDM_SCAN_WAVES");
         return e ? atoll(e) : 256 * 4 * 4;
@@ -952,7 +968,7 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
         const int64_t blocks = ddm::ceil_div(ddm::ceil_div(n_items, per_wave), kSpecThreads / 64);
         hipLaunchKernelGGL(k_scan_batches_spec, dim3((unsigned)blocks), dim3(kSpecThreads), 0, s, err, n_items,
                            stream_len, nb, nbp, *prm, reinterpret_cast<int2*>(ev_out), sc.flags, perm_map, per_wave,
-                           refill, sc.need);
+                           refill, pop_min, sc.need);
         if (int rc = ddm::launch_status("ddm_scan_batches")) return rc;
     }
     hipLaunchKernelGGL(k_scan_batches_list, dim3((unsigned)ddm::ceil_div(n_streams, 256)), dim3(256), 0, s, n_streams,
