@@ -511,6 +511,40 @@ __device__ __forceinline__ int small_add(SmallDet& d, int x, int min_inst, doubl
     return ps > d.pmin + wl * d.smin ? 1 : 0;
 }
 
+// Prefix table: a fresh detector's first kPre rows depend only on their kPre error bits,
+// so the spec kernel looks them up instead of stepping them.  Entry m (bit t = row t is
+// an error) holds the first warning row and the change row inside the prefix (-1 = none)
+// and, without a change, the detector after row kPre - 1 (p, p_min, s_min, psmin; n =
+// kPre + 1).  It is built with small_add itself and the same reciprocal table, so a
+// looked-up prefix is the stepped one bit for bit.
+constexpr int kPre = 16;
+constexpr int kPreN = 1 << kPre;
+
+__global__ __launch_bounds__(256) void k_scan_prefix_table(ddm_params P, double4* __restrict__ pst,
+                                                           int2* __restrict__ pinfo) {
+    __shared__ double rcp[kBatchRcp];
+    for (int k = threadIdx.x; k < kBatchRcp; k += 256) rcp[k] = 1.0 / (double)(k > 0 ? k : 1);
+    __syncthreads();
+    const int m = blockIdx.x * 256 + threadIdx.x;
+    if (m >= kPreN) return;
+    SmallDet d;
+    d.p = 1.0;
+    d.s = 0.0;
+    d.pmin = d.smin = d.psmin = __builtin_huge_val();
+    d.n = 1;
+    int wpos = -1, cpos = -1;
+    for (int i = 0; i < kPre; ++i) {
+        const int r = small_add(d, (m >> i) & 1, P.min_num_instances, P.warning_level, P.out_control_level, rcp);
+        if (r == 1 && wpos < 0) wpos = i;
+        if (r == 2) {
+            cpos = i;
+            break;
+        }
+    }
+    pinfo[m] = make_int2(wpos, cpos);
+    pst[m] = make_double4(d.p, d.pmin, d.smin, d.psmin);
+}
+
 __device__ __forceinline__ bool state_fresh(const ddm_state& st) {
     return st.in_concept_change || (st.sample_count == 1 && st.miss_prob == 1.0 && st.miss_std == 0.0 &&
                                     st.miss_prob_sd_min == __builtin_huge_val() &&
@@ -558,7 +592,8 @@ constexpr int kSpecQ = 256;
 __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
     const uint8_t* __restrict__ err, int64_t n_items, int64_t L, int64_t nb, int64_t nbp, ddm_params P,
     int2* __restrict__ ev, uint8_t* __restrict__ flags, const uint8_t* __restrict__ pmap,
-    int64_t items_per_wave, int fill_below, int pop_min, uint32_t* __restrict__ need) {
+    int64_t items_per_wave, int fill_below, int pop_min, uint32_t* __restrict__ need,
+    const double4* __restrict__ pst, const int2* __restrict__ pinfo) {
     __shared__ double rcp[kBatchRcp];
     __shared__ uint64_t qm0[kSpecThreads / 64][kSpecQ], qm1[kSpecThreads / 64][kSpecQ];
     __shared__ uint32_t qitem[kSpecThreads / 64][kSpecQ], qsid[kSpecThreads / 64][kSpecQ];
@@ -596,6 +631,13 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
         fpos = s * nbp + j;
         blen = (int)min((int64_t)pb, L - j * pb);
     };
+    auto finish = [&](bool chg, int wp, int c) {    // the batch's result (c: change row)
+        const int w = wp < 0 ? -1 : (pmap ? (int)pmap[bstart + wp] : wp);
+        const int cp = chg ? (pmap ? (int)pmap[bstart + c] : c) : -1;
+        ev[item] = make_int2(w, cp);
+        flags[fpos] = (uint8_t)((chg ? 1 : 0) | ((chg || wp >= 0) ? 2 : 0));
+        if (!chg) need[sid] = 1u;
+    };
 
     for (;;) {
         const uint64_t idle_m = __ballot(!busy);
@@ -624,6 +666,24 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
                     d.s = 0.0;
                     d.pmin = d.smin = d.psmin = __builtin_huge_val();
                     d.n = 1;
+                    if (pinfo && blen >= kPre) {
+                        // the first kPre rows from the prefix table
+                        const uint32_t ix = (uint32_t)(m0 & (uint64_t)(kPreN - 1));
+                        const int2 inf = pinfo[ix];
+                        if (inf.y >= 0 || blen == kPre) {
+                            finish(inf.y >= 0, inf.x, inf.y);
+                            busy = false;
+                        } else {
+                            const double4 q = pst[ix];
+                            d.p = q.x;
+                            d.pmin = q.y;
+                            d.smin = q.z;
+                            d.psmin = q.w;
+                            d.n = kPre + 1;
+                            i = kPre;
+                            wpos = inf.x;
+                        }
+                    }
                 }
             }
             qhead = (qhead + take) & (kSpecQ - 1);
@@ -691,12 +751,7 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
             if (r == 1 && wpos < 0) wpos = i;
             ++i;
             if (r == 2 || i >= blen) {
-                const bool chg = r == 2;
-                const int w = wpos < 0 ? -1 : (pmap ? (int)pmap[bstart + wpos] : wpos);
-                const int cp = chg ? (pmap ? (int)pmap[bstart + i - 1] : i - 1) : -1;
-                ev[item] = make_int2(w, cp);
-                flags[fpos] = (uint8_t)((chg ? 1 : 0) | ((chg || wpos >= 0) ? 2 : 0));
-                if (!chg) need[sid] = 1u;
+                finish(r == 2, wpos, i - 1);
                 busy = false;
             }
         }
@@ -895,6 +950,8 @@ struct BatchScratch {
     uint32_t* need;     // [n_streams]
     int32_t* list;      // [n_streams]
     uint8_t* flags;     // [n_streams * nbp], 64-byte aligned rows
+    double4* pst;       // [kPreN] prefix table (k_scan_prefix_table)
+    int2* pinfo;        // [kPreN]
     int64_t bytes;
 };
 
@@ -902,9 +959,12 @@ BatchScratch batch_scratch(void* base, int64_t n_streams, int64_t nb) {
     const auto up = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
     const int64_t nbp = ddm::ceil_div(nb, 64) * 64;
     const int64_t o_need = 256, o_list = o_need + up(4 * n_streams), o_flags = o_list + up(4 * n_streams);
+    const int64_t o_pst = o_flags + up(n_streams * nbp), o_pinfo = o_pst + 32 * (int64_t)kPreN;
     uint8_t* b = static_cast<uint8_t*>(base);
-    return {reinterpret_cast<uint32_t*>(b), reinterpret_cast<uint32_t*>(b + o_need),
-            reinterpret_cast<int32_t*>(b + o_list), b + o_flags, o_flags + up(n_streams * nbp)};
+    return {reinterpret_cast<uint32_t*>(b),      reinterpret_cast<uint32_t*>(b + o_need),
+            reinterpret_cast<int32_t*>(b + o_list), b + o_flags,
+            reinterpret_cast<double4*>(b + o_pst), reinterpret_cast<int2*>(b + o_pinfo),
+            o_pinfo + 8 * (int64_t)kPreN};
 }
 }  // namespace
 
@@ -948,6 +1008,10 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
         const char* e = getenv("DDM_FIX_REFILL");
         return e ? atoi(e) : 16;
     }();
+    static const bool use_pre = [] {
+        const char* e = getenv("DDM_SCAN_PRE");
+        return e ? atoi(e) != 0 : true;
+    }();
     static const int fix_open = [] {
         const char* e = getenv("DDM_FIX_OPEN");
         return e ? atoi(e) : 16;
@@ -966,9 +1030,14 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
             return DDM_E_ARG;
         }
         const int64_t blocks = ddm::ceil_div(ddm::ceil_div(n_items, per_wave), kSpecThreads / 64);
+        const bool pre = use_pre && prm->per_batch >= kPre;
+        if (pre) {
+            hipLaunchKernelGGL(k_scan_prefix_table, dim3(kPreN / 256), dim3(256), 0, s, *prm, sc.pst, sc.pinfo);
+            if (int rc = ddm::launch_status("ddm_scan_batches/prefix")) return rc;
+        }
         hipLaunchKernelGGL(k_scan_batches_spec, dim3((unsigned)blocks), dim3(kSpecThreads), 0, s, err, n_items,
                            stream_len, nb, nbp, *prm, reinterpret_cast<int2*>(ev_out), sc.flags, perm_map, per_wave,
-                           refill, pop_min, sc.need);
+                           refill, pop_min, sc.need, pre ? sc.pst : nullptr, pre ? sc.pinfo : nullptr);
         if (int rc = ddm::launch_status("ddm_scan_batches")) return rc;
     }
     hipLaunchKernelGGL(k_scan_batches_list, dim3((unsigned)ddm::ceil_div(n_streams, 256)), dim3(256), 0, s, n_streams,

@@ -447,6 +447,27 @@ __global__ __launch_bounds__(kCfThreads) void k_cforest_predict_batch(const Seg*
     cf_segment<kVR, kRows>(sg, gb - sg.block0, sg.nblocks, pb, smem);
 }
 
+// The same kernel with the segment table passed by value in the kernel arguments (up to
+// kArgSegs segments: a C3 GPU runs 8 partitions), so an epoch's predict needs no
+// host->device table copy ahead of it on the stream.  The table lives in the kernarg
+// segment; the lookup and the copy of the selected segment are scalar loads.
+constexpr int kArgSegs = 8;
+struct SegTab {
+    Seg s[kArgSegs];
+};
+
+template <int kVR, int kRows>
+__global__ __launch_bounds__(kCfThreads) void k_cforest_predict_arg(const SegTab tab, int n_segs, int64_t block_base,
+                                                                    int pb) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int64_t gb = block_base + blockIdx.x;
+    int s = 0;
+    while (s < n_segs && !(tab.s[s].block0 <= gb && gb < tab.s[s].block0 + tab.s[s].nblocks)) ++s;
+    if (s == n_segs) return;
+    const Seg sg = tab.s[s];
+    cf_segment<kVR, kRows>(sg, gb - sg.block0, sg.nblocks, pb, smem);
+}
+
 using cf_fn = void (*)(Seg, int);
 using cf_batch_fn = void (*)(const Seg*, int, int64_t, int);
 
@@ -463,6 +484,13 @@ cf_batch_fn pick_cf_batch_r(int vk) {
                    : vk == 1 ? k_cforest_predict_batch<2, kRows> : k_cforest_predict_batch<4, kRows>;
 }
 cf_batch_fn pick_cf_batch(int vk, int rows) { return rows == 1 ? pick_cf_batch_r<1>(vk) : pick_cf_batch_r<2>(vk); }
+using cf_arg_fn = void (*)(SegTab, int, int64_t, int);
+template <int kRows>
+cf_arg_fn pick_cf_arg_r(int vk) {
+    return vk == 0 ? k_cforest_predict_arg<1, kRows>
+                   : vk == 1 ? k_cforest_predict_arg<2, kRows> : k_cforest_predict_arg<4, kRows>;
+}
+cf_arg_fn pick_cf_arg(int vk, int rows) { return rows == 1 ? pick_cf_arg_r<1>(vk) : pick_cf_arg_r<2>(vk); }
 
 // LDS of the compiled path (cf_segment): column pointers + rank tables + labels +
 // classes + err + leaf classes + row slots [kRows][slots rounded to 8][512] when the
@@ -635,6 +663,23 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
         }
     }
     vbase[kNV] = b0;
+    bool all_cf = true;
+    for (int i = 0; i < n_segs; ++i) all_cf = all_cf && variant[i] >= 16;
+    if (all_cf && n_segs <= kArgSegs) {
+        // compiled forests only: the table rides in the kernel arguments (no table copy)
+        SegTab tab{};
+        for (int i = 0; i < n_segs; ++i) tab.s[i] = hs[i];
+        for (int v = 16; v < kNV; ++v) {
+            const int64_t nb = vbase[v + 1] - vbase[v];
+            if (nb == 0) continue;
+            hipLaunchKernelGGL(pick_cf_arg((v - 16) % 3, 1 + (v - 16) / 3), dim3((unsigned)nb), dim3(kCfThreads), vlds[v],
+                               s, tab, n_segs, vbase[v], (int)per_batch);
+            if (int rc = ddm::launch_status("ddm_forest_predict_batch")) return rc;
+        }
+        if (ev_end)
+            if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
+        return 0;
+    }
     if (b0 > 0) {
         if (int rc = ddm::hip_status(hipMemcpyAsync(segs_dev, hs, sizeof(Seg) * n_segs, hipMemcpyHostToDevice, s),
                                      "predict_batch table"))

@@ -196,6 +196,8 @@ class BatchRunner:
         self.t_pred = kernels.LaunchTimer() if timing else None
         self.t_scan = kernels.LaunchTimer() if timing else None
         self.t_shuf = kernels.LaunchTimer() if timing else None
+        # when a list: every predict launch's segment table is kept (replay_predict)
+        self.predict_log = None
         self.params = kernels.params_struct(self.s.min_num_instances, pb, self.s.warning_level,
                                             self.s.out_control_level)
         n = len(self.parts)
@@ -509,6 +511,29 @@ class BatchRunner:
         if upload:
             self.jobs.upload(len(live), self.stream)
 
+    def replay_predict(self, repeats=1):
+        """Launch the logged predict segment tables again back to back on the epoch stream
+        (same inputs, same shapes), HIP events on that stream around all of them.  With the
+        stream saturated the events time the kernels alone; in the epoch loop they also
+        time the stream's idle gap before each launch.  Returns (ms per launch, launches)."""
+        log = self.predict_log or []
+        if not log:
+            return 0.0, 0
+        cap = max(k for _, k, _ in log)
+        tabs = [kernels.PinnedTable(kernels.SEG_DTYPE, cap, self.device) for _ in log]
+        for t, (rec, k, _) in zip(tabs, log):
+            t.rec[:k] = rec
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(self.device)
+        e0.record(self.stream)
+        for _ in range(repeats):
+            for t, (_, k, pb) in zip(tabs, log):
+                kernels.forest_predict_batch(t, k, pb, self.stream)
+        e1.record(self.stream)
+        e1.synchronize()
+        n = repeats * len(log)
+        return e0.elapsed_time(e1) / n, n
+
     def run(self, rngs):
         """Returns, per partition, int64 [n_batches-1, 2]: partition rows of (first warning,
         change) per batch 1.. (-1 = none).  Consumes each `rngs[p]` (an MTStream, advanced
@@ -646,6 +671,8 @@ class BatchRunner:
             self._refit_fit(work)
             self._segment_table(live)
         kernels.forest_predict_batch(self.segs, len(live), pb, stream, self.t_pred)
+        if self.predict_log is not None:
+            self.predict_log.append((self.segs.rec[:len(live)].copy(), len(live), pb))
         kernels.scan_streams_raw(self.err_all.data_ptr(), base + self.o_off, n, self.params, base + self.o_state,
                                  base + self.o_bbase, self.ev_total, self.ev_d.data_ptr(), base + self.o_first,
                                  base + self.o_stop, base + self.o_nev, 0, None, stream, self.t_scan,

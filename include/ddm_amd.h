@@ -179,7 +179,9 @@ int ddm_forest_predict(const float* X, int64_t ld, int32_t n_features, const int
 /* Batched predict: one segment per partition window (the same work as one
  * ddm_forest_predict call each), all in one launch per kernel variant.  segs_host must
  * stay valid (e.g. pinned) until the stream has consumed the table copy; block0/nblocks
- * are filled in by the call; segs_dev (device) receives the table.  first_err of every
+ * are filled in by the call; segs_dev (device) receives the table (when every segment
+ * has a compiled forest and n_segs <= 8 the table is passed in the kernel arguments
+ * instead and segs_dev is not written).  first_err of every
  * segment (if non-NULL) is reset by the call. */
 typedef struct ddm_predict_segment {
     const float* X; int64_t ld; const int32_t* y; const uint8_t* perm; uint8_t* err;

@@ -133,6 +133,6 @@ def test_scan_batches_rejects_long_batches():
     e = torch.zeros(512, dtype=torch.uint8, device=dev)
     st = torch.from_numpy(kernels.fresh_states(1).view(np.uint8)).to(dev)
     ev = torch.empty((2, 2), dtype=torch.int32, device=dev)
-    fl = torch.empty(4096, dtype=torch.uint8, device=dev)
+    fl = torch.empty(kernels.scan_batches_scratch_size(1, 258, 129), dtype=torch.uint8, device=dev)
     with pytest.raises(DdmError):
         kernels.scan_batches(e, 1, 258, kernels.params_struct(3, 129), st, ev, fl)
