@@ -218,13 +218,33 @@ __device__ __forceinline__ double div_rn(double a, double n, double r) {
     return __builtin_fma(e, r, q0);
 }
 
+// sqrt for the DDM's q = p(1-p)/n: the operation sequence of the compiler's correctly
+// rounded f64 sqrt (rsq seed, Goldschmidt step, two Newton corrections) without its
+// denormal-range scaling and its inf check.  The scaling is the identity for
+// q >= 2^-767 and q is either 0 or far above that (p and 1-p are 0 or >= 1/n with
+// n < 2^63, so q >= 2^-190); q == 0 gives 0 as sqrt does.  Bit-identical to sqrt(q) on
+// that domain (the scan parity tests compare with the C oracle's libm sqrt).
+__device__ __forceinline__ double sqrt_q(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    double h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    return x == 0.0 ? x : g;
+}
+
 __device__ __forceinline__ void det_add_fast(Det& d, int x, int min_inst, double wl, double cl,
                                              const double* __restrict__ rcp) {
     if (d.chg) det_reset(d);
     const double n = (double)d.n;
     const double r = d.n < kRcpN ? rcp[d.n] : 1.0 / n;
     const double p = d.p + div_rn((double)x - d.p, n, r);
-    const double s = sqrt(div_rn(p * (1.0 - p), n, r));
+    const double s = sqrt_q(div_rn(p * (1.0 - p), n, r));
     d.p = p;
     d.s = s;
     d.n += 1;
@@ -496,7 +516,7 @@ __device__ __forceinline__ int small_add(SmallDet& d, int x, int min_inst, doubl
     const double n = (double)d.n;
     const double r = rcp[d.n];
     const double p = d.p + div_rn((double)x - d.p, n, r);
-    const double s = sqrt(div_rn(p * (1.0 - p), n, r));
+    const double s = sqrt_q(div_rn(p * (1.0 - p), n, r));
     d.p = p;
     d.s = s;
     d.n += 1;
