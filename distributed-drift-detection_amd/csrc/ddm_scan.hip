@@ -464,15 +464,17 @@ __device__ __forceinline__ uint32_t nz16(uint4 v) {
 // (m0, m1) = row bstart + t is an error.  All nine 16-byte loads are issued before any
 // is used (chunk addresses past the batch are clamped to its last chunk, their bits
 // dropped).
-__device__ __forceinline__ void batch_mask(const uint8_t* __restrict__ err, int64_t bstart, int blen,
-                                           uint64_t& m0, uint64_t& m1) {
+__device__ __forceinline__ void batch_load(const uint8_t* __restrict__ err, int64_t bstart, int blen, uint4 (&v)[9]) {
     const int64_t c0 = bstart & ~(int64_t)15;
     const int64_t clast = (bstart + blen - 1) & ~(int64_t)15;
-    const int off = (int)(bstart & 15);
-    const int nch = (off + blen + 15) >> 4;
-    uint4 v[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) v[k] = *reinterpret_cast<const uint4*>(err + min(c0 + 16 * k, clast));
+}
+
+__device__ __forceinline__ void batch_mask_of(const uint4 (&v)[9], int64_t bstart, int blen, uint64_t& m0,
+                                              uint64_t& m1) {
+    const int off = (int)(bstart & 15);
+    const int nch = (off + blen + 15) >> 4;
     uint32_t c[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) c[k] = k < nch ? nz16(v[k]) : 0u;
@@ -487,6 +489,13 @@ __device__ __forceinline__ void batch_mask(const uint8_t* __restrict__ err, int6
     } else if (blen < 128) {
         m1 &= (1ull << (blen - 64)) - 1;
     }
+}
+
+__device__ __forceinline__ void batch_mask(const uint8_t* __restrict__ err, int64_t bstart, int blen,
+                                           uint64_t& m0, uint64_t& m1) {
+    uint4 v[9];
+    batch_load(err, bstart, blen, v);
+    batch_mask_of(v, bstart, blen, m0, m1);
 }
 
 __device__ __forceinline__ int mask_bit(uint64_t m0, uint64_t m1, int i) {
@@ -563,6 +572,22 @@ __global__ __launch_bounds__(256) void k_scan_prefix_table(ddm_params P, double4
     }
     pinfo[m] = make_int2(wpos, cpos);
     pst[m] = make_double4(d.p, d.pmin, d.smin, d.psmin);
+}
+
+// The tests of one row whose p and s are already computed (small_add's second half).
+__device__ __forceinline__ int small_test(SmallDet& d, double p, double s, int min_inst, double wl, double cl) {
+    d.p = p;
+    d.s = s;
+    d.n += 1;
+    if (d.n < min_inst) return 0;
+    const double ps = p + s;
+    if (ps <= d.psmin) {
+        d.pmin = p;
+        d.smin = s;
+        d.psmin = ps;
+    }
+    if (ps > d.pmin + cl * d.smin) return 2;
+    return ps > d.pmin + wl * d.smin ? 1 : 0;
 }
 
 __device__ __forceinline__ bool state_fresh(const ddm_state& st) {
@@ -658,6 +683,10 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
     int64_t cursor = wstart;
     const double inv_nb = 1.0 / (double)nb;
     int qhead = 0, qcount = 0;                      // wave-uniform ring state
+    // the next fill's batch bytes, loaded right after the current fill so that their
+    // latency hides behind the exact rows in between
+    uint4 nv[9];
+    bool nv_ok = false;
 
     bool busy = false;
     int64_t item = 0, bstart = 0, fpos = 0, sid = 0;
@@ -747,7 +776,8 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
                 const int64_t keep_item = item, keep_b = bstart, keep_f = fpos, keep_s = sid;
                 const int keep_len = blen;
                 locate(it);
-                batch_mask(err, bstart, blen, a0, a1);
+                if (!nv_ok) batch_load(err, bstart, blen, nv);
+                batch_mask_of(nv, bstart, blen, a0, a1);
                 if (shortcuts && blen >= 2 && (a0 & 3ull) == 0) {
                     // fresh + two zero rows = trivial state (n = 3); its first error row
                     // is the change (p + s > 0), and zeros raise nothing
@@ -764,6 +794,13 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
                     exact = true;
                     e_sid = (uint32_t)sid;
                     e_jl = (uint32_t)(((fpos - sid * nbp) << 8) | (int64_t)blen);
+                }
+                // prefetch the next fill's item (this lane's, 64 on)
+                nv_ok = false;
+                if (it + 64 < wend) {
+                    locate(it + 64);
+                    batch_load(err, bstart, blen, nv);
+                    nv_ok = true;
                 }
                 item = keep_item;
                 bstart = keep_b;
@@ -792,10 +829,25 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
             continue;
         }
         if (busy) {
-            // one exact row of the lane's batch
-            const int r = small_add(d, mask_bit(m0, m1, i), min_inst, wl, cl, rcp);
+            // two exact rows of the lane's batch.  p and s of row i+1 depend on p_i
+            // alone, so both rows' arithmetic is computed first (two overlapping fp64
+            // chains, the same operations as small_add), then the tests in row order;
+            // row i+1 counts only if row i did not change.
+            const bool two = i + 1 < blen;
+            const int n0 = d.n;
+            const double nd0 = (double)n0, r0 = rcp[n0], nd1 = (double)(n0 + 1), r1 = rcp[n0 + 1];
+            const double p0 = d.p + div_rn((double)mask_bit(m0, m1, i) - d.p, nd0, r0);
+            const double p1 = p0 + div_rn((double)(two ? mask_bit(m0, m1, i + 1) : 0) - p0, nd1, r1);
+            const double s0 = sqrt_q(div_rn(p0 * (1.0 - p0), nd0, r0));
+            const double s1 = sqrt_q(div_rn(p1 * (1.0 - p1), nd1, r1));
+            int r = small_test(d, p0, s0, min_inst, wl, cl);
             if (r == 1 && wpos < 0) wpos = i;
             ++i;
+            if (r != 2 && two) {
+                r = small_test(d, p1, s1, min_inst, wl, cl);
+                if (r == 1 && wpos < 0) wpos = i;
+                ++i;
+            }
             if (r == 2 || i >= blen) {
                 finish(r == 2, wpos, i - 1);
                 if (r != 2 && pend) {
