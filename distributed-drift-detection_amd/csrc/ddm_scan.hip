@@ -659,6 +659,7 @@ __global__ __launch_bounds__(256) void k_scan_batches_list(int64_t n_streams, in
 
 // Per-wave LDS queue of the batches that need exact rows (mask + batch), see below.
 constexpr int kSpecQ = 256;
+constexpr bool kSpecPrefetch = false;   // next fill's bytes ahead (36 VGPRs; measured no gain)
 
 __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
     const uint8_t* __restrict__ err, int64_t n_items, int64_t L, int64_t nb, int64_t nbp, ddm_params P,
@@ -776,8 +777,12 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
                 const int64_t keep_item = item, keep_b = bstart, keep_f = fpos, keep_s = sid;
                 const int keep_len = blen;
                 locate(it);
-                if (!nv_ok) batch_load(err, bstart, blen, nv);
-                batch_mask_of(nv, bstart, blen, a0, a1);
+                if (kSpecPrefetch) {
+                    if (!nv_ok) batch_load(err, bstart, blen, nv);
+                    batch_mask_of(nv, bstart, blen, a0, a1);
+                } else {
+                    batch_mask(err, bstart, blen, a0, a1);
+                }
                 if (shortcuts && blen >= 2 && (a0 & 3ull) == 0) {
                     // fresh + two zero rows = trivial state (n = 3); its first error row
                     // is the change (p + s > 0), and zeros raise nothing
@@ -797,7 +802,7 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
                 }
                 // prefetch the next fill's item (this lane's, 64 on)
                 nv_ok = false;
-                if (it + 64 < wend) {
+                if (kSpecPrefetch && it + 64 < wend) {
                     locate(it + 64);
                     batch_load(err, bstart, blen, nv);
                     nv_ok = true;
