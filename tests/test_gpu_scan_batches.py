@@ -59,7 +59,8 @@ def mixed_streams(rs, n, L):
 
 
 @pytest.mark.parametrize("per_batch,L", [(100, 4096), (100, 1000), (1, 37), (3, 301), (64, 640), (127, 1000),
-                                         (128, 1031), (100, 1), (100, 100), (100, 199)])
+                                         (128, 1031), (100, 1), (100, 100), (100, 199), (15, 300), (16, 400),
+                                         (16, 1000), (17, 340)])
 @pytest.mark.parametrize("min_inst", [3, 5])
 def test_scan_batches_equals_scan_streams(oracle_lib, per_batch, L, min_inst):
     rs = np.random.RandomState(per_batch * 7919 + L + min_inst)
@@ -136,3 +137,20 @@ def test_scan_batches_rejects_long_batches():
     fl = torch.empty(kernels.scan_batches_scratch_size(1, 258, 129), dtype=torch.uint8, device=dev)
     with pytest.raises(DdmError):
         kernels.scan_batches(e, 1, 258, kernels.params_struct(3, 129), st, ev, fl)
+
+
+@pytest.mark.parametrize("per_batch,L", [(100, 100), (16, 16), (16, 32), (40, 80)])
+def test_scan_batches_prefix_table_exhaustive(oracle_lib, per_batch, L):
+    """Every 16-row error prefix (the spec kernel's prefix table, kPre = 16) opens a batch
+    once, followed by random rows, against the C oracle: events and carried states."""
+    rs = np.random.RandomState(per_batch + L)
+    n = 1 << 16
+    err = rs.binomial(1, 0.15, (n, L)).astype(np.uint8)
+    bits = (np.arange(n)[:, None] >> np.arange(16)[None, :]) & 1
+    err[:, :16] = bits
+    err = err.reshape(-1)
+    off = np.arange(n + 1, dtype=np.int64) * L
+    ev, nev, st = gpu_scan_batches(err, n, L, per_batch=per_batch)
+    oev, _, ost, _ = oracle_scan_c(oracle_lib, err, off, per_batch=per_batch, mode=1)
+    assert np.array_equal(ev, oev)
+    np.testing.assert_array_equal(_state_matrix(st), ost)
