@@ -460,6 +460,14 @@ __device__ __forceinline__ uint32_t nz16(uint4 v) {
     return nz4(v.x) | (nz4(v.y) << 4) | (nz4(v.z) << 8) | (nz4(v.w) << 12);
 }
 
+// nz4 for a word whose bytes are 0 or 1 (what predict writes): the multiply moves byte
+// k's bit 0 to bit 21 + k with no two partial products on the same bit (no carries).
+__device__ __forceinline__ uint32_t bin4(uint32_t w) { return ((w * 0x00204081u) >> 21) & 0xfu; }
+
+__device__ __forceinline__ uint32_t bin16(uint4 v) {
+    return bin4(v.x) | (bin4(v.y) << 4) | (bin4(v.z) << 8) | (bin4(v.w) << 12);
+}
+
 // 128-bit nonzero mask of the rows [bstart, bstart + blen), blen in 1..128: bit t of
 // (m0, m1) = row bstart + t is an error.  All nine 16-byte loads are issued before any
 // is used (chunk addresses past the batch are clamped to its last chunk, their bits
@@ -476,8 +484,16 @@ __device__ __forceinline__ void batch_mask_of(const uint4 (&v)[9], int64_t bstar
     const int off = (int)(bstart & 15);
     const int nch = (off + blen + 15) >> 4;
     uint32_t c[9];
+    uint32_t any = 0;
 #pragma unroll
-    for (int k = 0; k < 9; ++k) c[k] = k < nch ? nz16(v[k]) : 0u;
+    for (int k = 0; k < 9; ++k) any |= v[k].x | v[k].y | v[k].z | v[k].w;
+    if ((any & 0xfefefefeu) == 0u) {            // 0/1 bytes only: the cheap fold
+#pragma unroll
+        for (int k = 0; k < 9; ++k) c[k] = k < nch ? bin16(v[k]) : 0u;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) c[k] = k < nch ? nz16(v[k]) : 0u;
+    }
     const uint64_t a0 = (uint64_t)c[0] | ((uint64_t)c[1] << 16) | ((uint64_t)c[2] << 32) | ((uint64_t)c[3] << 48);
     const uint64_t a1 = (uint64_t)c[4] | ((uint64_t)c[5] << 16) | ((uint64_t)c[6] << 32) | ((uint64_t)c[7] << 48);
     const uint64_t a2 = c[8];
