@@ -677,6 +677,7 @@ __global__ __launch_bounds__(256) void k_scan_batches_list(int64_t n_streams, in
 constexpr int kSpecQ = 256;
 constexpr bool kSpecPrefetch = false;   // next fill's bytes ahead (36 VGPRs; measured no gain)
 
+template <bool kPmap>
 __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
     const uint8_t* __restrict__ err, int64_t n_items, int64_t L, int64_t nb, int64_t nbp, ddm_params P,
     int2* __restrict__ ev, uint8_t* __restrict__ flags, const uint8_t* __restrict__ pmap,
@@ -724,8 +725,10 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
         blen = (int)min((int64_t)pb, L - j * pb);
     };
     auto finish = [&](bool chg, int wp, int c) {    // the batch's result (c: change row)
-        const int w = wp < 0 ? -1 : (pmap ? (int)pmap[bstart + wp] : wp);
-        const int cp = chg ? (pmap ? (int)pmap[bstart + c] : c) : -1;
+        // without a perm map no load precedes the stores (a load here made every store
+        // wait for all outstanding memory operations)
+        const int w = wp < 0 ? -1 : (kPmap ? (int)pmap[bstart + wp] : wp);
+        const int cp = chg ? (kPmap ? (int)pmap[bstart + c] : c) : -1;
         ev[item] = make_int2(w, cp);
         flags[fpos] = (uint8_t)((chg ? 1 : 0) | ((chg || wp >= 0) ? 2 : 0));
         if (!chg) need[sid] = 1u;
@@ -760,13 +763,14 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
                     d.n = 1;
                     if (pinfo && blen >= kPre) {
                         // the first kPre rows from the prefix table
+                        // both table loads issued together: one wait per pop
                         const uint32_t ix = (uint32_t)(m0 & (uint64_t)(kPreN - 1));
                         const int2 inf = pinfo[ix];
+                        const double4 q = pst[ix];
                         if (inf.y >= 0 || blen == kPre) {
                             finish(inf.y >= 0, inf.x, inf.y);
                             busy = false;
                         } else {
-                            const double4 q = pst[ix];
                             d.p = q.x;
                             d.pmin = q.y;
                             d.smin = q.z;
@@ -1199,7 +1203,8 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
             hipLaunchKernelGGL(k_scan_prefix_table, dim3(kPreN / 256), dim3(256), 0, s, *prm, sc.pst, sc.pinfo);
             if (int rc = ddm::launch_status("ddm_scan_batches/prefix")) return rc;
         }
-        hipLaunchKernelGGL(k_scan_batches_spec, dim3((unsigned)blocks), dim3(kSpecThreads), 0, s, err, n_items,
+        hipLaunchKernelGGL(perm_map ? k_scan_batches_spec<true> : k_scan_batches_spec<false>, dim3((unsigned)blocks),
+                           dim3(kSpecThreads), 0, s, err, n_items,
                            stream_len, nb, nbp, *prm, reinterpret_cast<int2*>(ev_out), sc.flags, perm_map, per_wave,
                            refill, pop_min, sc.need, pre ? sc.pst : nullptr, pre ? sc.pinfo : nullptr,
                            use_pend ? sc.pend : nullptr);
