@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_gpu_scan_batches.py tests/test_gpu_scan.py tests/test_gpu_predict.py tests/test_gpu_controller.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_round.log 2>&1 || { tail -40 gpurun_out/pytest_round.log; exit 1; }
 tail -2 gpurun_out/pytest_round.log
-for cfg in DDM_X=0 DDM_SCAN_POP=24; do
+for cfg in DDM_X=0 DDM_FIX_OPEN=8 DDM_FIX_OPEN=32 DDM_FIX_REFILL=8 DDM_FIX_REFILL=32 DDM_FIX_BLOCKS=256 DDM_SCAN_FILL=128; do
   env $cfg timeout -k 10 120 python -u bench.py --workload c4 --cpu-baseline 0 --steps 5 > gpurun_out/c4_sweep.json 2> gpurun_out/c4_sweep.err || { tail -20 gpurun_out/c4_sweep.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/c4_sweep.json'));print('$cfg', d['value'], d['roofline']['avg_launch_ms'], d['roofline']['frac'])"
 done
