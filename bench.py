@@ -287,7 +287,7 @@ def run_c4(args, world, rank, dev, torch, dist):
                 "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_from_profile("ddm_scan_batches", S * L),
                 "kernel": "ddm_scan_batches", "alg_bytes_per_row": "1 + 8/100",
                 "avg_launch_ms": avg_ms,
-                "note": "k_scan_batches_spec + k_scan_batches_fix (batch-parallel speculation, per-stream fix-up)"}
+                "note": "one ddm_scan_batches call: k_scan_prefix_table + k_scan_batches_spec (batch-parallel speculation) + k_scan_batches_list + k_scan_batches_fix (per-stream fix-up); HIP events around the call"}
     return rows, elapsed, info, extra, roofline, cpu
 
 
