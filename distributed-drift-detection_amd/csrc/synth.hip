@@ -29,6 +29,31 @@ __global__ __launch_bounds__(256) void k_block_labels(int32_t* __restrict__ y, i
     }
 }
 
+// configs[4] (C5): class blocks whose global boundaries sit at k*period + jitter_k,
+// jitter_k ~ U[-jitter, jitter] (jitter_0 = 0, jitter < period/2), block k of class
+// k % n_classes, and each label flipped to another class with probability flip.  A row's
+// block is found from its own boundary neighbourhood, so any row regenerates alone.
+__device__ __forceinline__ int64_t jit_boundary(uint64_t seed, int64_t k, int64_t period, int64_t jitter) {
+    if (k <= 0 || jitter == 0) return k * period;
+    const int64_t j = (int64_t)(unit(seed, (uint64_t)k, 0xb10c0001ull) * (double)(2 * jitter + 1)) - jitter;
+    return k * period + j;
+}
+
+__global__ __launch_bounds__(256) void k_jitter_labels(int32_t* __restrict__ y, int64_t n, int64_t part,
+                                                       int64_t n_parts, int64_t period, int64_t jitter,
+                                                       int n_classes, double flip, uint64_t seed) {
+    for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
+        const int64_t g = r * n_parts + part;
+        int64_t k = g / period;
+        if (g < jit_boundary(seed, k, period, jitter)) --k;
+        else if (g >= jit_boundary(seed, k + 1, period, jitter)) ++k;
+        int c = (int)(k % n_classes);
+        if (flip > 0.0 && n_classes > 1 && unit(seed ^ 0x7f4a7c15ull, (uint64_t)g, 0xf119ull) < flip)
+            c = (c + 1 + (int)(unit(seed ^ 0x7f4a7c15ull, (uint64_t)g, 0xf11aull) * (n_classes - 1))) % n_classes;
+        y[r] = c;
+    }
+}
+
 // base(c, f) in {0.05, 0.15, ..., 0.95}: for classes c != c' (mod 10) every feature
 // differs by >= 0.1 while the noise stays below 0.05, so classes are separable on
 // every feature.
@@ -79,6 +104,21 @@ extern "C" int ddm_synth_block_labels(int32_t* y, int64_t n_rows, int64_t part, 
     hipLaunchKernelGGL(k_block_labels, dim3((unsigned)blocks), dim3(256), 0, ddm::as_hip(stream), y, n_rows, part,
                        n_parts, block_rows, (int)n_classes);
     return ddm::launch_status("ddm_synth_block_labels");
+}
+
+extern "C" int ddm_synth_jitter_labels(int32_t* y, int64_t n_rows, int64_t part, int64_t n_parts, int64_t period,
+                                       int64_t jitter, int32_t n_classes, double flip, uint64_t seed,
+                                       ddm_stream_t stream) {
+    if (!y || n_rows < 0 || n_parts <= 0 || part < 0 || part >= n_parts || period <= 0 || jitter < 0 ||
+        2 * jitter >= period || n_classes <= 0 || !(flip >= 0.0 && flip <= 1.0)) {
+        ddm::set_error("ddm_synth_jitter_labels: invalid argument");
+        return DDM_E_ARG;
+    }
+    if (n_rows == 0) return 0;
+    const int64_t blocks = std::min<int64_t>(ddm::ceil_div(n_rows, 256), 4096);
+    hipLaunchKernelGGL(k_jitter_labels, dim3((unsigned)blocks), dim3(256), 0, ddm::as_hip(stream), y, n_rows, part,
+                       n_parts, period, jitter, (int)n_classes, flip, seed);
+    return ddm::launch_status("ddm_synth_jitter_labels");
 }
 
 extern "C" int ddm_synth_features(float* X, int64_t ld, int32_t n_features, const int32_t* y, int64_t n_rows,

@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
@@ -82,6 +82,8 @@ SIGNATURES = {
     "ddm_words_perm_seeds": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _vp]),
     "ddm_rf_fit": (ctypes.c_int, [_vp, _i32, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp]),
     "ddm_synth_block_labels": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i32, _vp]),
+    "ddm_synth_jitter_labels": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i32, ctypes.c_double, _u64,
+                                               _vp]),
     "ddm_synth_features": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _i64, _i64, _u64, _f32, _vp]),
     "ddm_synth_bernoulli_streams": (ctypes.c_int, [_vp, _i64, _i64, _u64, _vp]),
 }

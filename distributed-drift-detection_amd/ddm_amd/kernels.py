@@ -220,6 +220,11 @@ def synth_block_labels(y, part, n_parts, block_rows, n_classes, stream=None):
                                      _stream(y, stream)), "ddm_synth_block_labels")
 
 
+def synth_jitter_labels(y, part, n_parts, period, jitter, n_classes, flip, seed, stream=None):
+    check(lib.ddm_synth_jitter_labels(y.data_ptr(), y.numel(), part, n_parts, period, jitter, n_classes,
+                                      float(flip), seed, _stream(y, stream)), "ddm_synth_jitter_labels")
+
+
 def synth_features(X, y, row0, row_stride, seed, noise=0.04, stream=None):
     F, ld = X.shape
     check(lib.ddm_synth_features(X.data_ptr(), ld, F, y.data_ptr(), y.numel(), row0, row_stride, seed,

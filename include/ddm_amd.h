@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 9
+#define DDM_AMD_ABI_VERSION 10
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -451,6 +451,15 @@ int ddm_rf_fit_device(const ddm_dfit_job* jobs_dev, int32_t n_jobs, int32_t max_
  * partition row r is global row g = r*n_parts + part, class (g / block_rows) % n_classes. */
 int ddm_synth_block_labels(int32_t* y, int64_t n_rows, int64_t part, int64_t n_parts,
                            int64_t block_rows, int32_t n_classes, ddm_stream_t stream);
+
+/* configs[4] (C5) labels: global row g = r*n_parts + part lies in block k, whose global
+ * boundaries are k*period + jitter_k (jitter_k ~ U[-jitter, jitter] from a counter hash of
+ * (seed, k), jitter_0 = 0, 2*jitter < period); class k % n_classes, flipped to another
+ * class with probability flip (label noise).  Blocks of 150-300 partition rows over 8
+ * partitions: period 1800, jitter 300 (block lengths 1800 +- 600). */
+int ddm_synth_jitter_labels(int32_t* y, int64_t n_rows, int64_t part, int64_t n_parts, int64_t period,
+                            int64_t jitter, int32_t n_classes, double flip, uint64_t seed,
+                            ddm_stream_t stream);
 
 /* Noise-free separable features for labels y: X[f*ld + r] = base(y[r], f) + noise*u,
  * u ~ U[0,1) from a counter hash of (seed, row0 + r*row_stride, f). */

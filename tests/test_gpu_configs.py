@@ -1,0 +1,109 @@
+"""BASELINE.json configs on the GPU vs the oracle:
+
+  configs[0] C1  rialto-shaped table, MULT=2, INSTANCES=1: all 164,500 rows, events ==
+                 oracle/controller.py run_partition (the restatement pinned to the
+                 reference's own outputs by tests/test_oracle.py);
+  configs[4] C5  short class blocks -> a refit every one or two batches: hundreds of
+                 refits per partition, every event and the RNG position == the oracle;
+  configs[2] C3  full-size property (one drift per class boundary, in the batch holding
+                 it, no warning) on the BatchRunner path the bench times;
+  device generators == their host mirror (oracle/synth.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import synth as hsynth
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    return torch.device("cuda", 0)
+
+
+def test_device_generators_match_host_mirror():
+    from ddm_amd import kernels, synth
+    dev = _dev()
+    n = 50_000
+    p = synth.jitter_partition(n, 5, 8, 123, dev, flip=0.02)
+    p3 = synth.block_partition(n, 2, 8, 10_037, 77, dev)
+    X, y = synth.host_copy(p)
+    assert np.array_equal(y, hsynth.jitter_labels(n, 5, 8, 1800, 300, 10, 0.02, 123))
+    assert np.array_equal(X.astype(np.float32), hsynth.features(y, 5, 8, 123))
+    X3, y3 = synth.host_copy(p3)
+    assert np.array_equal(y3, hsynth.block_labels(n, 2, 8, 10_037, 10))
+    assert np.array_equal(X3.astype(np.float32), hsynth.features(y3, 2, 8, 77))
+    yk = torch.empty(1000, dtype=torch.int32, device=dev)
+    with pytest.raises(Exception):
+        kernels.synth_jitter_labels(yk, 0, 8, 1800, 900, 10, 0.0, 1)      # 2*jitter >= period
+
+
+def test_c1_rialto_shaped_full_vs_oracle():
+    from ddm_amd.controller import run_partition_arrays
+    from ddm_amd.rng import MTStream
+    from ddm_amd.synth import rialto_partitions
+    from oracle.controller import run_partition
+    _, _, parts = rialto_partitions()
+    pa = parts[0]
+    n = len(pa.target)
+    assert n == 164_500
+    rng = MTStream.from_seed(20261015)
+    got = run_partition_arrays([pa], [rng], device=_dev())[0].to_numpy()
+    np.random.seed(20261015)
+    want = run_partition(pa.X32.T.astype(np.float64), pa.target, np.arange(n), pa.row_number)
+    assert np.array_equal(got, want)
+    after = np.random.get_state()
+    assert np.array_equal(rng.key, after[1]) and rng.pos.value == after[2]
+    assert (want[:, 2] >= 0).sum() >= 9
+
+
+@pytest.mark.parametrize("flip,parts_run", [(0.0, (0, 3)), (0.01, (6,))])
+def test_c5_refit_heavy_vs_oracle(flip, parts_run):
+    """C5-shaped partitions (20k rows each of an 8-partition stream) in ONE BatchRunner:
+    a drift and a device refit every one or two batches."""
+    from ddm_amd import synth
+    from ddm_amd.controller import BatchRunner
+    from ddm_amd.params import DDMSettings
+    from ddm_amd.rng import MTStream
+    from oracle.controller import run_partition
+    dev = _dev()
+    n = 20_000
+    parts = [synth.jitter_partition(n, d, 8, 20261015, dev, flip=flip) for d in parts_run]
+    host = [synth.host_copy(p) for p in parts]
+    runner = BatchRunner(parts, DDMSettings())
+    rngs = [MTStream.from_seed(9000 + d) for d in parts_run]
+    got = runner.run(rngs)
+    runner.close()
+    for k, d in enumerate(parts_run):
+        X, y = host[k]
+        np.random.seed(9000 + d)
+        want = run_partition(X, y, np.arange(n), np.arange(n))
+        assert np.array_equal(got[k][:, 0], want[:, 0]) and np.array_equal(got[k][:, 1], want[:, 2]), d
+        after = np.random.get_state()
+        assert np.array_equal(rngs[k].key, after[1]) and rngs[k].pos.value == after[2]
+        assert (want[:, 2] >= 0).sum() >= 60, d          # a refit every ~2-3 batches
+    assert runner.stats.device_refits >= 100
+
+
+def test_c3_full_size_property_on_bench_path():
+    """configs[2] at 8 x 12.5M rows (global class blocks of 1,000,037 rows): exactly one
+    drift per class boundary, in the batch holding it, no warning."""
+    import bench
+    from ddm_amd import synth
+    from ddm_amd.controller import BatchRunner
+    from ddm_amd.params import DDMSettings
+    from ddm_amd.rng import MTStream
+    dev = _dev()
+    n, P, block = 12_500_000, 8, 1_000_037
+    parts = [synth.block_partition(n, d, P, block, 20261015, dev) for d in range(P)]
+    runner = BatchRunner(parts, DDMSettings(), torch.cuda.Stream(dev, priority=-1), timing=True, fit_threads=16)
+    outs = runner.run([MTStream.from_seed(20261015 + d) for d in range(P)])
+    runner.close()
+    res = dict(enumerate(outs))
+    bench.c3_property_check(res, n, P, block)
+    assert sum(int((r[:, 1] >= 0).sum()) for r in outs) == sum(
+        len([k for k in range(1, (n * P + d) // block + 1) if 100 <= (k * block - d + P - 1) // P < n])
+        for d in range(P))
+    del parts
+    torch.cuda.empty_cache()

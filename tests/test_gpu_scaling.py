@@ -1,0 +1,56 @@
+"""configs[2]/[4] at N > 1 as the driver runs them: the SAME partitions, partition d on rank
+d % N (DDM_Process.py:225-226), must give the same events at every N.
+
+Rehearsed on one GPU: `torch.distributed.run` starts 2 ranks of bench.py that share
+cuda:0 and gather over gloo (DDM_BENCH_BACKEND=gloo); the digest of ALL partitions'
+gathered events must equal the N=1 run's."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bench(n, extra):
+    args = ["bench.py", "--gpus", str(n), "--steps", "1", "--warmup", "0", "--cpu-baseline", "0",
+            "--oracle-check-rows", "0"] + extra
+    env = dict(os.environ, DDM_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    if n == 1:
+        cmd = [sys.executable] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    return json.loads(line)
+
+
+@pytest.mark.parametrize("workload,extra", [
+    ("c3", ["--rows-per-part", "2000000", "--block-rows", "1000037"]),
+    ("c5", ["--c5-rows", "160000"]),
+])
+def test_events_do_not_depend_on_gpu_count(workload, extra):
+    one = _bench(1, ["--workload", workload] + extra)
+    two = _bench(2, ["--workload", workload] + extra)
+    d1, d2 = one["breakdown"]["checks"]["events_sha1"], two["breakdown"]["checks"]["events_sha1"]
+    assert d1 == d2
+    assert one["breakdown"]["drifts_per_step"] > 0
+    assert two["config"]["partitions_this_rank"] == 4 and one["config"]["partitions_this_rank"] == 8
+    assert one["scaling"] == two["scaling"] == "strong"
+    if workload == "c5":
+        assert two["breakdown"]["gather_ms_per_step"] is not None
