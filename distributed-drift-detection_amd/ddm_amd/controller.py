@@ -49,6 +49,21 @@ def ps_feats(part):
     return part.X.shape[0]
 
 
+def _int_labels(y):
+    """Labels as int64, refusing what the device path cannot reproduce: non-integer values
+    (the reference compares y_pred != y on the raw labels, DDM_Process.py:117) and values
+    outside int32."""
+    y = np.asarray(y)
+    if y.dtype.kind == "f":
+        if not np.isfinite(y).all() or not np.array_equal(y, np.floor(y)):
+            raise ValueError("labels must be integers on the device path (non-integer or NaN targets)")
+    elif y.dtype.kind not in "iub":
+        raise ValueError(f"labels must be integers on the device path (dtype {y.dtype})")
+    if y.size and (y.min() < np.iinfo(np.int32).min or y.max() > np.iinfo(np.int32).max):
+        raise ValueError("labels must fit int32 on the device path")
+    return y.astype(np.int64)
+
+
 class DevicePartition:
     """One partition's rows resident in HBM: X float32 [F, ld] (column f contiguous), y int32."""
 
@@ -69,9 +84,7 @@ class DevicePartition:
     def from_arrays(cls, X32, y, device, stream=None):
         """X32: [n, F] float32 host rows (the float32 cast sklearn applies), y: int labels."""
         X32 = np.ascontiguousarray(X32, dtype=np.float32)
-        y = np.asarray(y)
-        if y.size and (y.min() < np.iinfo(np.int32).min or y.max() > np.iinfo(np.int32).max):
-            raise ValueError("labels must fit int32 on the device path")
+        y = _int_labels(y)
         n, F = X32.shape
         part = cls.allocate(n, F, device)
         with torch.cuda.stream(stream or torch.cuda.current_stream(device)):
@@ -85,9 +98,7 @@ class DevicePartition:
     def from_columns(cls, Xc, y, device, stream=None):
         """Xc: float32 [F, n] columnar host array (loader.PartitionArrays.X32), y: int labels."""
         Xc = np.asarray(Xc, dtype=np.float32)
-        y = np.asarray(y)
-        if y.size and (y.min() < np.iinfo(np.int32).min or y.max() > np.iinfo(np.int32).max):
-            raise ValueError("labels must fit int32 on the device path")
+        y = _int_labels(y)
         F, n = Xc.shape
         part = cls.allocate(n, F, device)
         with torch.cuda.stream(stream or torch.cuda.current_stream(device)):
@@ -150,10 +161,10 @@ class _Part:
         return self.last_len if b == self.nb - 1 else self.pb
 
     def b_end_is_tail(self, pb):
-        """This epoch's window reaches a short last batch (shuffled on the host)."""
-        g0 = self.j + 1 if self.retrain else self.j
+        """This epoch's window reaches a short last batch (shuffled on the host); g0 must
+        already be this epoch's first GPU-shuffled batch."""
         b_end = min(self.nb, self.j + min(self.win, self.max_win))
-        return b_end == self.nb and self.last_len != pb and self.nb - 1 >= g0
+        return b_end == self.nb and self.last_len != pb and self.nb - 1 >= self.g0
 
 
 class BatchRunner:
@@ -604,14 +615,15 @@ class BatchRunner:
         for ps in live:
             ps.P_after_first = None
         work = self._refit_prep(need) if need else []
+        for ps in live:
+            if ps not in need:
+                ps.g0 = ps.j
         late_fit = bool(work) and not any(ps.b_end_is_tail(pb) for ps in live)
         if work and not late_fit:
             self._refit_fit(work)
         t1 = time.perf_counter()
         host = t1 - t0 - (self.stats.refit_s - refit_before)
         for ps in live:
-            if ps not in need:
-                ps.g0 = ps.j
             ps.b_end = min(ps.nb, ps.j + min(ps.win, ps.max_win))
             ps.Wg = max(0, min(ps.b_end, ps.n_full) - ps.g0)
             ps.tail = ps.b_end == ps.nb and ps.last_len != pb and ps.nb - 1 >= ps.g0
@@ -766,7 +778,7 @@ class BatchRunner:
                 # one, so the next window covers it with 1/8 to spare (one epoch per drift
                 # when concepts repeat their length; windows still double after a miss)
                 seg = d - ps.seg_start + 1
-                ps.win = max(max(1, s.window_batches), seg + seg // 8)
+                ps.win = max(max(1, min(s.window_batches, s.drift_window_batches)), seg + seg // 8)
                 ps.j = d + 1
             else:
                 if ps.tail:

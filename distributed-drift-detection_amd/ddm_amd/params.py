@@ -19,6 +19,8 @@ class DDMSettings:
     row_number: str = "full_df_row_number"   # DDM_Process.py:220
     window_batches: int = 256            # first speculative window (batches); doubles while no drift
     max_window_batches: int = 1 << 16
+    drift_window_batches: int = 16       # least window after a drift (short concepts: an epoch costs more
+                                         # than predicting a few batches past the next drift)
     extra: dict = field(default_factory=dict)
 
 

@@ -16,11 +16,14 @@ from ._capi import check, lib
 
 
 class MTStream:
-    __slots__ = ("key", "pos")
+    __slots__ = ("key", "pos", "gauss")
 
-    def __init__(self, key, pos):
+    def __init__(self, key, pos, gauss=(0, 0.0)):
         self.key = np.ascontiguousarray(key, dtype=np.uint32).copy()
         self.pos = ctypes.c_int32(int(pos))
+        # numpy's cached Gaussian (has_gauss, cached_gaussian): permutation and randint
+        # leave it alone, so it is carried through untouched
+        self.gauss = (int(gauss[0]), float(gauss[1]))
         assert self.key.shape == (624,)
 
     @classmethod
@@ -28,7 +31,8 @@ class MTStream:
         name, key, pos = state[0], state[1], state[2]
         if name != "MT19937":
             raise ValueError(f"unsupported bit generator {name}")
-        return cls(key, pos)
+        gauss = (state[3], state[4]) if len(state) >= 5 else (0, 0.0)
+        return cls(key, pos, gauss)
 
     @classmethod
     def from_global(cls):
@@ -39,7 +43,7 @@ class MTStream:
         return cls.from_numpy_state(np.random.RandomState(seed).get_state())
 
     def numpy_state(self):
-        return ("MT19937", self.key.copy(), int(self.pos.value), 0, 0.0)
+        return ("MT19937", self.key.copy(), int(self.pos.value), self.gauss[0], self.gauss[1])
 
     def to_random_state(self):
         rs = np.random.RandomState()
@@ -50,6 +54,7 @@ class MTStream:
         st = rs.get_state()
         self.key[:] = st[1]
         self.pos.value = int(st[2])
+        self.gauss = (int(st[3]), float(st[4]))
 
     def snapshot(self):
         return self.key.copy(), int(self.pos.value)
@@ -59,7 +64,7 @@ class MTStream:
         self.pos.value = snap[1]
 
     def copy(self):
-        return MTStream(self.key, self.pos.value)
+        return MTStream(self.key, self.pos.value, self.gauss)
 
     def perms(self, batch_len, out=None, draws=None):
         """Legacy `permutation(n)` for each n in batch_len (n <= 256), back to back as uint8."""

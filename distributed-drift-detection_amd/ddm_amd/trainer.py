@@ -35,7 +35,8 @@ class NativeForestTrainer:
         n, F = X32.shape
         classes, yi = np.unique(np.asarray(y), return_inverse=True)
         if classes.size > MAX_CLASSES:
-            raise ValueError(f"{classes.size} classes > {MAX_CLASSES}")
+            raise ValueError(f"a training batch holds {classes.size} classes; the device path supports at most "
+                                 f"{MAX_CLASSES} per batch (INTEGRATION.md, limits)")
         if n > self.max_rows:
             self._alloc(n)
         yi = np.ascontiguousarray(yi, dtype=np.int32)
@@ -108,7 +109,8 @@ class BatchForestTrainer:
             n, F = X32.shape
             classes, yi = np.unique(np.asarray(y), return_inverse=True)
             if classes.size > MAX_CLASSES:
-                raise ValueError(f"{classes.size} classes > {MAX_CLASSES}")
+                raise ValueError(f"a training batch holds {classes.size} classes; the device path supports at most "
+                                 f"{MAX_CLASSES} per batch (INTEGRATION.md, limits)")
             yi = np.ascontiguousarray(yi, dtype=np.int32)
             seeds = np.ascontiguousarray(seeds, dtype=np.int64)
             cls32 = classes.astype(np.int32)

@@ -30,13 +30,16 @@ def test_global_rng_left_where_reference_leaves_it():
     from oracle.controller import run_partition
     d, part, expect = golden_partitions(2, 4)[2]
     np.random.seed(5)
+    np.random.standard_normal()          # leaves a cached Gaussian (has_gauss = 1)
     ddm_amd.run_DDM_loop(part)
     after_gpu = np.random.get_state()
     np.random.seed(5)
+    np.random.standard_normal()
     run_partition(part[[str(i) for i in range(21)]].to_numpy(), part["target"].to_numpy(), part.index.to_numpy(),
                   part["full_df_row_number"].to_numpy())
     after_ref = np.random.get_state()
     assert np.array_equal(after_gpu[1], after_ref[1]) and after_gpu[2] == after_ref[2]
+    assert after_ref[3] == 1 and after_gpu[3:] == after_ref[3:]
 
 
 @pytest.mark.parametrize("win,maxwin", [(1, 1), (1, 4), (3, 1000), (10_000, 1 << 16)])
