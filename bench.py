@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--c4-len", type=int, default=4096)
     ap.add_argument("--c5-rows", type=int, default=64_000_000, help="c5 rows (all partitions)")
     ap.add_argument("--c5-flip", type=float, default=0.0, help="c5 label-noise rate")
+    ap.add_argument("--solo-world", type=int, default=0,
+                    help="measurement aid: run only rank 0's partitions of an N-GPU job (d % N == 0), one "
+                         "process, no collective (the per-GPU share of the strong-scaling workloads)")
     return ap.parse_args()
 
 
@@ -226,17 +229,19 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     from ddm_amd.params import DDMSettings
     from ddm_amd.rng import MTStream
     P = args.parts
+    # GPUs the partitions are placed on (solo_world: rank 0's share of an N-GPU job, alone)
+    gpus = args.solo_world if args.solo_world > 1 and world == 1 else world
     if kind == "c3":
         instances, block, n = P, args.block_rows, args.rows_per_part
-        mine = [d for d in range(instances) if d % world == rank]
+        mine = [d for d in range(instances) if d % gpus == rank]
     elif kind == "c3w":
-        instances = P * world
-        block = args.block_rows if world == 1 else (args.block_rows // 8) * instances + 37
+        instances = P * gpus
+        block = args.block_rows if gpus == 1 else (args.block_rows // 8) * instances + 37
         n = args.rows_per_part
         mine = [rank * P + p for p in range(P)]
     else:   # c5
         instances, block, n = P, None, args.c5_rows // P
-        mine = [d for d in range(instances) if d % world == rank]
+        mine = [d for d in range(instances) if d % gpus == rank]
     parts = []
     for d in mine:
         if kind == "c5":
@@ -325,8 +330,9 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     else:
         wl = (f"configs[2] weak-scaling variant: {P} partitions x {n} rows per GPU, INSTANCES={instances}, "
               f"class blocks of {block} global rows")
-    info = {"workload": wl, "rows_per_step": n * instances if kind != "c3w" else n * P * world,
+    info = {"workload": wl, "rows_per_step": n * instances if kind != "c3w" else n * P * gpus,
             "partitions": instances, "partitions_this_rank": len(parts),
+            "solo_share_of_gpus": gpus if gpus != world else None,
             "refit": "ddm_rf_fit_device (sklearn 1.7.2 RandomForestClassifier restated, identical trees) on the GPU",
             "execution": "all partitions of a GPU in lockstep epochs (BatchRunner): one batched shuffle, predict, "
                          "scan, stage and refit launch per epoch"}
@@ -505,6 +511,8 @@ def run_c4(args, world, rank, dev, torch, dist, cpu):
 def main():
     args = parse()
     world, rank, local_rank = dist_env()
+    if args.solo_world > 1 and world == 1:
+        args.cpu_baseline = 0
     cpu = None
     if args.cpu_baseline and rank == 0 and world == 1 and args.workload in ("c3", "c3w", "c5"):
         cpu = CpuBaseline(args.cpu_procs, args.cpu_cores)     # forked before any HIP call

@@ -44,35 +44,64 @@ struct Job {
 static_assert(sizeof(Job) == sizeof(ddm_stage_job), "Job must mirror ddm_stage_job");
 
 __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__ jobs) {
-    __shared__ int counts[kStageThreads];
+    __shared__ int counts[kStageThreads / 64];
     const Job jb = jobs[blockIdx.x];
     const int t = threadIdx.x;
     const int32_t stop = *jb.stop;
     const int64_t last = stop >= 0 ? jb.j + stop : jb.b_end - 1;   // last batch the scan covered
     const int64_t nrows = last - jb.j + 1;                         // window rows of ev to look at
-    // ---- compact the event rows: each thread a contiguous slice, block prefix of counts
-    const int64_t per = (nrows + kStageThreads - 1) / kStageThreads;
-    const int64_t r0 = t * per, r1 = min(nrows, r0 + per);
-    int c = 0;
-    for (int64_t r = r0; r < r1; ++r) c += (jb.ev[2 * r] >= 0 || jb.ev[2 * r + 1] >= 0) ? 1 : 0;
-    counts[t] = c;
-    __syncthreads();
-    for (int s = 1; s < kStageThreads; s <<= 1) {      // inclusive scan (Hillis-Steele)
-        const int v = t >= s ? counts[t - s] : 0;
+    // ---- compact the event rows, in row order: per round every thread reads 8 consecutive
+    // rows with four 16-byte loads (the whole block 2048 rows, coalesced, one memory
+    // latency per round), then a block prefix of the per-thread counts places them
+    const int lane = t & 63, wv = t >> 6;
+    int total = 0;
+    for (int64_t base = 0; base < nrows; base += 8 * kStageThreads) {
+        const int64_t r0 = base + 8 * (int64_t)t;
+        int4 q[4];
+        const bool vec = r0 + 8 <= nrows && ((reinterpret_cast<uintptr_t>(jb.ev + 2 * r0) & 15) == 0);
+        if (vec) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] = reinterpret_cast<const int4*>(jb.ev + 2 * r0)[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int64_t ra = r0 + 2 * k, rb = ra + 1;
+                q[k].x = ra < nrows ? jb.ev[2 * ra] : -1;
+                q[k].y = ra < nrows ? jb.ev[2 * ra + 1] : -1;
+                q[k].z = rb < nrows ? jb.ev[2 * rb] : -1;
+                q[k].w = rb < nrows ? jb.ev[2 * rb + 1] : -1;
+            }
+        }
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            bits |= (uint32_t)(q[k].x >= 0 || q[k].y >= 0) << (2 * k);
+            bits |= (uint32_t)(q[k].z >= 0 || q[k].w >= 0) << (2 * k + 1);
+        }
+        int c = __popc(bits);
+        int incl = c;                                   // inclusive prefix over the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int u = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += u;
+        }
+        if (lane == 63) counts[wv] = incl;
         __syncthreads();
-        counts[t] += v;
-        __syncthreads();
-    }
-    const int total = counts[kStageThreads - 1];
-    int k = counts[t] - c;
-    for (int64_t r = r0; r < r1 && k < jb.max_events; ++r) {
-        const int32_t w = jb.ev[2 * r], ch = jb.ev[2 * r + 1];
-        if (w >= 0 || ch >= 0) {
-            jb.ev_out[3 * k] = (int32_t)r;
-            jb.ev_out[3 * k + 1] = w;
-            jb.ev_out[3 * k + 2] = ch;
+        int before = total;
+        for (int w = 0; w < wv; ++w) before += counts[w];
+        const int round = counts[0] + counts[1] + counts[2] + counts[3];
+        int k = before + incl - c;
+        while (bits && k < jb.max_events) {
+            const int s = __builtin_ctz(bits);
+            bits &= bits - 1;
+            const int4 v = q[s >> 1];
+            jb.ev_out[3 * k] = (int32_t)(r0 + s);
+            jb.ev_out[3 * k + 1] = (s & 1) ? v.z : v.x;
+            jb.ev_out[3 * k + 2] = (s & 1) ? v.w : v.y;
             ++k;
         }
+        total += round;
+        __syncthreads();
     }
     if (t == 0) {
         jb.info_out[1] = total;

@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
@@ -55,6 +55,9 @@ SIGNATURES = {
     "ddm_scan_batches": (ctypes.c_int, [_vp, _i64, _i64, ctypes.POINTER(DdmParams), _vp, _vp, _vp, _vp, _vp, _vp,
                                         _vp, _vp]),
     "ddm_scan_batches_scratch_bytes": (_i64, [_i64, _i64, _i32]),
+    "ddm_scan_long": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, ctypes.POINTER(DdmParams), _vp, _vp, _vp, _vp, _vp,
+                                     _i32, _vp, _vp, _vp, _vp, _vp]),
+    "ddm_scan_long_scratch_bytes": (_i64, [_i64, _i64, _i32]),
     "ddm_forest_predict_batch": (ctypes.c_int, [_vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "ddm_shuffle_generate_batch": (ctypes.c_int, [_vp, _i32, _vp]),
     "ddm_mt_charpoly": (ctypes.c_int, [_vp]),

@@ -35,6 +35,23 @@ from .rng import MTStream
 from .shuffle import GpuShuffle, expected_draws_per_batch, perm_seeds_from_words
 from .trainer import BatchForestTrainer
 
+# A window runs on ddm_scan_long when its carried detector is neither fresh nor trivial
+# (every row of it is exact arithmetic) and it spans at least this many rows.
+LONG_SCAN_MIN_ROWS = int(os.environ.get("DDM_LONG_SCAN_ROWS", 4 * 64 * 100))
+
+
+def carried_exact(st):
+    """A carried ddm_state whose next rows all need the exact recurrence: not fresh (or
+    pending a reset) and not the trivial all-zero state (det.h det_fresh / det_trivial)."""
+    if st["in_concept_change"]:
+        return False
+    fresh = (st["sample_count"] == 1 and st["miss_prob"] == 1.0 and st["miss_std"] == 0.0
+             and np.isinf(st["miss_prob_sd_min"]))
+    trivial = (st["miss_prob"] == 0.0 and st["miss_prob_sd_min"] == 0.0 and st["miss_prob_min"] == 0.0
+               and st["miss_sd_min"] == 0.0)
+    return not (fresh or trivial)
+
+
 # Largest piece of a partition's MT19937 stream generated per side-stream launch: an epoch
 # waits only for the piece holding the draws it reads, so the generator (one sequential
 # recurrence per partition) runs ahead of the epochs instead of holding them to its end.
@@ -139,11 +156,11 @@ def sklearn_refit(settings):
 class RunStats:
     __slots__ = ("epochs", "refits", "predicted_rows", "refit_s", "gpu_s", "host_s", "predict_ms", "predict_bytes",
                  "scan_ms", "scan_rows", "shuffle_ms", "sklearn_refits", "refit_fit_s", "refit_readback_s",
-                 "prep_s", "dfit_ms", "device_refits")
+                 "prep_s", "dfit_ms", "device_refits", "long_scans")
 
     def __init__(self):
         self.epochs = self.refits = self.predicted_rows = self.predict_bytes = self.scan_rows = 0
-        self.sklearn_refits = self.device_refits = 0
+        self.sklearn_refits = self.device_refits = self.long_scans = 0
         self.refit_s = self.gpu_s = self.host_s = self.predict_ms = self.scan_ms = self.shuffle_ms = 0.0
         self.refit_fit_s = self.refit_readback_s = self.prep_s = self.dfit_ms = 0.0
 
@@ -155,7 +172,7 @@ class _Part:
     """Host-side epoch state of one partition in a BatchRunner."""
     __slots__ = ("i", "nb", "last_len", "n_full", "max_win", "base", "ev_base", "j", "P", "retrain", "train_rows",
                  "state", "win", "forest", "out", "done", "P_after_first", "g0", "b_end", "Wg", "tail",
-                 "P_tail_after", "seg_start", "pb", "staged")
+                 "P_tail_after", "seg_start", "pb", "staged", "rng_rows")
 
     def blen(self, b):
         return self.last_len if b == self.nb - 1 else self.pb
@@ -241,7 +258,9 @@ class BatchRunner:
         F = max(p.X.shape[0] for p in self.parts)
         self.n_words = max(3 * pb + self.s.n_estimators + 64, 1024)   # >= the stage kernel's LDS words
         self.max_events = 64
-        self.o_jobs = _round_up(self.o_state + 56 * k, 256)
+        # ranges of the partitions routed to ddm_scan_long this epoch (empty for the others)
+        self.o_loff, self.o_lend = 108 * k, 116 * k
+        self.o_jobs = _round_up(self.o_lend + 8 * k, 256)
         self.o_stage_tab = self.o_jobs + _round_up(n * kernels.JOB_DTYPE.itemsize, 256)
         self.o_dfit_tab = self.o_stage_tab + _round_up(n * kernels.STAGE_DTYPE.itemsize, 256)
         self.o_stage = self.o_dfit_tab + _round_up(n * dfit.DFIT_DTYPE.itemsize, 256)
@@ -265,6 +284,14 @@ class BatchRunner:
         self.end_h = c[self.o_end:self.o_end + 8 * n].view(np.int64)
         self.bbase_h = c[self.o_bbase:self.o_bbase + 8 * n].view(np.int64)
         self.state_h = c[self.o_state:self.o_state + 56 * n].view(kernels.STATE_DTYPE)
+        self.loff_h = c[self.o_loff:self.o_loff + 8 * n].view(np.int64)
+        self.lend_h = c[self.o_lend:self.o_lend + 8 * n].view(np.int64)
+        # long carried segments (a detector that is neither fresh nor trivial over a window
+        # of >= LONG_SCAN_MIN_ROWS rows) run on ddm_scan_long instead of one lane
+        self.long_max_rows = max(self.max_wins) * pb
+        self.long_scratch = torch.empty(kernels.scan_long_scratch_size(n, self.long_max_rows, pb), dtype=torch.uint8,
+                                        device=dev)
+        self.t_long = kernels.LaunchTimer() if timing else None
         self.bbase_h[:] = self.ev_bases
         self.segs = kernels.PinnedTable(kernels.SEG_DTYPE, n, dev)
         self.jobs = kernels.PinnedTable(kernels.JOB_DTYPE, n, dev, self.ctrl_h[self.o_jobs:],
@@ -654,12 +681,21 @@ class BatchRunner:
         # scan ranges and carried DDM states (the control block), segment table (predict)
         self.off_h[:] = 0
         self.end_h[:] = 0
+        self.loff_h[:] = 0
+        self.lend_h[:] = 0
+        long_rows = 0
         for ps in live:
             p0 = ps.base + ps.j * pb
             p1 = ps.base + (ps.b_end - 1) * pb + ps.blen(ps.b_end - 1)
+            ps.rng_rows = (p0, p1)
             self.off_h[ps.i], self.end_h[ps.i] = p0, p1
             # a refitting partition starts a fresh DDM (:136-139), whenever its fit runs
             self.state_h[ps.i] = kernels.fresh_states(1)[0] if ps.retrain else ps.state[0]
+            if not ps.retrain and p1 - p0 >= LONG_SCAN_MIN_ROWS and carried_exact(ps.state[0]):
+                self.loff_h[ps.i], self.lend_h[ps.i] = p0, p1
+                self.end_h[ps.i] = p0            # nothing for the one-lane scan
+                long_rows = max(long_rows, p1 - p0)
+                st.long_scans += 1
         if not late_fit:
             self._segment_table(live)
         t2 = time.perf_counter()
@@ -689,6 +725,11 @@ class BatchRunner:
                                  base + self.o_bbase, self.ev_total, self.ev_d.data_ptr(), base + self.o_first,
                                  base + self.o_stop, base + self.o_nev, 0, None, stream, self.t_scan,
                                  self.perm_all.data_ptr(), base + self.o_end)
+        if long_rows:
+            kernels.scan_long_raw(self.err_all.data_ptr(), base + self.o_loff, base + self.o_lend, n, long_rows,
+                                  self.params, base + self.o_state, base + self.o_bbase, self.ev_d.data_ptr(),
+                                  base + self.o_stop, base + self.o_nev, 0, self.perm_all.data_ptr(),
+                                  self.long_scratch.data_ptr(), stream, self.t_long)
         if shuf:
             kernels.shuffle_pick_batch(self.jobs, len(shuf), stream)
         # stage what the host needs next, then one copy back and one synchronisation
@@ -706,6 +747,8 @@ class BatchRunner:
         if self.timing:
             st.predict_ms += self.t_pred.elapsed_ms()
             st.scan_ms += self.t_scan.elapsed_ms()
+            if long_rows:
+                st.scan_ms += self.t_long.elapsed_ms()
             if shuf:
                 st.shuffle_ms += self.t_shuf.elapsed_ms()
             if self.t_fit is not None:
@@ -715,7 +758,7 @@ class BatchRunner:
         for ps in live:
             stop, nev = int(self.stop_h[ps.i]), int(self.nev_h[ps.i])
             ps_last = ps.j + stop if stop >= 0 else ps.b_end - 1
-            p0, p1 = int(self.off_h[ps.i]), int(self.end_h[ps.i])
+            p0, p1 = ps.rng_rows
             st.predicted_rows += p1 - p0
             if self.timing:
                 st.predict_bytes += (p1 - p0) * (4 * ps.forest.features_read + 6)

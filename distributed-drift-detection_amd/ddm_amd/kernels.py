@@ -206,6 +206,31 @@ def scan_batches(err, n_streams, stream_len, params, state, ev, scratch, nev=Non
                                *_evs(timer)), "ddm_scan_batches")
 
 
+def scan_long_scratch_size(n_streams, max_rows, per_batch=100):
+    """Bytes of device scratch ddm_scan_long needs."""
+    return int(lib.ddm_scan_long_scratch_bytes(int(n_streams), int(max_rows), int(per_batch)))
+
+
+def scan_long(err, offsets, params, state, batch_base, ev, max_rows, scratch, ends=None, stop=None, nev=None, mode=0,
+              perm_map=None, stream=None, timer=None):
+    """ddm_scan_long over streams err[offsets[s]:ends[s]] (ends None: offsets[s+1]); the
+    results of scan_streams for long carried segments (see include/ddm_amd.h)."""
+    n = offsets.numel() - (0 if ends is not None else 1)
+    assert scratch.numel() >= scan_long_scratch_size(n, max_rows, params.per_batch)
+    check(lib.ddm_scan_long(err.data_ptr(), offsets.data_ptr(), _ptr(ends), int(n), int(max_rows),
+                            ctypes.byref(params), state.data_ptr(), batch_base.data_ptr(), ev.data_ptr(), _ptr(stop),
+                            _ptr(nev), int(mode), _ptr(perm_map), scratch.data_ptr(), _stream(err, stream),
+                            *_evs(timer)), "ddm_scan_long")
+
+
+def scan_long_raw(err_ptr, off_ptr, end_ptr, n_streams, max_rows, params, state_ptr, batch_base_ptr, ev_ptr, stop_ptr,
+                  nev_ptr, mode, perm_map_ptr, scratch_ptr, stream, timer=None):
+    """Pointer-level ddm_scan_long (the controller's long carried windows)."""
+    check(lib.ddm_scan_long(err_ptr, off_ptr, end_ptr, int(n_streams), int(max_rows), ctypes.byref(params), state_ptr,
+                            batch_base_ptr, ev_ptr, stop_ptr, nev_ptr, int(mode), perm_map_ptr, scratch_ptr,
+                            ctypes.c_void_p(stream.cuda_stream), *_evs(timer)), "ddm_scan_long")
+
+
 def scan_streams_raw(err_ptr, offsets_ptr, n_streams, params, state_ptr, batch_base_ptr, n_batches_total, ev_ptr,
                      first_nz_ptr, stop_ptr, nev_ptr, mode, ps_ptr, stream, timer=None, perm_map_ptr=None,
                      end_ptr=None):

@@ -11,6 +11,8 @@
  *                           DDM state carried (:202), first warning / first change +
  *                           break per batch (:147-152), DDM dropped after a change
  *                           (:207-210)
+ *   ddm_scan_long        <- run_DDM over long carried segments (wave-parallel tests,
+ *                           chunk-chained carry)
  *   ddm_mt_perms         <- `DataFrame.sample(frac=1)` (:187, :190) on numpy's global
  *                           MT19937 (legacy RandomState.permutation)
  *   ddm_mt_randint31     <- the 100 `randint(2**31-1)` tree seeds RandomForestClassifier
@@ -36,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 10
+#define DDM_AMD_ABI_VERSION 11
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -248,6 +250,26 @@ int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t stream_len, 
                      ddm_state* state_io, int32_t* ev_out, int64_t* nev_out, void* scratch,
                      const uint8_t* perm_map, ddm_stream_t stream, ddm_event_t ev_begin,
                      ddm_event_t ev_end);
+
+/* run_DDM over LONG carried segments (DDM_Process.py:135-159 with the DDM carried across
+ * batches, :144-152, :202): the results of ddm_scan_streams (same stream_off / stream_end /
+ * batch_base / ev_out / stop_out / nev_out / mode / perm_map meaning) for streams whose
+ * detector runs exact rows for very long (no change for millions of rows while not in
+ * its trivial state).  One wave per chunk of 64 * per_batch rows: the p recurrence is the
+ * only sequential part, s, the running arg-min of p + s and the tests are lane-parallel
+ * over 64-row tiles, and chunks are chained by a one-step look-back on the carried
+ * detector (each chunk loads and masks its bytes before the carry reaches it).
+ * Differences from ddm_scan_streams: streams with an empty range are left untouched
+ * (state, stop, nev and events); ev_out is written for every batch of a non-empty stream
+ * (-1 where none), never memset as a whole; max_rows bounds every stream's length (grid
+ * size); per_batch must be 1..256; scratch is ddm_scan_long_scratch_bytes(...) bytes of
+ * device memory, 256-byte aligned (its second uint32 is set to 1 if a chunk ever gave up
+ * waiting for its predecessor, i.e. the results are void). */
+int64_t ddm_scan_long_scratch_bytes(int64_t n_streams, int64_t max_rows, int32_t per_batch);
+int ddm_scan_long(const uint8_t* err, const int64_t* stream_off, const int64_t* stream_end, int64_t n_streams,
+                  int64_t max_rows, const ddm_params* prm, ddm_state* state_io, const int64_t* batch_base,
+                  int32_t* ev_out, int32_t* stop_out, int64_t* nev_out, int32_t mode, const uint8_t* perm_map,
+                  void* scratch, ddm_stream_t stream, ddm_event_t ev_begin, ddm_event_t ev_end);
 
 /* Timing events for the ev_begin / ev_end arguments (hipEventCreate / Destroy /
  * ElapsedTime; elapsed needs both events completed, e.g. after a stream sync). */
