@@ -196,7 +196,10 @@ def c3_property_check(results, n_rows, n_parts, block, pb=100):
             want[f // pb - 1] = f // pb
         got = np.where(r[:, 1] >= 0, r[:, 1] // pb, -1)
         if not np.array_equal(got, want) or (r[:, 0] >= 0).any():
-            raise RuntimeError(f"partition {d}: drifts are not one per class boundary")
+            bad = np.nonzero(got != want)[0][:8]
+            raise RuntimeError(f"partition {d}: drifts are not one per class boundary (batches {bad.tolist()}: got "
+                               f"{got[bad].tolist()} want {want[bad].tolist()}; warnings at "
+                               f"{np.nonzero(r[:, 0] >= 0)[0][:8].tolist()})")
         # the drift row itself is one of the new class's rows of that batch
         for f in firsts:
             c = r[f // pb - 1, 1]

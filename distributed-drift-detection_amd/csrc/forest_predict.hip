@@ -429,10 +429,173 @@ __device__ __forceinline__ void cf_segment(const Seg& sg, int64_t blk, int64_t n
     }
 }
 
+// Stump forests with per_batch % 4 == 0: a thread owns FOUR consecutive rows and reads
+// each feature slot of them with one 16-byte load (a wave: 1 KiB contiguous per slot),
+// labels with one 16-byte load, and in the position phase four DDM positions (one
+// 4-byte perm load, one 4-byte err store).  A tile is floor(2048 / pb) * pb rows; the
+// next tile's first slot chunk and labels are loaded during the current tile.  Rows of a
+// partition start 16-byte aligned (ld % 64 == 0, windows start on batches of a multiple
+// of 4 rows) and ld covers every row a clamped lane may read.
+constexpr int kVecRows = 4;
+
+template <int kVR>
+__device__ __forceinline__ void cf_segment_vec(const Seg& sg, int64_t blk, int64_t nblk, int pb, unsigned char* smem) {
+    const uint8_t* blob = sg.cforest;
+    const ddm_cforest_head* H = reinterpret_cast<const ddm_cforest_head*>(blob);
+    const int U = ldu(&H->n_slots), K = ldu(&H->n_classes);
+    const int tab_words = ldu(&H->rank_tab_entries) * kVR;
+    const ddm_cforest_slot* slots = reinterpret_cast<const ddm_cforest_slot*>(blob + ldu(&H->slots_off));
+    const float4* xthr = reinterpret_cast<const float4*>(blob + ldu(&H->xthr_off));
+    const int tid = threadIdx.x;
+    // LDS (cf_lds_bytes with rows 4): column pointers [32] | rank tables | labels [2048] |
+    // classes [16] | err [2048]
+    const float** s_colp = reinterpret_cast<const float**>(smem);
+    uint32_t* s_tab = reinterpret_cast<uint32_t*>(s_colp + 32);
+    int32_t* s_pred = reinterpret_cast<int32_t*>(s_tab + ((tab_words + 3) & ~3));
+    int32_t* s_cls = s_pred + kVecRows * kCfThreads;
+    uint8_t* s_e = reinterpret_cast<uint8_t*>(s_cls + 16);
+    {
+        const uint32_t* gt = reinterpret_cast<const uint32_t*>(blob + ldu(&H->rank_tab_off));
+        for (int k = tid; k < tab_words; k += kCfThreads) s_tab[k] = gt[k];
+    }
+    if (tid < 16) s_cls[tid] = H->classes[tid];
+    if (tid < 32) s_colp[tid] = sg.X + (int64_t)H->cols[tid] * sg.ld;
+    uint32_t base_votes[kVR];
+#pragma unroll
+    for (int j = 0; j < kVR; ++j) base_votes[j] = ldu(&H->base_votes[j]);
+
+    const int tile = ((kVecRows * kCfThreads) / pb) * pb;
+    const int q0 = kVecRows * tid;                  // this thread's rows / positions in the tile
+    const int lane = tid & 63;
+    bool wave_done = false;
+    const int64_t step = nblk * tile;
+    const int64_t last_row = ((sg.pos_end - 1 - sg.row_base) & ~(int64_t)3);
+    auto row_of = [&](int64_t gt0) -> int64_t {    // first of the 4 rows (clamped: in bounds)
+        const int64_t r = gt0 + q0 - sg.row_base;
+        return (q0 < tile && r <= last_row) ? r : last_row;
+    };
+    auto load_chunk = [&](int c, int64_t row, float4 (&xc)[kChunk]) {
+#pragma unroll
+        for (int k = 0; k < kChunk; ++k) xc[k] = *reinterpret_cast<const float4*>(s_colp[c + k] + row);
+    };
+    float4 xa[kChunk], xb[kChunk];
+#pragma unroll
+    for (int k = 0; k < kChunk; ++k) xa[k] = xb[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    int4 ynext = make_int4(0, 0, 0, 0);
+    int64_t g0 = sg.pos_begin + blk * tile;
+    __syncthreads();                                // column pointers, tables
+    if (g0 < sg.pos_end) {
+        const int64_t row = row_of(g0);
+        if (U > 0) load_chunk(0, row, xa);
+        ynext = *reinterpret_cast<const int4*>(sg.y + row);
+    }
+    for (; g0 < sg.pos_end; g0 += step) {
+        const int64_t row = row_of(g0);
+        const bool has_next = g0 + step < sg.pos_end;
+        const int64_t nrow = has_next ? row_of(g0 + step) : row;
+        const int4 yv = ynext;
+        if (has_next) ynext = *reinterpret_cast<const int4*>(sg.y + nrow);
+        uint32_t votes[kVecRows][kVR];
+#pragma unroll
+        for (int i = 0; i < kVecRows; ++i)
+#pragma unroll
+            for (int j = 0; j < kVR; ++j) votes[i][j] = base_votes[j];
+        // ---- row phase
+        for (int c = 0; c < U; c += kChunk) {
+            if (c + kChunk < U) load_chunk(c + kChunk, row, xb);
+            else if (has_next) load_chunk(0, nrow, xb);
+            const ddm_cforest_slot* sc = slots + c;
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) {
+                const int n4 = ldu(&sc[k].n4);
+                if (n4 > 0) {
+                    const float xv[kVecRows] = {xa[k].x, xa[k].y, xa[k].z, xa[k].w};
+                    const float4 t0 = ldu(reinterpret_cast<const float4*>(sc[k].thr));
+                    const float tt0[4] = {t0.x, t0.y, t0.z, t0.w};
+                    int r[kVecRows];
+#pragma unroll
+                    for (int i = 0; i < kVecRows; ++i) r[i] = rank4(xv[i], tt0);
+                    if (n4 > 1) {
+                        const float4* xt = xthr + ldu(&sc[k].xthr);
+                        for (int q = 0; q < n4 - 1; ++q) {
+                            const float4 t = ldu(xt + q);
+                            const float tt[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+                            for (int i = 0; i < kVecRows; ++i) r[i] += rank4(xv[i], tt);
+                        }
+                    }
+                    const uint32_t* tab = s_tab + ldu(&sc[k].tab) * kVR;
+#pragma unroll
+                    for (int i = 0; i < kVecRows; ++i) add_votes<kVR>(tab + r[i] * kVR, votes[i]);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) xa[k] = xb[k];
+        }
+        const int yl[kVecRows] = {yv.x, yv.y, yv.z, yv.w};
+        uint32_t e4 = 0;
+#pragma unroll
+        for (int i = 0; i < kVecRows; ++i) {
+            int best = 0, bestv = -1;               // first argmax over the vote counters
+#pragma unroll
+            for (int c = 0; c < 4 * kVR; ++c) {
+                const int v = (int)((votes[i][c >> 2] >> (8 * (c & 3))) & 0xffu);
+                const bool better = c < K && v > bestv;
+                bestv = better ? v : bestv;
+                best = better ? c : best;
+            }
+            const int32_t label = s_cls[best];
+            e4 |= (uint32_t)(label != yl[i]) << (8 * i);
+            if (sg.pred && q0 < tile) s_pred[q0 + i] = label;
+        }
+        if (q0 < tile) *reinterpret_cast<uint32_t*>(s_e + q0) = e4;
+        __syncthreads();
+        // ---- position phase: positions g0 + q0 .. g0 + q0 + 3
+        const int64_t g = g0 + q0;
+        int e_any = 0;
+        int64_t g_first = g;
+        if (q0 < tile && g < sg.pos_end) {
+            const uint32_t p4 = *reinterpret_cast<const uint32_t*>(sg.perm + g);
+            uint32_t out = 0;
+            int first = -1;
+#pragma unroll
+            for (int i = 0; i < kVecRows; ++i) {
+                const int q = q0 + i;
+                const int k = (q / pb) * pb + (int)((p4 >> (8 * i)) & 0xffu);
+                const uint32_t e = s_e[k];
+                const bool ok = g + i < sg.pos_end;
+                out |= (ok ? e : 0u) << (8 * i);
+                if (ok && e && first < 0) first = i;
+            }
+            if (g + kVecRows <= sg.pos_end) {
+                *reinterpret_cast<uint32_t*>(sg.err + g) = out;
+            } else {
+                for (int i = 0; g + i < sg.pos_end; ++i) sg.err[g + i] = (uint8_t)((out >> (8 * i)) & 0xffu);
+            }
+            if (sg.pred) {
+                for (int i = 0; i < kVecRows && g + i < sg.pos_end; ++i) {
+                    const int q = q0 + i;
+                    sg.pred[g + i] = s_pred[(q / pb) * pb + (int)((p4 >> (8 * i)) & 0xffu)];
+                }
+            }
+            e_any = first >= 0;
+            g_first = g + (first >= 0 ? first : 0);
+        }
+        if (sg.first_err) note_first_error(sg.first_err, e_any, g_first, lane, wave_done);
+        __syncthreads();                            // s_e / s_pred consumed
+    }
+}
+
+template <int kVR, int kRows>
+__device__ __forceinline__ void cf_dispatch(const Seg& sg, int64_t blk, int64_t nblk, int pb, unsigned char* smem) {
+    if constexpr (kRows == kVecRows) cf_segment_vec<kVR>(sg, blk, nblk, pb, smem);
+    else cf_segment<kVR, kRows>(sg, blk, nblk, pb, smem);
+}
+
 template <int kVR, int kRows>
 __global__ __launch_bounds__(kCfThreads) void k_cforest_predict(Seg sg, int pb) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    cf_segment<kVR, kRows>(sg, blockIdx.x, gridDim.x, pb, smem);
+    cf_dispatch<kVR, kRows>(sg, blockIdx.x, gridDim.x, pb, smem);
 }
 
 template <int kVR, int kRows>
@@ -444,7 +607,7 @@ __global__ __launch_bounds__(kCfThreads) void k_cforest_predict_batch(const Seg*
     while (s < n_segs && !(ldu(&segs[s].block0) <= gb && gb < ldu(&segs[s].block0) + ldu(&segs[s].nblocks))) ++s;
     if (s == n_segs) return;
     const Seg sg = ldu(segs + s);
-    cf_segment<kVR, kRows>(sg, gb - sg.block0, sg.nblocks, pb, smem);
+    cf_dispatch<kVR, kRows>(sg, gb - sg.block0, sg.nblocks, pb, smem);
 }
 
 // The same kernel with the segment table passed by value in the kernel arguments (up to
@@ -465,50 +628,76 @@ __global__ __launch_bounds__(kCfThreads) void k_cforest_predict_arg(const SegTab
     while (s < n_segs && !(tab.s[s].block0 <= gb && gb < tab.s[s].block0 + tab.s[s].nblocks)) ++s;
     if (s == n_segs) return;
     const Seg sg = tab.s[s];
-    cf_segment<kVR, kRows>(sg, gb - sg.block0, sg.nblocks, pb, smem);
+    cf_dispatch<kVR, kRows>(sg, gb - sg.block0, sg.nblocks, pb, smem);
 }
 
 using cf_fn = void (*)(Seg, int);
 using cf_batch_fn = void (*)(const Seg*, int, int64_t, int);
 
 int cf_vkind(int vr) { return vr <= 1 ? 0 : vr <= 2 ? 1 : 2; }
-int cf_rows(int leaves) { return leaves > 0 ? 1 : 2; }
+// rows per thread: 1 with general trees, 4 consecutive (16-byte loads) for stump forests
+// whose rows and positions are 16- / 4-byte aligned, else 2
+bool vec_env() {
+    static const bool on = [] {
+        const char* e = getenv("DDM_PREDICT_VEC");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return on;
+}
+int cf_rows(const Seg& g, int pb) {
+    if (g.cf_leaves > 0) return 1;
+    const bool aligned = pb % 4 == 0 && g.ld % 4 == 0 && g.row_base % 4 == 0 &&
+                         ((reinterpret_cast<uintptr_t>(g.X) | reinterpret_cast<uintptr_t>(g.y)) & 15) == 0 &&
+                         ((reinterpret_cast<uintptr_t>(g.perm) | reinterpret_cast<uintptr_t>(g.err)) & 3) == 0;
+    return aligned && vec_env() ? kVecRows : 2;
+}
+int cf_rows_idx(int rows) { return rows == 1 ? 0 : rows == 2 ? 1 : 2; }
+int cf_rows_of_idx(int i) { return i == 0 ? 1 : i == 1 ? 2 : kVecRows; }
+// positions one block step covers
+int cf_unit(int rows, int pb) {
+    return rows == kVecRows ? ((kVecRows * kCfThreads) / pb) * pb : rows * ((kCfThreads / pb) * pb);
+}
 template <int kRows>
 cf_fn pick_cf_r(int vk) {
     return vk == 0 ? k_cforest_predict<1, kRows> : vk == 1 ? k_cforest_predict<2, kRows> : k_cforest_predict<4, kRows>;
 }
-cf_fn pick_cf(int vk, int rows) { return rows == 1 ? pick_cf_r<1>(vk) : pick_cf_r<2>(vk); }
+cf_fn pick_cf(int vk, int rows) {
+    return rows == 1 ? pick_cf_r<1>(vk) : rows == 2 ? pick_cf_r<2>(vk) : pick_cf_r<kVecRows>(vk);
+}
 template <int kRows>
 cf_batch_fn pick_cf_batch_r(int vk) {
     return vk == 0 ? k_cforest_predict_batch<1, kRows>
                    : vk == 1 ? k_cforest_predict_batch<2, kRows> : k_cforest_predict_batch<4, kRows>;
 }
-cf_batch_fn pick_cf_batch(int vk, int rows) { return rows == 1 ? pick_cf_batch_r<1>(vk) : pick_cf_batch_r<2>(vk); }
+cf_batch_fn pick_cf_batch(int vk, int rows) {
+    return rows == 1 ? pick_cf_batch_r<1>(vk) : rows == 2 ? pick_cf_batch_r<2>(vk) : pick_cf_batch_r<kVecRows>(vk);
+}
 using cf_arg_fn = void (*)(SegTab, int, int64_t, int);
 template <int kRows>
 cf_arg_fn pick_cf_arg_r(int vk) {
     return vk == 0 ? k_cforest_predict_arg<1, kRows>
                    : vk == 1 ? k_cforest_predict_arg<2, kRows> : k_cforest_predict_arg<4, kRows>;
 }
-cf_arg_fn pick_cf_arg(int vk, int rows) { return rows == 1 ? pick_cf_arg_r<1>(vk) : pick_cf_arg_r<2>(vk); }
+cf_arg_fn pick_cf_arg(int vk, int rows) {
+    return rows == 1 ? pick_cf_arg_r<1>(vk) : rows == 2 ? pick_cf_arg_r<2>(vk) : pick_cf_arg_r<kVecRows>(vk);
+}
 
-// LDS of the compiled path (cf_segment): column pointers + rank tables + labels +
-// classes + err + leaf classes + row slots [kRows][slots rounded to 8][512] when the
-// forest has general trees (leaves > 0).
-size_t cf_lds_bytes(int leaves, int slots, int tab_words) {
-    const int kRows = cf_rows(leaves);
+// LDS of the compiled path (cf_segment / cf_segment_vec): column pointers + rank tables
+// + labels + classes + err + leaf classes + row slots [kRows][slots rounded to 8][512]
+// when the forest has general trees (leaves > 0).
+size_t cf_lds_bytes(int leaves, int slots, int tab_words, int kRows) {
     const size_t slots8 = (size_t)((slots + kChunk - 1) & ~(kChunk - 1));
     return 8 * 32 + (size_t)4 * ((tab_words + 3) & ~3) + (size_t)4 * kRows * kCfThreads + 64 +
            (size_t)kRows * kCfThreads + (size_t)((leaves + 15) & ~15) +
            (leaves > 0 ? (size_t)4 * kRows * kCfThreads * slots8 : 0);
 }
 
-size_t cf_lds_bound(const Seg& g) { return cf_lds_bytes(g.cf_leaves, g.cf_slots, g.cf_tab_words); }
+size_t cf_lds_bound(const Seg& g, int pb) { return cf_lds_bytes(g.cf_leaves, g.cf_slots, g.cf_tab_words, cf_rows(g, pb)); }
 
 bool cf_usable(const Seg& g, int pb) {
     return g.cforest && g.cf_slots >= 0 && g.cf_slots <= 32 && g.cf_vote_regs >= 1 && g.cf_vote_regs <= 4 &&
            g.cf_tab_words >= 0 &&
-           g.pos_begin % pb == 0 && cf_lds_bound(g) <= 80 * 1024;
+           g.pos_begin % pb == 0 && cf_lds_bound(g, pb) <= 80 * 1024;
 }
 
 // ---------------------------------------------------------------------------------
@@ -579,11 +768,11 @@ extern "C" int ddm_forest_predict(const float* X, int64_t ld, int32_t n_features
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
     if (cf_usable(sg, per_batch)) {
-        const int rows = cf_rows(sg.cf_leaves);
-        const int tile = rows * ((kCfThreads / per_batch) * per_batch);
+        const int rows = cf_rows(sg, per_batch);
+        const int tile = cf_unit(rows, per_batch);
         sg.nblocks = std::min<int64_t>(ddm::ceil_div(n, tile), kMaxBlocks);
         hipLaunchKernelGGL(pick_cf(cf_vkind(sg.cf_vote_regs), rows), dim3((unsigned)sg.nblocks),
-                           dim3(kCfThreads), cf_lds_bound(sg), s, sg, (int)per_batch);
+                           dim3(kCfThreads), cf_lds_bound(sg, per_batch), s, sg, (int)per_batch);
     } else {
         const size_t lds = forest_lds_bytes(forest->n_nodes, forest->n_trees);
         const bool use_lds = lds <= (size_t)kMaxLdsForest;
@@ -627,30 +816,30 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
     }
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
-    constexpr int kNV = 16 + 6;
+    constexpr int kNV = 16 + 9;
     std::vector<int> variant(n_segs);
     for (int i = 0; i < n_segs; ++i) {
         const Seg& g = hs[i];
         if (cf_usable(g, per_batch)) {
-            variant[i] = 16 + 3 * (cf_rows(g.cf_leaves) - 1) + cf_vkind(g.cf_vote_regs);
+            variant[i] = 16 + 3 * cf_rows_idx(cf_rows(g, per_batch)) + cf_vkind(g.cf_vote_regs);
         } else {
             const bool lds = forest_lds_bytes(g.n_nodes, g.n_trees) <= (size_t)kMaxLdsForest;
             const int kc = g.n_classes <= 4 ? 0 : g.n_classes <= 8 ? 1 : g.n_classes <= 16 ? 2 : 3;
             variant[i] = (g.pure ? 1 : 0) * 8 + (lds ? 4 : 0) + kc;
         }
     }
-    const int tile = (kCfThreads / per_batch) * per_batch;   // positions per block step (x rows)
     int64_t vbase[kNV + 1] = {0};
     size_t vlds[kNV] = {0};
     int64_t b0 = 0;
     for (int v = 0; v < kNV; ++v) {
         vbase[v] = b0;
-        const int unit = v >= 16 ? (1 + (v - 16) / 3) * tile : kThreads;
+        const int unit = v >= 16 ? cf_unit(cf_rows_of_idx((v - 16) / 3), per_batch) : kThreads;
         int64_t rows = 0;
         for (int i = 0; i < n_segs; ++i)
             if (variant[i] == v) {
                 rows += hs[i].pos_end - hs[i].pos_begin;
-                vlds[v] = std::max(vlds[v], v >= 16 ? cf_lds_bound(hs[i]) : forest_lds_bytes(hs[i].n_nodes, hs[i].n_trees));
+                vlds[v] = std::max(vlds[v], v >= 16 ? cf_lds_bound(hs[i], per_batch)
+                                                    : forest_lds_bytes(hs[i].n_nodes, hs[i].n_trees));
             }
         const int64_t total_blocks = rows ? std::min<int64_t>(ddm::ceil_div(rows, unit), kMaxBlocks) : 0;
         for (int i = 0; i < n_segs; ++i) {
@@ -672,7 +861,8 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
         for (int v = 16; v < kNV; ++v) {
             const int64_t nb = vbase[v + 1] - vbase[v];
             if (nb == 0) continue;
-            hipLaunchKernelGGL(pick_cf_arg((v - 16) % 3, 1 + (v - 16) / 3), dim3((unsigned)nb), dim3(kCfThreads), vlds[v],
+            hipLaunchKernelGGL(pick_cf_arg((v - 16) % 3, cf_rows_of_idx((v - 16) / 3)), dim3((unsigned)nb),
+                               dim3(kCfThreads), vlds[v],
                                s, tab, n_segs, vbase[v], (int)per_batch);
             if (int rc = ddm::launch_status("ddm_forest_predict_batch")) return rc;
         }
@@ -689,7 +879,8 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
         const int64_t nb = vbase[v + 1] - vbase[v];
         if (nb == 0) continue;
         if (v >= 16) {
-            hipLaunchKernelGGL(pick_cf_batch((v - 16) % 3, 1 + (v - 16) / 3), dim3((unsigned)nb), dim3(kCfThreads), vlds[v], s,
+            hipLaunchKernelGGL(pick_cf_batch((v - 16) % 3, cf_rows_of_idx((v - 16) / 3)), dim3((unsigned)nb),
+                               dim3(kCfThreads), vlds[v], s,
                                reinterpret_cast<const Seg*>(segs_dev), n_segs, vbase[v], (int)per_batch);
         } else {
             const bool lds = (v & 4) != 0;

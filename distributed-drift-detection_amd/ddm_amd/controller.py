@@ -590,6 +590,13 @@ class BatchRunner:
             ps.last_len = part.n - (ps.nb - 1) * pb
             ps.n_full = ps.nb if ps.last_len == pb else ps.nb - 1
             pss.append(ps)
+        # everything enqueued so far on the caller's stream (the partitions' rows, and the
+        # fills of this runner's own zero-initialised buffers) happens before the runner's
+        # streams touch them
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(self.device))
+        for s_ in (self.stream, self.gen_stream, self.tab_stream):
+            s_.wait_event(ready)
         for ps, rng in zip(pss, rngs):
             self.shuffles[ps.i].reset(rng)
         started = []

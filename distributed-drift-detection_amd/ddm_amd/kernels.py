@@ -155,6 +155,8 @@ class LaunchTimer:
         return ms.value
 
     def __del__(self):
+        if lib is None or getattr(lib, "ddm_event_destroy", None) is None:     # interpreter shutdown
+            return
         for e in getattr(self, "ev", []):
             if e.value:
                 lib.ddm_event_destroy(e)
