@@ -270,7 +270,7 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
             # partition on every rank, one all_gather of the batches with an event
             from ddm_amd.dist import gather_events
             tg = time.perf_counter()
-            allev = gather_events({d: events_rows(results[d]) for d, _ in parts}, n_rows=n_rows)
+            allev = gather_events({d: events_rows(results[d]) for d, _ in parts}, n_rows=n_rows, comm=args.comm)
             gather_s[0] += time.perf_counter() - tg
             for d, _ in parts:
                 if not np.array_equal(allev[d], events_rows(results[d])):
@@ -350,6 +350,8 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
              "host_s_per_step": agg["host_s"] / args.steps, "gpu_wait_s_per_step": agg["gpu_s"] / args.steps,
              "stream_prep_s_per_step": agg["prep_s"] / args.steps,
              "gather_ms_per_step": gather_s[0] / args.steps * 1e3 if world > 1 else None,
+             "gather_backend": (None if world == 1 else "rccl (ctypes ncclAllGather, HBM to HBM)" if args.comm
+                                else "torch.distributed all_gather"),
              "checks": checks}
     roofline = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_from_profile("ddm_forest_predict", rows_per_launch),
@@ -526,11 +528,21 @@ def main():
     backend = os.environ.get("DDM_BENCH_BACKEND", "nccl")
     dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
+    comm = None
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
+            # the event collect runs on RCCL itself (ctypes), torch.distributed only for the
+            # rendezvous, the barrier and the timing reduction
+            try:
+                from ddm_amd.rccl import RcclComm
+                comm = RcclComm.from_default_group(dev)
+            except Exception as e:      # noqa: BLE001  (reported in the JSON line)
+                print(f"rank {rank}: RCCL ctypes communicator unavailable ({e}); gathering over torch.distributed",
+                      file=sys.stderr)
         else:
             dist.init_process_group(backend)
+    args.comm = comm
     if args.workload == "c1":
         res = run_c1(args, world, rank, dev, torch, dist, cpu if rank == 0 and args.cpu_baseline else None)
     elif args.workload == "c4":
@@ -562,6 +574,8 @@ def main():
                                                 f"no data-path collective"),
                "roofline": roofline, "cpu_baseline": cpu_res, "breakdown": extra}
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

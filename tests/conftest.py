@@ -13,6 +13,15 @@ for p in (ROOT, PKG_ROOT):
         sys.path.insert(0, p)
 
 
+# Tests that start other Python processes on the GPU run first, while this process has
+# not initialised the GPU itself (a GPU-initialised process must not exec programs).
+SPAWNING_MODULES = ("test_gpu_scaling.py", "test_gpu_dist.py::test_two_ranks")
+
+
+def pytest_collection_modifyitems(config, items):
+    items.sort(key=lambda it: 0 if any(m in it.nodeid for m in SPAWNING_MODULES) else 1)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
     config.addinivalue_line("markers", "slow: long-running parity sweep")

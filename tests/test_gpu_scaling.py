@@ -45,6 +45,8 @@ def _bench(n, extra):
     ("c5", ["--c5-rows", "160000"]),
 ])
 def test_events_do_not_depend_on_gpu_count(workload, extra):
+    import torch
+    assert not torch.cuda.is_initialized(), "must run before this process touches the GPU"
     one = _bench(1, ["--workload", workload] + extra)
     two = _bench(2, ["--workload", workload] + extra)
     d1, d2 = one["breakdown"]["checks"]["events_sha1"], two["breakdown"]["checks"]["events_sha1"]

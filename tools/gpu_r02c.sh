@@ -4,6 +4,8 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_dist.py -x -v --timeout 250 --timeout-method thread > gpurun_out/pytest_dist.log 2>&1 || { tail -60 gpurun_out/pytest_dist.log; exit 1; }
+tail -3 gpurun_out/pytest_dist.log
 timeout -k 10 600 python -u -m pytest tests/test_gpu_scan_long.py -x -v -s --timeout 200 --timeout-method thread > gpurun_out/pytest_long.log 2>&1 || { tail -80 gpurun_out/pytest_long.log; exit 1; }
 grep -E "PASS|FAIL|carried segment" gpurun_out/pytest_long.log | tail -30
 timeout -k 10 600 python -u -m pytest tests/test_gpu_predict.py tests/test_gpu_scan.py tests/test_gpu_scan_batches.py tests/test_gpu_controller.py tests/test_gpu_configs.py -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_scan.log 2>&1 || { tail -40 gpurun_out/pytest_scan.log; exit 1; }
