@@ -437,6 +437,7 @@ __device__ __forceinline__ void cf_segment(const Seg& sg, int64_t blk, int64_t n
 // partition start 16-byte aligned (ld % 64 == 0, windows start on batches of a multiple
 // of 4 rows) and ld covers every row a clamped lane may read.
 constexpr int kVecRows = 4;
+constexpr int kVecChunk = 4;     // slots per load chunk (8 held 166 VGPRs: 3 waves per SIMD)
 
 template <int kVR>
 __device__ __forceinline__ void cf_segment_vec(const Seg& sg, int64_t blk, int64_t nblk, int pb, unsigned char* smem) {
@@ -474,13 +475,13 @@ __device__ __forceinline__ void cf_segment_vec(const Seg& sg, int64_t blk, int64
         const int64_t r = gt0 + q0 - sg.row_base;
         return (q0 < tile && r <= last_row) ? r : last_row;
     };
-    auto load_chunk = [&](int c, int64_t row, float4 (&xc)[kChunk]) {
+    auto load_chunk = [&](int c, int64_t row, float4 (&xc)[kVecChunk]) {
 #pragma unroll
-        for (int k = 0; k < kChunk; ++k) xc[k] = *reinterpret_cast<const float4*>(s_colp[c + k] + row);
+        for (int k = 0; k < kVecChunk; ++k) xc[k] = *reinterpret_cast<const float4*>(s_colp[c + k] + row);
     };
-    float4 xa[kChunk], xb[kChunk];
+    float4 xa[kVecChunk], xb[kVecChunk];
 #pragma unroll
-    for (int k = 0; k < kChunk; ++k) xa[k] = xb[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < kVecChunk; ++k) xa[k] = xb[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     int4 ynext = make_int4(0, 0, 0, 0);
     int64_t g0 = sg.pos_begin + blk * tile;
     __syncthreads();                                // column pointers, tables
@@ -501,12 +502,12 @@ __device__ __forceinline__ void cf_segment_vec(const Seg& sg, int64_t blk, int64
 #pragma unroll
             for (int j = 0; j < kVR; ++j) votes[i][j] = base_votes[j];
         // ---- row phase
-        for (int c = 0; c < U; c += kChunk) {
-            if (c + kChunk < U) load_chunk(c + kChunk, row, xb);
+        for (int c = 0; c < U; c += kVecChunk) {
+            if (c + kVecChunk < U) load_chunk(c + kVecChunk, row, xb);
             else if (has_next) load_chunk(0, nrow, xb);
             const ddm_cforest_slot* sc = slots + c;
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) {
+            for (int k = 0; k < kVecChunk; ++k) {
                 const int n4 = ldu(&sc[k].n4);
                 if (n4 > 0) {
                     const float xv[kVecRows] = {xa[k].x, xa[k].y, xa[k].z, xa[k].w};
@@ -530,7 +531,7 @@ __device__ __forceinline__ void cf_segment_vec(const Seg& sg, int64_t blk, int64
                 }
             }
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) xa[k] = xb[k];
+            for (int k = 0; k < kVecChunk; ++k) xa[k] = xb[k];
         }
         const int yl[kVecRows] = {yv.x, yv.y, yv.z, yv.w};
         uint32_t e4 = 0;
