@@ -13,6 +13,7 @@
 // DDM_Process.py:190), streams back to back; events are int32 pairs per batch.
 #include "common.h"
 #include "det.h"
+#include "wave_det.h"
 
 namespace {
 
@@ -576,6 +577,19 @@ __global__ __launch_bounds__(256) void k_scan_batches_list(int64_t n_streams, in
     }
 }
 
+// Flag byte of a batch (k_scan_batches_spec -> k_scan_batches_fix): bit 0 change, bit 1
+// any event, bit 2 end state stored (pend), and what a TRIVIAL carried detector (every
+// error so far 0, gate passed) makes of the batch, without its bytes: bit 5 no error at
+// all (it stays trivial), bit 3 an error in row 0 or 1 (the change is that row; bit 4:
+// row 1), else the change is the batch's first error row, as the fresh speculation found.
+constexpr uint8_t kFlagLead01 = 8, kFlagLeadRow1 = 16, kFlagNoError = 32;
+
+__device__ __forceinline__ uint8_t lead_bits(uint64_t m0, uint64_t m1) {
+    if ((m0 | m1) == 0) return kFlagNoError;
+    if (m0 & 3ull) return (uint8_t)(kFlagLead01 | ((m0 & 1ull) ? 0 : kFlagLeadRow1));
+    return 0;
+}
+
 // Per-wave LDS queue of the batches that need exact rows (mask + batch), see below.
 constexpr int kSpecQ = 256;
 constexpr bool kSpecPrefetch = false;   // next fill's bytes ahead (36 VGPRs; measured no gain)
@@ -633,7 +647,7 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
         const int w = wp < 0 ? -1 : (kPmap ? (int)pmap[bstart + wp] : wp);
         const int cp = chg ? (kPmap ? (int)pmap[bstart + c] : c) : -1;
         ev[item] = make_int2(w, cp);
-        flags[fpos] = (uint8_t)((chg ? 1 : 0) | ((chg || wp >= 0) ? 2 : 0));
+        flags[fpos] = (uint8_t)((chg ? 1 : 0) | ((chg || wp >= 0) ? 2 : 0) | lead_bits(m0, m1));
         if (!chg) need[sid] = 1u;
     };
 
@@ -715,7 +729,7 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
                         flags[fpos] = 3;
                     } else {
                         ev[it] = make_int2(-1, -1);
-                        flags[fpos] = 0;
+                        flags[fpos] = kFlagNoError;
                         need[sid] = 1u;
                     }
                 } else {
@@ -785,7 +799,7 @@ __global__ __launch_bounds__(kSpecThreads) void k_scan_batches_spec(
                     e[0] = make_double2(d.p, d.s);
                     e[1] = make_double2(d.pmin, d.smin);
                     e[2] = make_double2(d.psmin, (double)(2 * d.n + (r == 1 ? 1 : 0)));
-                    flags[fpos] = (uint8_t)(((wpos >= 0) ? 2 : 0) | 4);
+                    flags[fpos] = (uint8_t)(((wpos >= 0) ? 2 : 0) | 4 | lead_bits(m0, m1));
                 }
                 busy = false;
             }
@@ -832,27 +846,40 @@ constexpr int kFixThreads = 256;
 
 // One 64-batch window of flag bytes as bit masks: bit 0 of each byte (change) into the
 // result, bit 2 (end state stored) into sm, bit 1 (event) into em.
+// bits [i, i + 64) of the 128-bit mask (a0 | a1 << 64), i < 64
+__device__ __forceinline__ uint64_t m0_shift(uint64_t a0, uint64_t a1, int i) {
+    return i == 0 ? a0 : (a0 >> i) | (a1 << (64 - i));
+}
+
+struct LeadMasks {           // flag bits 3, 4, 5 of a 64-batch window as bit masks
+    uint64_t l01, row1, none;
+};
+
 __device__ __forceinline__ uint64_t change_window(const uint8_t* __restrict__ fl, int64_t wbase, int64_t nb,
-                                                  uint64_t& sm, uint64_t& em) {
-    uint64_t m = 0, ms = 0, me = 0;
+                                                  uint64_t& sm, uint64_t& em, LeadMasks& lm) {
+    uint64_t m = 0, ms = 0, me = 0, ml = 0, mr = 0, mz = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const uint4 v = *reinterpret_cast<const uint4*>(fl + wbase + 16 * q);
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t b = w[k] & 0x01010101u;
-            const uint32_t bs = (w[k] >> 2) & 0x01010101u;
-            const uint32_t be = (w[k] >> 1) & 0x01010101u;
-            m |= (uint64_t)(((b * 0x00204081u) >> 21) & 0xfu) << (16 * q + 4 * k);
-            ms |= (uint64_t)(((bs * 0x00204081u) >> 21) & 0xfu) << (16 * q + 4 * k);
-            me |= (uint64_t)(((be * 0x00204081u) >> 21) & 0xfu) << (16 * q + 4 * k);
+            const int sh = 16 * q + 4 * k;
+            m |= (uint64_t)(((((w[k] >> 0) & 0x01010101u) * 0x00204081u) >> 21) & 0xfu) << sh;
+            me |= (uint64_t)(((((w[k] >> 1) & 0x01010101u) * 0x00204081u) >> 21) & 0xfu) << sh;
+            ms |= (uint64_t)(((((w[k] >> 2) & 0x01010101u) * 0x00204081u) >> 21) & 0xfu) << sh;
+            ml |= (uint64_t)(((((w[k] >> 3) & 0x01010101u) * 0x00204081u) >> 21) & 0xfu) << sh;
+            mr |= (uint64_t)(((((w[k] >> 4) & 0x01010101u) * 0x00204081u) >> 21) & 0xfu) << sh;
+            mz |= (uint64_t)(((((w[k] >> 5) & 0x01010101u) * 0x00204081u) >> 21) & 0xfu) << sh;
         }
     }
     const int64_t valid = nb - wbase;
     const uint64_t vm = valid < 64 ? (1ull << valid) - 1 : ~0ull;
     sm = ms & vm;
     em = me & vm;
+    lm.l01 = ml & vm;
+    lm.row1 = mr & vm;
+    lm.none = mz & vm;
     return m & vm;
 }
 
@@ -862,6 +889,7 @@ __global__ __launch_bounds__(kFixThreads) void k_scan_batches_fix(
     int64_t* __restrict__ nev_out, const uint8_t* __restrict__ pmap, const int32_t* __restrict__ list,
     uint32_t* __restrict__ ctr, int refill, int open_thr, const double2* __restrict__ pend) {
     __shared__ double rcp[kRcpN];
+    __shared__ double s_nr[kFixThreads / 64][2][64];       // wave_tile scratch per wave
     for (int k = threadIdx.x; k < kRcpN; k += kFixThreads) rcp[k] = 1.0 / (double)(k > 0 ? k : 1);
     __syncthreads();
     const int64_t pb = P.per_batch;
@@ -873,13 +901,18 @@ __global__ __launch_bounds__(kFixThreads) void k_scan_batches_fix(
     const uint32_t n_list = __atomic_load_n(ctr, __ATOMIC_RELAXED);
     uint32_t claimed = 0;                           // wave-uniform: claims exhausted once >= n_list
 
-    enum { IDLE = 0, OPEN = 1, STEP = 2 };
+    enum { IDLE = 0, OPEN = 1, STEP = 2, COOP = 3 };
+    bool fin = false;                               // a COOP batch came back: finish it
+    int fin_cpos = -1;
+    double* const s_n = s_nr[threadIdx.x >> 6][0];
+    double* const s_r = s_nr[threadIdx.x >> 6][1];
     Det d;
     d.p = d.s = d.pmin = d.smin = d.psmin = 0.0;
     d.n = 1;
     d.chg = d.warn = 0;
     int64_t sid = 0, j = 0, wbase = 0, nev = 0, bstart = 0;
     uint64_t chg_m = 0, st_m = 0, ev_m = 0, m0 = 0, m1 = 0;
+    LeadMasks lm{0, 0, 0};
     int blen = 0, i = 0, wpos = -1, mode = IDLE;
     for (;;) {
         const uint64_t idle_m = __ballot(mode == IDLE);
@@ -899,7 +932,7 @@ __global__ __launch_bounds__(kFixThreads) void k_scan_batches_fix(
                     load_det(d, state[sid]);
                     j = 0;
                     wbase = 0;
-                    chg_m = nb > 0 ? change_window(flags + sid * nbp, 0, nb, st_m, ev_m) : 0;
+                    chg_m = nb > 0 ? change_window(flags + sid * nbp, 0, nb, st_m, ev_m, lm) : 0;
                     nev = 0;
                     mode = OPEN;
                 }
@@ -912,7 +945,25 @@ __global__ __launch_bounds__(kFixThreads) void k_scan_batches_fix(
                     if (j >= nb) break;
                     if (j >= wbase + 64) {          // next 64-batch window (nb > 64 only)
                         wbase = j & ~(int64_t)63;
-                        chg_m = change_window(flags + sid * nbp, wbase, nb, st_m, ev_m);
+                        chg_m = change_window(flags + sid * nbp, wbase, nb, st_m, ev_m, lm);
+                    }
+                    if (shortcuts && det_trivial(d)) {
+                        // a trivial detector (after a batch of zeros): the batch's flag
+                        // bits give its result without its bytes (see kFlagNoError)
+                        const int o = (int)(j - wbase);
+                        if ((lm.none >> o) & 1ull) {
+                            d.n += min(pb, L - j * pb);
+                            d.warn = 0;
+                        } else {
+                            if ((lm.l01 >> o) & 1ull) {     // the change is row 0 or 1
+                                const int t = (int)((lm.row1 >> o) & 1ull);
+                                ev[sid * nb + j] = make_int2(-1, pmap ? (int)pmap[sid * L + j * pb + t] : t);
+                            }                               // else: the speculative change stands
+                            ++nev;
+                            det_reset(d);
+                        }
+                        ++j;
+                        continue;
                     }
                     if (!det_fresh(d)) break;
                     const uint64_t rel = chg_m >> (j - wbase);
@@ -957,11 +1008,61 @@ __global__ __launch_bounds__(kFixThreads) void k_scan_batches_fix(
             continue;
         }
         if (!stepping) break;                       // all idle, claims exhausted
+        // Exact rows of a carried detector (rare, but a long carried chain is the whole
+        // kernel's tail when one lane steps it): the wave runs them for one lane at a time,
+        // the p chain once and everything else lane-parallel (wave_det.h)
+        uint64_t coop_m = __ballot(mode == COOP);
+        while (coop_m) {
+            const int ld = __builtin_ctzll(coop_m);
+            coop_m &= coop_m - 1;
+            Det c;
+            c.p = shfl_d(d.p, ld);
+            c.s = shfl_d(d.s, ld);
+            c.pmin = shfl_d(d.pmin, ld);
+            c.smin = shfl_d(d.smin, ld);
+            c.psmin = shfl_d(d.psmin, ld);
+            c.n = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(d.n >> 32), ld, 64) << 32) |
+                            (uint64_t)(uint32_t)__shfl((int)d.n, ld, 64));
+            c.chg = 0;
+            c.warn = __shfl(d.warn, ld, 64);
+            const uint64_t a0 = ((uint64_t)(uint32_t)__shfl((int)(m0 >> 32), ld, 64) << 32) |
+                                (uint64_t)(uint32_t)__shfl((int)m0, ld, 64);
+            const uint64_t a1 = ((uint64_t)(uint32_t)__shfl((int)(m1 >> 32), ld, 64) << 32) |
+                                (uint64_t)(uint32_t)__shfl((int)m1, ld, 64);
+            int ci = __shfl(i, ld, 64), cw = __shfl(wpos, ld, 64);
+            const int cb = __shfl(blen, ld, 64);
+            int cp = -1;
+            while (ci < cb) {
+                const int cnt = min(64, cb - ci);
+                const uint64_t m = ci < 64 ? ((m0_shift(a0, a1, ci))) : (a1 >> (ci - 64));
+                const TileOut to = wave_tile(c, m, cnt, min_inst, wl, cl, s_n, s_r);
+                const uint64_t upto = to.last >= 63 ? ~0ull : ((1ull << (to.last + 1)) - 1);
+                const uint64_t wb = to.warn & upto;
+                if (cw < 0 && wb) cw = ci + __builtin_ctzll(wb);
+                if (to.kc >= 0) {
+                    cp = ci + to.kc;
+                    break;
+                }
+                ci += cnt;
+            }
+            if (lane == ld) {
+                d = c;
+                i = cp >= 0 ? cp + 1 : cb;
+                wpos = cw;
+                fin = true;
+                fin_cpos = cp;
+                mode = STEP;
+            }
+        }
         if (mode != STEP) continue;
+        int cpos = -1;
+        if (fin) {                                  // a batch the wave finished for this lane
+            fin = false;
+            cpos = fin_cpos;
+        } else {
         // one step of the rescan of batch j
         const int xi = mask_bit(m0, m1, i);
         const bool triv = det_trivial(d);
-        int cpos = -1;
         if (shortcuts && !triv && i + 1 < blen && det_fresh(d) && xi == 0 && mask_bit(m0, m1, i + 1) == 0) {
             d.p = d.s = d.pmin = d.smin = d.psmin = 0.0;
             d.n = 3;
@@ -976,20 +1077,9 @@ __global__ __launch_bounds__(kFixThreads) void k_scan_batches_fix(
             cpos = i;
             ++i;
         } else {
-            // exact rows until a change or the end of the batch, in one tight loop: the long
-            // carried chains (a detector that stays unchanged batch after batch) are the
-            // tail of this kernel, and the shortcuts above are exact equivalents only
-            for (int x = xi;;) {
-                det_add_fast(d, x, min_inst, wl, cl, rcp);
-                if (d.warn && wpos < 0) wpos = i;
-                ++i;
-                if (d.chg) {
-                    cpos = i - 1;
-                    break;
-                }
-                if (i >= blen) break;
-                x = mask_bit(m0, m1, i);
-            }
+            mode = COOP;                            // exact rows: the wave runs them (above)
+            continue;
+        }
         }
         if (cpos >= 0 || i >= blen) {
             int w = wpos, c = cpos;

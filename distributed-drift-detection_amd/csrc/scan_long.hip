@@ -27,6 +27,7 @@
 // same `<=` arg-min and the same `elif` between change and warning.
 #include "common.h"
 #include "det.h"
+#include "wave_det.h"
 
 namespace {
 
@@ -41,27 +42,6 @@ struct Carry {                 // a chunk's inclusive state (look-back record)
     int64_t stop;              // batch of the (mode 0) change or -1
 };
 
-__device__ __forceinline__ double readlane_d(double v, int k) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)b, k);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
-    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
-}
-
-__device__ __forceinline__ double shfl_d(double v, int src) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __shfl((int)b, src, 64);
-    const int hi = __shfl((int)(b >> 32), src, 64);
-    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
-}
-
-__device__ __forceinline__ double shfl_up_d(double v, int d) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __shfl_up((int)b, d, 64);
-    const int hi = __shfl_up((int)(b >> 32), d, 64);
-    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
-}
-
 __global__ __launch_bounds__(64) void k_scan_long(
     const uint8_t* __restrict__ err, const int64_t* __restrict__ off, const int64_t* __restrict__ stream_end,
     int64_t n_streams, int64_t n_chunks, ddm_params P, ddm_state* __restrict__ state,
@@ -71,6 +51,7 @@ __global__ __launch_bounds__(64) void k_scan_long(
     __shared__ uint4 sbytes[kLongChunkMax / 16 + 1];
     __shared__ uint64_t smask[kLongChunkMax / 64];
     __shared__ int2 sev[64];
+    __shared__ double s_n[64], s_r[64];
     __shared__ uint32_t stk;
     const int lane = threadIdx.x;
     if (lane == 0) stk = atomicAdd(ticket, 1u);
@@ -161,50 +142,13 @@ __global__ __launch_bounds__(64) void k_scan_long(
         uint64_t m = smask[tile] >> sh;
         if (sh && tile + 1 < ntiles) m |= smask[tile + 1] << (64 - sh);
         if (cnt < 64) m &= (1ull << cnt) - 1;
-        if (det_trivial(d) && m == 0) {                        // zeros in the trivial state
-            d.n += cnt;
-            d.warn = 0;
+        const TileOut to = wave_tile(d, m, cnt, min_inst, wl, cl, s_n, s_r);
+        const int kc = to.kc, last = to.last;
+        const uint64_t W_ = to.warn;
+        if (kc < 0 && W_ == 0) {                               // no event in the tile
             pos += cnt;
             continue;
         }
-        // p chain: every lane runs it (the wave issues once either way); lane k keeps p_k
-        const double nd = (double)d.n;
-        const double nl = nd + (double)lane;                   // divisor of row pos + lane
-        const double rl = 1.0 / nl;                            // RN(1/n), as rcp[] / 1.0/n in det.h
-        double p = d.p, myp = 0.0;
-        for (int k = 0; k < cnt; ++k) {
-            const double x = (double)((m >> k) & 1ull);
-            const double nk = readlane_d(nl, k), rk = readlane_d(rl, k);
-            p = p + div_rn(x - p, nk, rk);
-            myp = lane == k ? p : myp;
-        }
-        // lane-parallel part of rows pos .. pos + cnt - 1
-        const bool valid = lane < cnt;
-        const double s = sqrt_q(div_rn(myp * (1.0 - myp), nl, rl));
-        const bool gated = valid && (d.n + lane + 1 >= (int64_t)min_inst);
-        const double ps = myp + s;
-        // inclusive arg-min scan of ps over gated rows, later row on ties
-        double mps = gated ? ps : __builtin_huge_val();
-        int midx = gated ? lane : -1;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const double ops = shfl_up_d(mps, o);
-            const int oidx = __shfl_up(midx, o, 64);
-            if (lane >= o && oidx >= 0 && (midx < 0 || !(mps <= ops))) {
-                mps = ops;
-                midx = oidx;
-            }
-        }
-        const bool from_lane = midx >= 0 && mps <= d.psmin;
-        const int src = midx >= 0 ? midx : 0;
-        const double lp = shfl_d(myp, src), ls = shfl_d(s, src);
-        const double pm = from_lane ? lp : d.pmin, sm = from_lane ? ls : d.smin;
-        const double psm = from_lane ? mps : d.psmin;
-        const bool chg = gated && ps > pm + cl * sm;
-        const bool wrn = gated && !chg && ps > pm + wl * sm;
-        const uint64_t C_ = __ballot(chg), W_ = __ballot(wrn);
-        const int kc = C_ ? __builtin_ctzll(C_) : -1;
-        const int last = kc >= 0 ? kc : cnt - 1;                // last committed row of the tile
         // first warning of each batch the committed rows touch
         uint64_t wcommit = kc >= 0 ? (W_ & ((kc ? (~0ull >> (64 - kc)) : 0ull))) : W_;
         if (lane == 0) {
@@ -224,15 +168,6 @@ __global__ __launch_bounds__(64) void k_scan_long(
             }
         }
         __syncthreads();
-        // the detector after the last committed row
-        d.p = shfl_d(myp, last);
-        d.s = shfl_d(s, last);
-        d.pmin = shfl_d(pm, last);
-        d.smin = shfl_d(sm, last);
-        d.psmin = shfl_d(psm, last);
-        d.n += last + 1;
-        d.chg = kc >= 0;
-        d.warn = (int)((W_ >> last) & 1ull);
         if (kc >= 0) {
             const int64_t rr = c0 - lo + pos + kc;
             if (mode == 0) {

@@ -1,0 +1,97 @@
+// Wave-cooperative exact DDM rows (used by scan_long.hip and the fix-up of ddm_scan.hip).
+//
+// run_DDM's detector (det.h, DDM_Process.py:135-159) over a tile of up to 64 rows whose
+// error bits are m, by all 64 lanes of a wave holding the same detector:
+//   * the p recurrence p += (x - p) / n is the only sequential part: the wave runs it once
+//     (5 dependent fp64 operations per row; n and RN(1/n) of every row come from LDS by
+//     broadcast reads issued ahead of the chain), and lane k keeps p_k;
+//   * s_k, the running arg-min of p + s (an inclusive wave scan, the later row on ties: the
+//     reference's `<=`), the change and warning tests and their ballots are lane-parallel.
+// The detector comes back as it stands after the last committed row: the first change,
+// or the tile's last row.  Bit for bit the sequential det_add_fast.
+#pragma once
+#include "det.h"
+
+namespace {
+
+__device__ __forceinline__ double shfl_d(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __shfl((int)b, src, 64);
+    const int hi = __shfl((int)(b >> 32), src, 64);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+__device__ __forceinline__ double shfl_up_d(double v, int d) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __shfl_up((int)b, d, 64);
+    const int hi = __shfl_up((int)(b >> 32), d, 64);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+struct TileOut {
+    int kc;          // first change row of the tile or -1
+    int last;        // last committed row (kc, or cnt - 1)
+    uint64_t warn;   // rows with in_warning_zone set (committed rows only are meaningful)
+};
+
+// s_n, s_r: this wave's 64-double LDS scratch each.  d must be uniform over the wave and
+// not in a pending change (the caller resets it first); rows >= cnt are ignored.
+__device__ __forceinline__ TileOut wave_tile(Det& d, uint64_t m, int cnt, int min_inst, double wl, double cl,
+                                             double* s_n, double* s_r) {
+    const int lane = threadIdx.x & 63;
+    if (cnt < 64) m &= (1ull << cnt) - 1;
+    if (det_trivial(d) && m == 0) {                 // zeros in the trivial state: only n moves
+        d.n += cnt;
+        d.warn = 0;
+        return {-1, cnt - 1, 0ull};
+    }
+    const double nl = (double)d.n + (double)lane;   // divisor of row lane
+    const double rl = 1.0 / nl;                     // RN(1/n), as det_add_fast's rcp[] / 1.0 / n
+    s_n[lane] = nl;
+    s_r[lane] = rl;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double p = d.p, myp = 0.0;
+#pragma unroll 8
+    for (int k = 0; k < cnt; ++k) {
+        const double x = (double)((m >> k) & 1ull);
+        p = p + div_rn(x - p, s_n[k], s_r[k]);
+        myp = lane == k ? p : myp;
+    }
+    const double s = sqrt_q(div_rn(myp * (1.0 - myp), nl, rl));
+    const bool gated = lane < cnt && (d.n + lane + 1 >= (int64_t)min_inst);
+    const double ps = myp + s;
+    double mps = gated ? ps : __builtin_huge_val();
+    int midx = gated ? lane : -1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double ops = shfl_up_d(mps, o);
+        const int oidx = __shfl_up(midx, o, 64);
+        if (lane >= o && oidx >= 0 && (midx < 0 || !(mps <= ops))) {
+            mps = ops;
+            midx = oidx;
+        }
+    }
+    const bool from_lane = midx >= 0 && mps <= d.psmin;
+    const int src = midx >= 0 ? midx : 0;
+    const double lp = shfl_d(myp, src), ls = shfl_d(s, src);
+    const double pm = from_lane ? lp : d.pmin, sm = from_lane ? ls : d.smin;
+    const double psm = from_lane ? mps : d.psmin;
+    const bool chg = gated && ps > pm + cl * sm;
+    const bool wrn = gated && !chg && ps > pm + wl * sm;
+    const uint64_t C = __ballot(chg), W = __ballot(wrn);
+    const int kc = C ? __builtin_ctzll(C) : -1;
+    const int last = kc >= 0 ? kc : cnt - 1;
+    d.p = shfl_d(myp, last);
+    d.s = shfl_d(s, last);
+    d.pmin = shfl_d(pm, last);
+    d.smin = shfl_d(sm, last);
+    d.psmin = shfl_d(psm, last);
+    d.n += last + 1;
+    d.chg = kc >= 0;
+    d.warn = (int)((W >> last) & 1ull);
+    return {kc, last, W};
+}
+
+}  // namespace
