@@ -966,6 +966,18 @@ __global__ __launch_bounds__(kFixThreads) void k_scan_batches_fix(
                         continue;
                     }
                     if (!det_fresh(d)) break;
+                    if (shortcuts && ((lm.none >> (j - wbase)) & 1ull)) {
+                        // a fresh detector and a batch without an error: two zeros make it
+                        // trivial (n = 3), the rest only move n (no bytes needed)
+                        const int bl = (int)min(pb, L - j * pb);
+                        if (bl >= 2) {
+                            d.p = d.s = d.pmin = d.smin = d.psmin = 0.0;
+                            d.n = 1 + bl;
+                            d.chg = d.warn = 0;
+                            ++j;
+                            continue;
+                        }
+                    }
                     const uint64_t rel = chg_m >> (j - wbase);
                     const int run = (int)min((int64_t)(rel == ~0ull ? 64 : __builtin_ctzll(~rel)), wbase + 64 - j);
                     if (run == 0) {
