@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--features", type=int, default=27)
     ap.add_argument("--refit", default="device", choices=["device", "native", "sklearn"])
     ap.add_argument("--fit-threads", type=int, default=16, help="host threads for native refits")
+    ap.add_argument("--groups", type=int, default=2,
+                    help="partition groups per GPU, each on its own epoch stream and host thread (pipelined)")
     ap.add_argument("--seed", type=int, default=SEED)
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-procs", type=int, default=8, help="CPU baseline worker processes (P)")
@@ -228,7 +230,7 @@ def oracle_prefix_check(part, n, seed, got):
 def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     import numpy as np
     from ddm_amd import synth
-    from ddm_amd.controller import BatchRunner, RunStats
+    from ddm_amd.controller import BatchRunner, GroupedRunner, RunStats
     from ddm_amd.params import DDMSettings
     from ddm_amd.rng import MTStream
     P = args.parts
@@ -257,8 +259,13 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     gather_s = [0.0]
     if not parts:
         raise RuntimeError(f"rank {rank} owns no partition ({instances} partitions over {world} GPUs)")
-    runner = BatchRunner([p for _, p in parts], DDMSettings(), torch.cuda.Stream(dev, priority=-1),
-                         refit=args.refit, timing=True, fit_threads=args.fit_threads)
+    if args.groups > 1 and len(parts) > 1:
+        # partition groups pipelined on their own epoch streams and host threads
+        runner = GroupedRunner([p for _, p in parts], DDMSettings(), groups=args.groups, refit=args.refit,
+                               timing=True, fit_threads=args.fit_threads)
+    else:
+        runner = BatchRunner([p for _, p in parts], DDMSettings(), torch.cuda.Stream(dev, priority=-1),
+                             refit=args.refit, timing=True, fit_threads=args.fit_threads)
     torch.cuda.synchronize()
 
     def step():
@@ -337,8 +344,9 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
             "partitions": instances, "partitions_this_rank": len(parts),
             "solo_share_of_gpus": gpus if gpus != world else None,
             "refit": "ddm_rf_fit_device (sklearn 1.7.2 RandomForestClassifier restated, identical trees) on the GPU",
-            "execution": "all partitions of a GPU in lockstep epochs (BatchRunner): one batched shuffle, predict, "
-                         "scan, stage and refit launch per epoch"}
+            "execution": (f"the GPU's partitions in {min(args.groups, len(parts))} groups (GroupedRunner), each in "
+                          "lockstep epochs on its own stream and host thread: one batched shuffle, predict, scan, "
+                          "stage and refit launch per group epoch")}
     extra = {"drifts_per_step": drifts, "warnings_per_step": warns,
              "refits_per_step": agg["refits"] / args.steps, "epochs_per_step": agg["epochs"] / args.steps,
              "refits_per_s": agg["refits"] / elapsed,

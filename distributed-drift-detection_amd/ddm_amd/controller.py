@@ -201,7 +201,8 @@ class BatchRunner:
     partitions that drifted in an epoch are one call: every tree on a pool of
     `fit_threads` host threads."""
 
-    def __init__(self, parts, settings=None, stream=None, refit="device", timing=False, fit_threads=8):
+    def __init__(self, parts, settings=None, stream=None, refit="device", timing=False, fit_threads=8,
+                 gen_stream=None, tab_stream=None):
         self.parts = list(parts)
         if not self.parts:
             raise ValueError("no partitions")
@@ -314,10 +315,10 @@ class BatchRunner:
                       if timing and refit == "device" else None)
         # the partitions' MT19937 streams are generated and tabulated on a side stream, in
         # pieces, while the epochs run (GpuShuffle.wait_for orders the consumers)
-        self.gen_stream = torch.cuda.Stream(dev)
+        self.gen_stream = gen_stream or torch.cuda.Stream(dev)
         # tables on a stream of their own: the generator (8 workgroups, one sequential
         # recurrence per partition) never waits for a piece's tables before the next piece
-        self.tab_stream = torch.cuda.Stream(dev)
+        self.tab_stream = tab_stream or torch.cuda.Stream(dev)
         self.gen_tables = []
         # pinned staging per partition: [0] batch-j shuffle of a refit epoch, [1] short last
         # batch, [2] drift batch's shuffle read back
@@ -640,6 +641,10 @@ class BatchRunner:
                 ns = self.shuffles[ps.i].numpy_state(ps.P)
                 rngs[ps.i].key[:] = ns[1]
                 rngs[ps.i].pos.value = ns[2]
+            # pieces of the streams may still be generated / tabulated ahead on the side
+            # streams: nothing may write into this runner's buffers once the caller can free them
+            self.gen_stream.synchronize()
+            self.tab_stream.synchronize()
 
     def _epoch(self, live):
         s, st, pb, stream = self.s, self.stats, self.s.per_batch, self.stream
@@ -843,6 +848,89 @@ class BatchRunner:
             if ps.j >= ps.nb:
                 ps.done = True
         st.host_s += host + time.perf_counter() - t2
+
+
+class GroupedRunner:
+    """The partitions of one GPU in `groups` BatchRunners, each on its own epoch stream and
+    driven by its own host thread, sharing the generation and table streams.  An epoch of
+    one group is host work (refit inputs, window tables) and a chain of small kernels; with
+    two groups the GPU runs one group's kernels while the host prepares the other's, and
+    the two groups' small kernels run side by side.  Results are those of one BatchRunner
+    over all partitions (partitions are independent, DDM_Process.py:226)."""
+
+    def __init__(self, parts, settings=None, groups=2, refit="device", timing=False, fit_threads=8):
+        parts = list(parts)
+        if not parts:
+            raise ValueError("no partitions")
+        dev = parts[0].device
+        g = max(1, min(int(groups), len(parts)))
+        # balance rows: partitions in decreasing size, each to the lightest group
+        order = sorted(range(len(parts)), key=lambda k: -parts[k].n)
+        self.members = [[] for _ in range(g)]
+        load = [0] * g
+        for k in order:
+            t = load.index(min(load))
+            self.members[t].append(k)
+            load[t] += parts[k].n
+        self.gen_stream, self.tab_stream = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        self.runners = [BatchRunner([parts[k] for k in m], settings, torch.cuda.Stream(dev, priority=-1), refit,
+                                    timing, max(1, fit_threads // g), self.gen_stream, self.tab_stream)
+                        for m in self.members]
+        from concurrent.futures import ThreadPoolExecutor
+        self._pool = ThreadPoolExecutor(g) if g > 1 else None
+        self.n = len(parts)
+
+    def run(self, rngs):
+        if len(rngs) != self.n:
+            raise ValueError("one MT19937 stream per partition")
+        jobs = [(r, [rngs[k] for k in m]) for r, m in zip(self.runners, self.members)]
+        if self._pool is None:
+            outs = [r.run(x) for r, x in jobs]
+        else:
+            outs = list(self._pool.map(lambda a: a[0].run(a[1]), jobs))
+        res = [None] * self.n
+        for m, o in zip(self.members, outs):
+            for k, v in zip(m, o):
+                res[k] = v
+        return res
+
+    @property
+    def stats(self):
+        agg = RunStats()
+        for r in self.runners:
+            for k in RunStats.__slots__:
+                setattr(agg, k, getattr(agg, k) + getattr(r.stats, k))
+        return agg
+
+    @stats.setter
+    def stats(self, value):
+        for r in self.runners:
+            r.stats = RunStats()
+
+    @property
+    def predict_log(self):
+        logs = [r.predict_log for r in self.runners]
+        return None if all(x is None for x in logs) else [e for x in logs if x for e in x]
+
+    @predict_log.setter
+    def predict_log(self, value):
+        for r in self.runners:
+            r.predict_log = None if value is None else []
+
+    def replay_predict(self, repeats=1):
+        tot, n = 0.0, 0
+        for r in self.runners:
+            ms, k = r.replay_predict(repeats)
+            tot += ms * k
+            n += k
+        return (tot / n if n else 0.0), n
+
+    def close(self):
+        for r in self.runners:
+            r.close()
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
+            self._pool = None
 
 
 class PartitionRunner(BatchRunner):

@@ -49,7 +49,10 @@ class PinnedTable:
         self.dtype, self.n = dtype, int(n)
         nbytes = max(1, self.n) * dtype.itemsize
         self.h = torch.zeros(nbytes, dtype=torch.uint8, pin_memory=True) if h is None else h[:nbytes]
-        self.d = torch.zeros(nbytes, dtype=torch.uint8, device=device) if d is None else d[:nbytes]
+        # no fill on the device side: every table is uploaded before a kernel reads it, and a
+        # fill kernel on the caller's stream would not be ordered with the stream that
+        # uploads and reads the table
+        self.d = torch.empty(nbytes, dtype=torch.uint8, device=device) if d is None else d[:nbytes]
         self.rec = self.h.numpy().view(dtype)
 
     def upload(self, count, stream):

@@ -160,9 +160,9 @@ class GpuShuffle:
         self.gen_stream.synchronize()       # nothing of the previous run may still read R
         self.tab_stream.synchronize()
         self.n_seg = self._segments_for(self.cap)
-        if getattr(self, "seg", None) is None or self.seg.shape[0] < self.n_seg:
-            self.seg = torch.zeros((self.n_seg, 640), dtype=torch.int32, device=self.device)
-        with torch.cuda.stream(self.gen_stream):
+        with torch.cuda.stream(self.gen_stream):   # allocated, filled and read on gen_stream
+            if getattr(self, "seg", None) is None or self.seg.shape[0] < self.n_seg:
+                self.seg = torch.zeros((self.n_seg, 640), dtype=torch.int32, device=self.device)
             self.mt.copy_(torch.from_numpy(st.view(np.int32)))
             self.seg[0, :625].copy_(self.mt)
         self.jumped = 1                     # segments whose start state exists
@@ -199,8 +199,9 @@ class GpuShuffle:
             return
         if n_seg > self.seg.shape[0]:
             torch.cuda.synchronize(self.device)
-            seg = torch.zeros((2 * n_seg, 640), dtype=torch.int32, device=self.device)
-            seg[:self.seg.shape[0]].copy_(self.seg)
+            with torch.cuda.stream(self.gen_stream):   # before the jumps and generation that read it
+                seg = torch.zeros((2 * n_seg, 640), dtype=torch.int32, device=self.device)
+                seg[:self.seg.shape[0]].copy_(self.seg)
             self.seg = seg
         nj = n_seg - self.jumped
         if self.jump_scratch is None or self.jump_scratch.shape[0] < nj:

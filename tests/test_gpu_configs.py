@@ -87,17 +87,18 @@ def test_c5_refit_heavy_vs_oracle(flip, parts_run):
 
 
 def test_c3_full_size_property_on_bench_path():
-    """configs[2] at 8 x 12.5M rows (global class blocks of 1,000,037 rows): exactly one
-    drift per class boundary, in the batch holding it, no warning."""
+    """configs[2] at 8 x 12.5M rows (global class blocks of 1,000,037 rows), through the
+    GroupedRunner the bench times: exactly one drift per class boundary, in the batch holding
+    it, no warning."""
     import bench
     from ddm_amd import synth
-    from ddm_amd.controller import BatchRunner
+    from ddm_amd.controller import GroupedRunner
     from ddm_amd.params import DDMSettings
     from ddm_amd.rng import MTStream
     dev = _dev()
     n, P, block = 12_500_000, 8, 1_000_037
     parts = [synth.block_partition(n, d, P, block, 20261015, dev) for d in range(P)]
-    runner = BatchRunner(parts, DDMSettings(), torch.cuda.Stream(dev, priority=-1), timing=True, fit_threads=16)
+    runner = GroupedRunner(parts, DDMSettings(), groups=2, timing=True, fit_threads=16)   # as bench.py runs it
     outs = runner.run([MTStream.from_seed(20261015 + d) for d in range(P)])
     runner.close()
     res = dict(enumerate(outs))
