@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--features", type=int, default=27)
     ap.add_argument("--refit", default="device", choices=["device", "native", "sklearn"])
     ap.add_argument("--fit-threads", type=int, default=16, help="host threads for native refits")
-    ap.add_argument("--groups", type=int, default=2,
+    ap.add_argument("--groups", type=int, default=1,
                     help="partition groups per GPU, each on its own epoch stream and host thread (pipelined)")
     ap.add_argument("--seed", type=int, default=SEED)
     ap.add_argument("--cpu-baseline", type=int, default=1)
@@ -346,7 +346,9 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
             "refit": "ddm_rf_fit_device (sklearn 1.7.2 RandomForestClassifier restated, identical trees) on the GPU",
             "execution": (f"the GPU's partitions in {min(args.groups, len(parts))} groups (GroupedRunner), each in "
                           "lockstep epochs on its own stream and host thread: one batched shuffle, predict, scan, "
-                          "stage and refit launch per group epoch")}
+                          "stage and refit launch per group epoch" if min(args.groups, len(parts)) > 1 else
+                          "all partitions of the GPU in lockstep epochs (BatchRunner): one batched shuffle, predict, "
+                          "scan, stage and refit launch per epoch")}
     extra = {"drifts_per_step": drifts, "warnings_per_step": warns,
              "refits_per_step": agg["refits"] / args.steps, "epochs_per_step": agg["epochs"] / args.steps,
              "refits_per_s": agg["refits"] / elapsed,

@@ -856,7 +856,11 @@ class GroupedRunner:
     one group is host work (refit inputs, window tables) and a chain of small kernels; with
     two groups the GPU runs one group's kernels while the host prepares the other's, and
     the two groups' small kernels run side by side.  Results are those of one BatchRunner
-    over all partitions (partitions are independent, DDM_Process.py:226)."""
+    over all partitions (partitions are independent, DDM_Process.py:226).
+
+    Measured on one MI355X it does not pay where the GPU is the bottleneck: C3 141.6 ms
+    (1 group) vs 147-171 ms (2), C5 at 8M rows 2.65 vs 1.97 M rows/s (each group runs as
+    many epochs as the whole GPU did); the bench defaults to one group."""
 
     def __init__(self, parts, settings=None, groups=2, refit="device", timing=False, fit_threads=8):
         parts = list(parts)

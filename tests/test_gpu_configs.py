@@ -58,12 +58,12 @@ def test_c1_rialto_shaped_full_vs_oracle():
     assert (want[:, 2] >= 0).sum() >= 9
 
 
-@pytest.mark.parametrize("flip,parts_run", [(0.0, (0, 3)), (0.01, (6,))])
-def test_c5_refit_heavy_vs_oracle(flip, parts_run):
-    """C5-shaped partitions (20k rows each of an 8-partition stream) in ONE BatchRunner:
-    a drift and a device refit every one or two batches."""
+@pytest.mark.parametrize("flip,parts_run,groups", [(0.0, (0, 3), 1), (0.01, (6,), 1), (0.0, (1, 2, 5), 2)])
+def test_c5_refit_heavy_vs_oracle(flip, parts_run, groups):
+    """C5-shaped partitions (20k rows each of an 8-partition stream) in one BatchRunner, or
+    in a GroupedRunner of two threads: a drift and a device refit every one or two batches."""
     from ddm_amd import synth
-    from ddm_amd.controller import BatchRunner
+    from ddm_amd.controller import BatchRunner, GroupedRunner
     from ddm_amd.params import DDMSettings
     from ddm_amd.rng import MTStream
     from oracle.controller import run_partition
@@ -71,7 +71,7 @@ def test_c5_refit_heavy_vs_oracle(flip, parts_run):
     n = 20_000
     parts = [synth.jitter_partition(n, d, 8, 20261015, dev, flip=flip) for d in parts_run]
     host = [synth.host_copy(p) for p in parts]
-    runner = BatchRunner(parts, DDMSettings())
+    runner = BatchRunner(parts, DDMSettings()) if groups == 1 else GroupedRunner(parts, DDMSettings(), groups=groups)
     rngs = [MTStream.from_seed(9000 + d) for d in parts_run]
     got = runner.run(rngs)
     runner.close()
@@ -98,7 +98,7 @@ def test_c3_full_size_property_on_bench_path():
     dev = _dev()
     n, P, block = 12_500_000, 8, 1_000_037
     parts = [synth.block_partition(n, d, P, block, 20261015, dev) for d in range(P)]
-    runner = GroupedRunner(parts, DDMSettings(), groups=2, timing=True, fit_threads=16)   # as bench.py runs it
+    runner = GroupedRunner(parts, DDMSettings(), groups=1, timing=True, fit_threads=16)   # as bench.py runs it
     outs = runner.run([MTStream.from_seed(20261015 + d) for d in range(P)])
     runner.close()
     res = dict(enumerate(outs))
