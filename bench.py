@@ -272,6 +272,9 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
         outs = runner.run([MTStream.from_seed(args.seed + d) for d, _ in parts])
         for (d, _), o in zip(parts, outs):
             results[d] = o
+        if getattr(runner, "trace", None) and os.environ.get("DDM_HOST_TRACE_OUT"):
+            with open(os.environ["DDM_HOST_TRACE_OUT"], "w") as f:    # the last run's host phases
+                json.dump(runner.trace, f)
         if world > 1:
             # the collect of DDM_Process.py:258: the drift/warning positions of every
             # partition on every rank, one all_gather of the batches with an event

@@ -7,16 +7,18 @@
 // the host that chain is latency bound (~10 ns/row).  Here it is made parallel:
 //   1. k_mt_generate   one workgroup per partition emits the raw tempered stream R;
 //                      a 624-word block is regenerated in LDS in three barrier phases.
-//   2. k_fsm_sub       interval acceptance is a finite-state machine whose state is the
+//   2. k_fsm_prefix    interval acceptance is a finite-state machine whose state is the
 //                      interval index s in [1, L-1] (s == 1 accepted -> batch done,
-//                      s := L-1).  For every 128-draw sub-chunk and EVERY start state a
-//                      lane simulates the sub-chunk: table (end state, batches done).
-//   3. k_fsm_chunk     composes 64 sub-chunk tables into 8192-draw chunk tables.
-//   4. k_fsm_walk      one lane walks chunk tables from a window start (a batch
-//                      boundary at draw P) to find every chunk's start (state, batch).
-//   5. k_fsm_replay    one wave per chunk: lane 0 composes the sub-chunk tables, then
-//                      each lane replays its 128 draws and records, per batch, the j of
-//                      every interval and the draw that completes the batch.
+//                      s := L-1).  For every 8192-draw chunk and EVERY state it may be
+//                      entered in: the state and batches done after each of its 64
+//                      128-draw sub-chunks (prefix tables, coupled trajectories merged).
+//   3. k_fsm_first     per window: classic per-sub-chunk tables for the rest of the
+//                      chunk holding the window start P (entered mid-chunk).
+//   4. k_fsm_walk      one lane walks from P (draws, first-chunk tables, then chunk
+//                      tables) to find every piece's start (state, batch).
+//   5. k_fsm_replay    one wave per chunk piece: lane t takes sub-chunk t's start from
+//                      the prefix tables and replays its 128 draws, recording per batch
+//                      the j of every interval and the draw that completes the batch.
 //   6. k_fsm_perms     one lane per batch applies its L-1 swaps -> perm bytes in HBM.
 // Steps 2-3 depend only on the RNG stream (not on drifts), so they run once per stream
 // segment; 4-6 run per speculative window.  Tempering is invertible, so the host
@@ -107,79 +109,74 @@ __global__ __launch_bounds__(256) void k_mt_generate(uint32_t* __restrict__ stat
 // g(T) * key on the device.  T^i(key) is the window (x_i .. x_{i+623}) of the MT19937
 // word sequence that starts with key (x_{k+624} = f(x_k, x_{k+1}, x_{k+397})), so by
 // linearity g(T) * key = XOR over the set coefficients i of g of those windows:
-//   1. the sequence x_0 .. x_{623 + deg g} (untempered) is generated into scratch, a
-//      624-word block per three barrier phases;
-//   2. thread j accumulates out[j] = XOR_i x_{i+j} over the ~10k set bits of g (coalesced
-//      reads across the threads, the bit scan uniform).
+//   1. the sequence x_0 .. x_{623 + deg g} (untempered) is generated in LDS (85 KB: one
+//      workgroup per CU), a 624-word block per three barrier phases;
+//   2. thread j accumulates out[j] = XOR_i x_{i+j} over the ~10k set bits of g, every read
+//      an LDS read (consecutive threads, consecutive words: no bank conflict), so a jump
+//      costs ~10k x 2.5 KB of LDS bandwidth instead of as much L2 traffic.
 struct JumpJob {
     const uint32_t* key;
     const uint64_t* poly;
     uint32_t* out;
-    uint32_t* scratch;
+    uint32_t* scratch;   // unused (the sequence lives in LDS)
 };
 
-__global__ __launch_bounds__(256) void k_mt_jump(const JumpJob* __restrict__ jobs) {
+constexpr int kJumpThreads = 640;    // >= 624 outputs, a multiple of 64
+constexpr int kJumpZero = DDM_MT_JUMP_SCRATCH_WORDS;   // 624 zero words after the sequence
+
+__global__ __launch_bounds__(kJumpThreads) void k_mt_jump(const JumpJob* __restrict__ jobs) {
     __shared__ uint64_t P[DDM_MT_POLY_WORDS];
-    __shared__ uint32_t blk[2][kN];
+    __shared__ uint32_t x[DDM_MT_JUMP_SCRATCH_WORDS + kN];
     __shared__ int top_s;
     const JumpJob jb = jobs[blockIdx.x];
     const int t = threadIdx.x;
     if (t == 0) top_s = -1;
-    for (int k = t; k < DDM_MT_POLY_WORDS; k += 256) P[k] = jb.poly[k];
-    for (int k = t; k < kN; k += 256) {
-        blk[0][k] = jb.key[k];
-        jb.scratch[k] = jb.key[k];
-    }
+    for (int k = t; k < DDM_MT_POLY_WORDS; k += kJumpThreads) P[k] = jb.poly[k];
+    if (t < kN) x[t] = jb.key[t];
     __syncthreads();
-    for (int k = t; k < DDM_MT_POLY_WORDS; k += 256)
+    for (int k = t; k < DDM_MT_POLY_WORDS; k += kJumpThreads)
         if (P[k]) atomicMax(&top_s, 64 * k + 63 - __builtin_clzll(P[k]));
     __syncthreads();
     const int top = top_s;
-    // 1. x_624 .. x_{623 + top}: whole blocks
-    int cur = 0;
-    for (int64_t base = kN; base < kN + top; base += kN) {
-        const uint32_t* o = blk[cur];
-        uint32_t* w = blk[cur ^ 1];
-        if (t < 227) {
-            const uint32_t v = mt_word(o[t], o[t + 1], o[t + 397]);
-            w[t] = v;
-            jb.scratch[base + t] = v;
-        }
+    // 1. x_624 .. x_{623 + top}: whole blocks, x_k = f(x_{k-624}, x_{k-623}, x_{k-227})
+    for (int base = kN; base < kN + top; base += kN) {
+        if (t < 227) x[base + t] = mt_word(x[base + t - kN], x[base + t - kN + 1], x[base + t - 227]);
         __syncthreads();
         if (t < 227) {
-            const int i = 227 + t;
-            const uint32_t v = mt_word(o[i], o[i + 1], w[t]);
-            w[i] = v;
-            jb.scratch[base + i] = v;
+            const int i = base + 227 + t;
+            x[i] = mt_word(x[i - kN], x[i - kN + 1], x[i - 227]);
         }
         __syncthreads();
         if (t < 170) {
-            const int i = 454 + t;
-            const uint32_t v = (i < kN - 1) ? mt_word(o[i], o[i + 1], w[i - 227]) : mt_word(o[kN - 1], w[0], w[396]);
-            w[i] = v;
-            jb.scratch[base + i] = v;
+            const int i = base + 454 + t;
+            x[i] = mt_word(x[i - kN], x[i - kN + 1], x[i - 227]);
         }
         __syncthreads();
-        cur ^= 1;
     }
-    __threadfence_block();
+    // 2. out[j] = XOR over set bits i of x_{i+j}: eight set bits per round, their eight LDS
+    //    reads in flight together (a missing bit reads the zero block after the sequence)
+    for (int k = t; k < kN; k += kJumpThreads) x[kJumpZero + k] = 0u;
     __syncthreads();
-    // 2. out[j] = XOR over set bits i of x_{i+j}
-    uint32_t a0 = 0, a1 = 0, a2 = 0;
-    const uint32_t* x = jb.scratch;
-    for (int wd = 0; wd * 64 <= top; ++wd) {
-        uint64_t bits = P[wd];
-        while (bits) {
-            const int i = 64 * wd + __builtin_ctzll(bits);
-            bits &= bits - 1;
-            a0 ^= x[i + t];
-            a1 ^= x[i + t + 256];
-            if (t < kN - 512) a2 ^= x[i + t + 512];
+    uint32_t a = 0;
+    if (t < kN) {
+        for (int wd = 0; wd * 64 <= top; ++wd) {
+            uint64_t bits = P[wd];
+            const int b0 = 64 * wd + t;
+            while (bits) {
+                int i[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    i[u] = bits ? b0 + __builtin_ctzll(bits) : kJumpZero + t;
+                    bits &= bits - 1;
+                }
+                uint32_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = x[i[u]];
+                a ^= (v[0] ^ v[1]) ^ (v[2] ^ v[3]) ^ (v[4] ^ v[5]) ^ (v[6] ^ v[7]);
+            }
         }
+        jb.out[t] = top >= 0 ? a : 0u;
     }
-    jb.out[t] = top >= 0 ? a0 : 0u;
-    jb.out[t + 256] = top >= 0 ? a1 : 0u;
-    if (t < kN - 512) jb.out[t + 512] = top >= 0 ? a2 : 0u;
     if (t == 0) jb.out[kN] = kN;
 }
 
@@ -194,59 +191,146 @@ __global__ __launch_bounds__(256) void k_mt_generate_batch(const GenJob* __restr
     mt_generate(j.state, j.R, j.n);
 }
 
-// Tsub[sub][s-1] = end_state | batches_done << 8, for s in [1, L-1].  A 256-thread block
-// serves 256 / G sub-chunks at once, G = the start states rounded up to a wave multiple
-// (L = 100: two sub-chunks of 99 states per block, 77% of the lanes busy).
-__global__ __launch_bounds__(256) void k_fsm_sub(const uint32_t* __restrict__ R, int64_t sub0, int64_t nsub,
-                                                 int L, uint16_t* __restrict__ Tsub) {
-    __shared__ uint32_t draws[4][kSub];
-    const int S = L - 1;
-    const int G = (S + 63) & ~63;               // lanes per sub-chunk
-    const int per = 256 / G >= 1 ? 256 / G : 1; // sub-chunks per block (1, 2 or 4)
-    const int q = threadIdx.x / G, lane_s = threadIdx.x % G;
-    for (int64_t sb0 = sub0 + (int64_t)blockIdx.x * per; sb0 < sub0 + nsub; sb0 += (int64_t)gridDim.x * per) {
-        __syncthreads();
-        for (int k = threadIdx.x; k < per * kSub; k += 256) {
-            const int64_t sb = sb0 + k / kSub;
-            draws[k / kSub][k % kSub] = sb < sub0 + nsub ? R[sb * kSub + k % kSub] : 0u;
-        }
-        __syncthreads();
-        const int64_t sb = sb0 + q;
-        if (q >= per || sb >= sub0 + nsub) continue;
-        for (int s0 = lane_s + 1; s0 <= S; s0 += G) {
-            uint32_t s = (uint32_t)s0, done = 0;
-            for (int k = 0; k < kSub; ++k) {
-                const bool acc = (draws[q][k] & imask(s)) <= s;
-                const bool wrap = acc && s == 1;
-                done += wrap ? 1u : 0u;
-                s = wrap ? (uint32_t)S : (acc ? s - 1 : s);
-            }
-            Tsub[sb * S + (s0 - 1)] = (uint16_t)(s | (done << 8));
-        }
-    }
+__device__ __forceinline__ void fsm_step(uint32_t v, uint32_t& s, uint32_t& d, uint32_t S) {
+    const bool acc = (v & imask(s)) <= s;
+    const bool wrap = acc && s == 1;
+    d += wrap ? 1u : 0u;
+    s = wrap ? S : (acc ? s - 1 : s);
 }
 
-// Tchunk[c][s-1] = end_state | batches_done << 8 over 64 sub-chunks.
-__global__ __launch_bounds__(256) void k_fsm_chunk(const uint16_t* __restrict__ Tsub, int64_t chunk0, int64_t nchunk,
-                                                   int L, uint32_t* __restrict__ Tchunk) {
-    const int S = L - 1;
-    for (int64_t c = chunk0 + blockIdx.x; c < chunk0 + nchunk; c += gridDim.x) {
-        for (int s0 = threadIdx.x + 1; s0 <= S; s0 += 256) {
-            uint32_t s = (uint32_t)s0, done = 0;
-            const uint16_t* t = Tsub + c * kSubPerChunk * S;
-            for (int k = 0; k < kSubPerChunk; ++k) {
-                const uint32_t e = t[(int64_t)k * S + (s - 1)];
-                s = e & 0xffu;
-                done += e >> 8;
-            }
-            Tchunk[c * S + (s0 - 1)] = s | (done << 8);
+// Prefix tables.  For every chunk c of the stream and every interval state s it may be
+// entered in: Tpre[c][k][s-1] = (state after sub-chunks 0..k of the chunk) | (batches
+// completed since the chunk start) << 8, and Tchunk[c][s-1] = Tpre[c][63][s-1].
+//
+// The S trajectories of a chunk couple fast (two that reach the same state at the same
+// draw never part again): for L = 100 about 27 distinct states are left after the first
+// 128 draws, 10 after 512 and 3 after 8192.  A workgroup runs 16 chunks as ONE list of
+// distinct (chunk, state) trajectories: per sub-chunk it steps every listed trajectory
+// over the 128 draws (LDS rows, 16-byte reads), merges the ones that met (LDS atomicMin
+// on the end state picks the survivor), renumbers the survivors in order, and writes
+// every start state's entry through its trajectory index plus a done offset.  After the
+// first sub-chunks ~16 trajectories per chunk remain, one pass of 256 lanes for all 16
+// chunks: ~6x fewer FSM steps than stepping every start state through every sub-chunk.
+constexpr int kPreChunks = 16;
+constexpr int kPreRow = kSub + 4;   // LDS row stride in words: 16-byte rows, the chunks' rows in distinct banks
+
+size_t prefix_lds_bytes(int L) {
+    const size_t S = (size_t)L - 1, NP = kPreChunks * S;
+    return (size_t)kPreChunks * kPreRow * 4 + (size_t)kPreChunks * (S + 1) * 4 + NP * (6 * 2 + 4 * 1);
+}
+
+__global__ __launch_bounds__(256) void k_fsm_prefix(const uint32_t* __restrict__ R, int64_t chunk0, int64_t nchunk,
+                                                    int L, uint32_t* __restrict__ Tpre, uint32_t* __restrict__ Tchunk) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t pre_lds[];
+    __shared__ int wsum[4];
+    __shared__ int n_sh;
+    const int S = L - 1, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t cb = chunk0 + (int64_t)blockIdx.x * kPreChunks;
+    const int nc = (int)min((int64_t)kPreChunks, chunk0 + nchunk - cb);
+    const int NP = kPreChunks * S;
+    uint32_t* draws = pre_lds;                                              // [16][kPreRow]
+    int32_t* owner = reinterpret_cast<int32_t*>(draws + kPreChunks * kPreRow); // [16][S + 1]
+    uint16_t* dn = reinterpret_cast<uint16_t*>(owner + kPreChunks * (S + 1));  // batches done, per trajectory
+    uint16_t* dn2 = dn + NP;
+    int16_t* nidx = reinterpret_cast<int16_t*>(dn2 + NP);                   // index after the merge
+    int16_t* dlt = nidx + NP;                                               // done minus its survivor's
+    int16_t* cls = dlt + NP;                                                // per start state: trajectory
+    int16_t* off = cls + NP;                                                //   and done offset
+    uint8_t* st = reinterpret_cast<uint8_t*>(off + NP);
+    uint8_t* st2 = st + NP;
+    uint8_t* ch = st2 + NP;
+    uint8_t* ch2 = ch + NP;
+    const int ns = nc * S;
+    for (int e = tid; e < ns; e += 256) {
+        st[e] = (uint8_t)(e % S + 1);
+        dn[e] = 0;
+        ch[e] = (uint8_t)(e / S);
+        cls[e] = (int16_t)e;
+        off[e] = 0;
+    }
+    if (tid == 0) n_sh = ns;
+    for (int k = 0; k < kSubPerChunk; ++k) {
+        __syncthreads();
+        for (int e = tid; e < nc * (kSub / 4); e += 256) {
+            const int c = e / (kSub / 4), q = e % (kSub / 4);
+            *reinterpret_cast<uint4*>(draws + c * kPreRow + 4 * q) =
+                *reinterpret_cast<const uint4*>(R + (cb + c) * kChunk + (int64_t)k * kSub + 4 * q);
         }
+        __syncthreads();
+        const int n = n_sh;
+        for (int p = tid; p < n; p += 256) {
+            uint32_t s = st[p], d = dn[p];
+            const uint32_t* row = draws + ch[p] * kPreRow;
+#pragma unroll 4
+            for (int q = 0; q < kSub; q += 4) {
+                const uint4 v = *reinterpret_cast<const uint4*>(row + q);
+                fsm_step(v.x, s, d, (uint32_t)S);
+                fsm_step(v.y, s, d, (uint32_t)S);
+                fsm_step(v.z, s, d, (uint32_t)S);
+                fsm_step(v.w, s, d, (uint32_t)S);
+            }
+            st2[p] = (uint8_t)s;
+            dn2[p] = (uint16_t)d;
+            ch2[p] = ch[p];
+        }
+        for (int e = tid; e < nc * (S + 1); e += 256) owner[e] = 0x7fffffff;
+        __syncthreads();
+        for (int p = tid; p < n; p += 256) atomicMin(&owner[ch2[p] * (S + 1) + st2[p]], p);
+        __syncthreads();
+        // survivors: the first trajectory of each (chunk, end state), renumbered in order
+        const int per = (n + 255) / 256;
+        const int p0 = min(n, tid * per), p1 = min(n, p0 + per);
+        int cnt = 0;
+        for (int p = p0; p < p1; ++p) cnt += owner[ch2[p] * (S + 1) + st2[p]] == p ? 1 : 0;
+        int inc = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) wsum[wv] = inc;
+        __syncthreads();
+        int base = 0;
+        for (int w = 0; w < wv; ++w) base += wsum[w];
+        int idx = base + inc - cnt;
+        for (int p = p0; p < p1; ++p)
+            if (owner[ch2[p] * (S + 1) + st2[p]] == p) nidx[p] = (int16_t)idx++;
+        if (tid == 255) n_sh = base + inc;
+        __syncthreads();
+        for (int p = tid; p < n; p += 256) {
+            const int o = owner[ch2[p] * (S + 1) + st2[p]];
+            if (o != p) {
+                nidx[p] = nidx[o];
+                dlt[p] = (int16_t)((int)dn2[p] - (int)dn2[o]);
+            } else {
+                dlt[p] = 0;
+            }
+        }
+        __syncthreads();
+        // every start state's entry; then its trajectory after the merge
+        for (int e = tid; e < ns; e += 256) {
+            const int i = cls[e], o = off[e];
+            const uint32_t val = (uint32_t)st2[i] | ((uint32_t)((int)dn2[i] + o) << 8);
+            const int64_t c = cb + e / S;
+            const int s0 = e % S;
+            Tpre[(c * kSubPerChunk + k) * S + s0] = val;
+            if (k == kSubPerChunk - 1) Tchunk[c * S + s0] = val;
+            cls[e] = nidx[i];
+            off[e] = (int16_t)(o + dlt[i]);
+        }
+        for (int p = tid; p < n; p += 256)
+            if (owner[ch2[p] * (S + 1) + st2[p]] == p) {
+                const int q = nidx[p];
+                st[q] = st2[p];
+                dn[q] = dn2[p];
+                ch[q] = ch2[p];
+            }
     }
 }
 
 struct Job {
     const uint32_t* R;
-    const uint16_t* Tsub;
+    const uint32_t* Tpre;
     const uint32_t* Tchunk;
     int64_t avail, P, W;
     void* pieces;
@@ -257,6 +341,7 @@ struct Job {
     const int32_t* stop;
     int64_t pick_offset, pick_last;
     int64_t* pick_out;
+    uint16_t* first;   // [64][S]: sub-chunk tables of the chunk holding P (k_fsm_first)
 };
 
 struct ChunkStart {
@@ -265,32 +350,70 @@ struct ChunkStart {
     int32_t batch;    // batches completed (relative to the window) before pos
 };
 
-// From draw P at a batch boundary, walk to the first chunk boundary (draw by draw, then
-// by sub-chunk tables) and then chunk by chunk until W batches are done.  The chunk
-// table rows are staged in LDS 64 chunks at a time (all lanes load, lane 0 walks), so
-// the serial walk does LDS lookups, not dependent HBM loads.
-// out[0] = the piece [P, first chunk boundary); out[k] = chunk starts.
-// info = {pieces, end draw, batches reached}.
-__device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restrict__ Tsub,
+// The prefix tables only describe chunks entered at their first draw.  A window starts at
+// a batch boundary P anywhere in a chunk (the refit seeds before it are not shuffle draws),
+// so the rest of that one chunk gets classic per-sub-chunk tables, every start state
+// stepped through every sub-chunk after the one holding P: first[q][s-1] = end state |
+// batches << 8.  One workgroup per (sub-chunk, job); they run side by side.
+constexpr int kFirstThreads = 128;
+
+__device__ void fsm_first(const Job& j, int L) {
+    __shared__ __attribute__((aligned(16))) uint32_t dr[kSub];
+    if (j.W <= 0) return;
+    const int S = L - 1;
+    const int64_t cstart = j.P / kChunk * kChunk;
+    const int q = (int)((j.P - cstart) / kSub) + 1 + (int)blockIdx.x;
+    if (q >= kSubPerChunk) return;
+    const int64_t d0 = cstart + (int64_t)q * kSub;
+    if (d0 + kSub > j.avail) return;
+    if (threadIdx.x < kSub / 4)
+        reinterpret_cast<uint4*>(dr)[threadIdx.x] = reinterpret_cast<const uint4*>(j.R + d0)[threadIdx.x];
+    __syncthreads();
+    for (int s0 = threadIdx.x + 1; s0 <= S; s0 += blockDim.x) {
+        uint32_t s = (uint32_t)s0, d = 0;
+#pragma unroll 4
+        for (int k = 0; k < kSub; k += 4) {
+            const uint4 v = reinterpret_cast<const uint4*>(dr)[k / 4];
+            fsm_step(v.x, s, d, (uint32_t)S);
+            fsm_step(v.y, s, d, (uint32_t)S);
+            fsm_step(v.z, s, d, (uint32_t)S);
+            fsm_step(v.w, s, d, (uint32_t)S);
+        }
+        j.first[q * S + (s0 - 1)] = (uint16_t)(s | (d << 8));
+    }
+}
+
+__global__ __launch_bounds__(kFirstThreads) void k_fsm_first(Job j, int L) { fsm_first(j, L); }
+
+__global__ __launch_bounds__(kFirstThreads) void k_fsm_first_batch(const Job* __restrict__ jobs, int L) {
+    const Job j = jobs[blockIdx.y];
+    fsm_first(j, L);
+}
+
+// From draw P at a batch boundary: draw by draw to the next sub-chunk boundary, then by
+// the first-chunk tables (k_fsm_first) to the chunk boundary, then chunk by chunk (Tchunk)
+// until W batches are done.  Table rows are staged in LDS (all lanes load, lane 0 walks),
+// so the serial walk does LDS lookups, not dependent HBM loads.
+// Pieces: out[0] = [P, next sub-chunk boundary); then every sub-chunk of P's chunk; then
+// chunk starts.  info = {pieces, end draw, batches reached}.
+__device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restrict__ first,
                          const uint32_t* __restrict__ Tchunk, int64_t P, int64_t W, int L, int64_t avail,
                          ChunkStart* __restrict__ out, int64_t* __restrict__ info) {
-    extern __shared__ uint32_t tab[];   // [64][S] chunk rows; phase A: draws + sub-chunk rows
+    extern __shared__ uint32_t tab[];   // [64][S] chunk rows; phase A: draws + first-chunk rows
     __shared__ int64_t sh_pos, sh_batch, sh_k;
     __shared__ uint32_t sh_s;
     const int S = L - 1;
-    // phase A inputs: the draws up to the next sub-chunk boundary and the sub-chunk rows up
-    // to the next chunk boundary, staged in LDS by all lanes
     const int64_t sub_end = min(avail, (P / kSub + 1) * kSub);
     const int64_t chunk_end = min(avail, (P / kChunk + 1) * kChunk);
     const int n_draws = (int)max((int64_t)0, sub_end - P);
-    const int64_t first_sub = sub_end / kSub;
+    const int q0 = (int)((sub_end % kChunk) / kSub);          // first sub-chunk after P's
     const int n_subrows = (int)max((int64_t)0, (chunk_end - sub_end) / kSub);
     uint32_t* a_draws = tab;
-    uint16_t* a_sub = reinterpret_cast<uint16_t*>(tab + kSub);
+    uint16_t* a_first = reinterpret_cast<uint16_t*>(tab + kSub);
 #pragma unroll 2
     for (int k = threadIdx.x; k < n_draws; k += 64) a_draws[k] = R[P + k];
 #pragma unroll 8
-    for (int e = threadIdx.x; e < n_subrows * S; e += 64) a_sub[e] = Tsub[first_sub * S + e];
+    for (int e = threadIdx.x; e < n_subrows * S; e += 64) a_first[e] = first[q0 * S + e];
     __syncthreads();
     if (threadIdx.x == 0) {
         int64_t pos = P, batch = 0, k = 0;
@@ -309,7 +432,8 @@ __device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restr
             }
         }
         while (batch < W && pos % kChunk != 0 && pos + kSub <= avail) {
-            const uint32_t e = a_sub[(pos / kSub - first_sub) * S + (s - 1)];
+            out[k++] = ChunkStart{pos, (int32_t)s, (int32_t)batch};
+            const uint32_t e = a_first[((pos - sub_end) / kSub) * S + (s - 1)];
             s = e & 0xffu;
             batch += e >> 8;
             pos += kSub;
@@ -354,128 +478,87 @@ __device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restr
 }
 
 __global__ __launch_bounds__(64) void k_fsm_walk(Job j, int L) {
-    fsm_walk(j.R, j.Tsub, j.Tchunk, j.P, j.W, L, j.avail, reinterpret_cast<ChunkStart*>(j.pieces), j.info);
+    fsm_walk(j.R, j.first, j.Tchunk, j.P, j.W, L, j.avail, reinterpret_cast<ChunkStart*>(j.pieces), j.info);
 }
 
 __global__ __launch_bounds__(64) void k_fsm_walk_batch(const Job* __restrict__ jobs, int L) {
     const Job j = jobs[blockIdx.x];
     if (j.W <= 0) return;
-    fsm_walk(j.R, j.Tsub, j.Tchunk, j.P, j.W, L, j.avail, reinterpret_cast<ChunkStart*>(j.pieces), j.info);
+    fsm_walk(j.R, j.first, j.Tchunk, j.P, j.W, L, j.avail, reinterpret_cast<ChunkStart*>(j.pieces), j.info);
 }
 
-// One wave per window piece.  The chunk's sub-chunk table rows are staged in LDS (16-byte
-// loads) together with the draws of the piece's first and last sub-chunk (the only ones
-// lane 0 may have to step draw by draw); lane 0 derives every sub-chunk's start (state,
-// batch); then each lane replays one sub-chunk straight from HBM, 16 draws per round of
-// loads: for each accepted draw of batch b < W record J[b*L + s] = v & mask(s) and, when
-// s == 1, E[b] = draw index.  (LDS per wave ~13 KB, so a CU holds many pieces at once.)
+// One wave per window piece.  A piece of at most one sub-chunk (the start of the window's
+// first chunk) is replayed by lane 0; a chunk piece starts on a chunk boundary, so lane t
+// reads sub-chunk t's start state and batch straight from the prefix tables and every
+// lane replays its sub-chunk from HBM, 16 draws per round of loads: for each accepted draw
+// of batch b < W record J[b*L + s] = v & mask(s) and, when s == 1, E[b] = draw index.
 constexpr int kReplayBatch = 16;
 
-__device__ void fsm_replay(const uint32_t* __restrict__ R, const uint16_t* __restrict__ Tsub,
+__device__ __forceinline__ void replay_range(const uint32_t* __restrict__ R, int64_t beg, int64_t fin, uint32_t s,
+                                             int64_t b, int64_t W, int L, uint8_t* __restrict__ J,
+                                             int64_t* __restrict__ E) {
+    const uint32_t S = (uint32_t)(L - 1);
+    for (int64_t q0 = beg; q0 < fin && b < W; q0 += kReplayBatch) {
+        uint32_t v[kReplayBatch];
+#pragma unroll
+        for (int k = 0; k < kReplayBatch; ++k) v[k] = R[min(q0 + k, fin - 1)];
+#pragma unroll
+        for (int k = 0; k < kReplayBatch; ++k) {
+            if (q0 + k < fin && b < W) {
+                const uint32_t m = v[k] & imask(s);
+                if (m <= s) {
+                    J[b * L + s] = (uint8_t)m;
+                    if (s == 1) {
+                        E[b] = q0 + k;
+                        s = S;
+                        ++b;
+                    } else {
+                        --s;
+                    }
+                }
+            }
+        }
+    }
+}
+
+__device__ void fsm_replay(const uint32_t* __restrict__ R, const uint32_t* __restrict__ Tpre,
                            const ChunkStart* __restrict__ pieces, const int64_t* __restrict__ info, int64_t W, int L,
                            uint8_t* __restrict__ J, int64_t* __restrict__ E, int64_t blk, int64_t nblk) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t rep_lds[];   // [64][S] sub-chunk rows (u16)
-    uint16_t* subtab = reinterpret_cast<uint16_t*>(rep_lds);
-    __shared__ uint32_t edge[2][kSub];
-    __shared__ int64_t sub_pos[kSubPerChunk + 2];
-    __shared__ int32_t sub_state[kSubPerChunk + 2], sub_batch[kSubPerChunk + 2];
-    __shared__ int n_subs;
     const int64_t npieces = info[0], end = info[1];
     const int S = L - 1;
+    const int lane = threadIdx.x;
     for (int64_t pc = blk; pc < npieces; pc += nblk) {
         const ChunkStart c = pieces[pc];
         const int64_t stop = (pc + 1 < npieces) ? pieces[pc + 1].pos : end;
         if (stop <= c.pos) continue;
-        // the chunk's sub-chunk rows: 64 * S u16 = 8 * S uint4, 16-byte aligned (the chunk's
-        // rows start at chunk * 128 * S bytes); rows past the piece are not read below
-        const int64_t chunk = c.pos / kChunk;
-        const int64_t first_sub = chunk * kSubPerChunk;
-        {
-            const uint4* src = reinterpret_cast<const uint4*>(Tsub + first_sub * S);
-            uint4* dst = reinterpret_cast<uint4*>(subtab);
-#pragma unroll 4
-            for (int e = threadIdx.x; e < 8 * S; e += 64) dst[e] = src[e];
+        if (stop - c.pos <= kSub) {
+            if (lane == 0) replay_range(R, c.pos, stop, (uint32_t)c.state, c.batch, W, L, J, E);
+            continue;
         }
-        const int64_t sA = c.pos / kSub, sB = (stop - 1) / kSub;
-        for (int k = threadIdx.x; k < kSub; k += 64) {
-            edge[0][k] = R[sA * kSub + k];
-            edge[1][k] = R[sB * kSub + k];
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int64_t pos = c.pos;
+        const int64_t chunk = c.pos / kChunk;        // c.pos % kChunk == 0 (a chunk piece)
+        const int nsub = (int)((stop - c.pos + kSub - 1) / kSub);
+        for (int t = lane; t < nsub; t += 64) {
             uint32_t s = (uint32_t)c.state;
-            int32_t b = c.batch;
-            int n = 0;
-            while (pos < stop) {
-                sub_pos[n] = pos;
-                sub_state[n] = (int32_t)s;
-                sub_batch[n] = b;
-                ++n;
-                const int64_t nxt = min(stop, (pos / kSub + 1) * kSub);
-                if (pos % kSub == 0 && nxt - pos == kSub) {
-                    const uint32_t e = subtab[(pos / kSub - first_sub) * S + (s - 1)];
-                    s = e & 0xffu;
-                    b += (int32_t)(e >> 8);
-                } else {
-                    const uint32_t* d = edge[pos / kSub == sA ? 0 : 1] - (pos / kSub) * kSub;
-                    for (int64_t q = pos; q < nxt; ++q) {
-                        const uint32_t v = d[q];
-                        if ((v & imask(s)) <= s) {
-                            if (s == 1) {
-                                s = (uint32_t)S;
-                                ++b;
-                            } else {
-                                --s;
-                            }
-                        }
-                    }
-                }
-                pos = nxt;
+            int64_t b = c.batch;
+            if (t > 0) {
+                const uint32_t e = Tpre[(chunk * kSubPerChunk + (t - 1)) * S + (c.state - 1)];
+                s = e & 0xffu;
+                b += e >> 8;
             }
-            sub_pos[n] = stop;
-            n_subs = n;
+            replay_range(R, c.pos + (int64_t)t * kSub, min(stop, c.pos + (int64_t)(t + 1) * kSub), s, b, W, L, J, E);
         }
-        __syncthreads();
-        for (int t = threadIdx.x; t < n_subs; t += 64) {
-            uint32_t s = (uint32_t)sub_state[t];
-            int64_t b = sub_batch[t];
-            const int64_t beg = sub_pos[t], fin = sub_pos[t + 1];
-            for (int64_t q0 = beg; q0 < fin && b < W; q0 += kReplayBatch) {
-                uint32_t v[kReplayBatch];
-#pragma unroll
-                for (int k = 0; k < kReplayBatch; ++k) v[k] = R[min(q0 + k, fin - 1)];
-#pragma unroll
-                for (int k = 0; k < kReplayBatch; ++k) {
-                    if (q0 + k < fin && b < W) {
-                        const uint32_t m = v[k] & imask(s);
-                        if (m <= s) {
-                            J[b * L + s] = (uint8_t)m;
-                            if (s == 1) {
-                                E[b] = q0 + k;
-                                s = (uint32_t)S;
-                                ++b;
-                            } else {
-                                --s;
-                            }
-                        }
-                    }
-                }
-            }
-        }
-        __syncthreads();
     }
 }
 
 __global__ __launch_bounds__(64) void k_fsm_replay(Job j, int L) {
-    fsm_replay(j.R, j.Tsub, reinterpret_cast<const ChunkStart*>(j.pieces), j.info, j.W, L, j.J, j.E, blockIdx.x,
+    fsm_replay(j.R, j.Tpre, reinterpret_cast<const ChunkStart*>(j.pieces), j.info, j.W, L, j.J, j.E, blockIdx.x,
                gridDim.x);
 }
 
 __global__ __launch_bounds__(64) void k_fsm_replay_batch(const Job* __restrict__ jobs, int L) {
     const Job j = jobs[blockIdx.y];
     if (j.W <= 0) return;
-    fsm_replay(j.R, j.Tsub, reinterpret_cast<const ChunkStart*>(j.pieces), j.info, j.W, L, j.J, j.E, blockIdx.x,
+    fsm_replay(j.R, j.Tpre, reinterpret_cast<const ChunkStart*>(j.pieces), j.info, j.W, L, j.J, j.E, blockIdx.x,
                gridDim.x);
 }
 
@@ -525,8 +608,6 @@ size_t walk_lds_bytes(int L) {
                     kSub * sizeof(uint32_t) + (size_t)kSubPerChunk * (L - 1) * sizeof(uint16_t));
 }
 
-size_t replay_lds_bytes(int L) { return (size_t)kSubPerChunk * (L - 1) * sizeof(uint16_t); }
-
 }  // namespace
 
 static_assert(sizeof(Job) == sizeof(ddm_shuffle_job), "ddm_shuffle_job layout");
@@ -555,12 +636,15 @@ extern "C" int ddm_shuffle_window_batch(const ddm_shuffle_job* jobs_dev, int32_t
     const Job* jobs = reinterpret_cast<const Job*>(jobs_dev);
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
+    hipLaunchKernelGGL(k_fsm_first_batch, dim3(kSubPerChunk - 1, (unsigned)n_jobs), dim3(kFirstThreads), 0, s, jobs,
+                       (int)batch_len);
+    if (int rc = ddm::launch_status("ddm_shuffle_window_batch/first")) return rc;
     hipLaunchKernelGGL(k_fsm_walk_batch, dim3((unsigned)n_jobs), dim3(64), walk_lds_bytes(batch_len), s, jobs,
                        (int)batch_len);
     if (int rc = ddm::launch_status("ddm_shuffle_window_batch/walk")) return rc;
     const int64_t pblocks = std::max<int64_t>(1, std::min<int64_t>(max_pieces, 2048));
-    hipLaunchKernelGGL(k_fsm_replay_batch, dim3((unsigned)pblocks, (unsigned)n_jobs), dim3(64),
-                       replay_lds_bytes(batch_len), s, jobs, (int)batch_len);
+    hipLaunchKernelGGL(k_fsm_replay_batch, dim3((unsigned)pblocks, (unsigned)n_jobs), dim3(64), 0, s, jobs,
+                       (int)batch_len);
     if (int rc = ddm::launch_status("ddm_shuffle_window_batch/replay")) return rc;
     const int64_t bblocks = std::min<int64_t>(ddm::ceil_div(max_W, 256), 1024);
     hipLaunchKernelGGL(k_fsm_perms_batch, dim3((unsigned)bblocks, (unsigned)n_jobs), dim3(256),
@@ -610,47 +694,44 @@ extern "C" int ddm_mt_jump(const ddm_jump_job* jobs_dev, int32_t n_jobs, ddm_str
     if (n_jobs == 0) return 0;
     static_assert(sizeof(JumpJob) == sizeof(ddm_jump_job), "JumpJob must mirror ddm_jump_job");
     static_assert(DDM_MT_JUMP_SCRATCH_WORDS >= kN * ((kN + 64 * DDM_MT_POLY_WORDS + kN - 1) / kN + 1),
-                  "jump scratch holds the whole blocks of x_0 .. x_{623 + deg}");
-    hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)n_jobs), dim3(256), 0, ddm::as_hip(stream),
+                  "the LDS sequence holds the whole blocks of x_0 .. x_{623 + deg}");
+    hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)n_jobs), dim3(kJumpThreads), 0, ddm::as_hip(stream),
                        reinterpret_cast<const JumpJob*>(jobs_dev));
     return ddm::launch_status("ddm_mt_jump");
 }
 
 extern "C" int ddm_shuffle_tables(const uint32_t* R, int64_t chunk0, int64_t nchunk, int32_t batch_len,
-                                  uint16_t* Tsub, uint32_t* Tchunk, ddm_stream_t stream) {
-    if (!R || !Tsub || !Tchunk || chunk0 < 0 || nchunk < 0 || batch_len < 2 || batch_len > 256) {
+                                  uint32_t* Tpre, uint32_t* Tchunk, ddm_stream_t stream) {
+    if (!R || !Tpre || !Tchunk || chunk0 < 0 || nchunk < 0 || batch_len < 2 || batch_len > 256) {
         ddm::set_error("ddm_shuffle_tables: invalid argument");
         return DDM_E_ARG;
     }
     if (nchunk == 0) return 0;
-    hipStream_t s = ddm::as_hip(stream);
-    const int64_t nsub = nchunk * kSubPerChunk;
-    hipLaunchKernelGGL(k_fsm_sub, dim3((unsigned)std::min<int64_t>(nsub, 65536)), dim3(256), 0, s, R,
-                       chunk0 * kSubPerChunk, nsub, (int)batch_len, Tsub);
-    if (int rc = ddm::launch_status("ddm_shuffle_tables/sub")) return rc;
-    hipLaunchKernelGGL(k_fsm_chunk, dim3((unsigned)std::min<int64_t>(nchunk, 65536)), dim3(256), 0, s, Tsub, chunk0,
-                       nchunk, (int)batch_len, Tchunk);
-    return ddm::launch_status("ddm_shuffle_tables/chunk");
+    const int64_t blocks = ddm::ceil_div(nchunk, (int64_t)kPreChunks);
+    hipLaunchKernelGGL(k_fsm_prefix, dim3((unsigned)blocks), dim3(256), prefix_lds_bytes(batch_len), ddm::as_hip(stream),
+                       R, chunk0, nchunk, (int)batch_len, Tpre, Tchunk);
+    return ddm::launch_status("ddm_shuffle_tables");
 }
 
-extern "C" int ddm_shuffle_window(const uint32_t* R, const uint16_t* Tsub, const uint32_t* Tchunk, int64_t avail,
+extern "C" int ddm_shuffle_window(const uint32_t* R, const uint32_t* Tpre, const uint32_t* Tchunk, int64_t avail,
                                   int64_t P, int64_t W, int32_t batch_len, void* pieces, int64_t max_pieces,
-                                  int64_t* info, uint8_t* J, int64_t* E, uint8_t* perm_out, ddm_stream_t stream,
-                                  ddm_event_t ev_begin, ddm_event_t ev_end) {
-    if (!R || !Tsub || !Tchunk || !pieces || !info || !J || !E || !perm_out || P < 0 || W <= 0 ||
-        batch_len < 2 || batch_len > 256 || max_pieces < 2 + (W * batch_len * 3) / kChunk) {
+                                  int64_t* info, uint8_t* J, int64_t* E, uint8_t* perm_out, uint16_t* first,
+                                  ddm_stream_t stream, ddm_event_t ev_begin, ddm_event_t ev_end) {
+    if (!R || !Tpre || !Tchunk || !pieces || !info || !J || !E || !perm_out || !first || P < 0 || W <= 0 ||
+        batch_len < 2 || batch_len > 256 || max_pieces < 2 + kSubPerChunk + (W * batch_len * 3) / kChunk) {
         ddm::set_error("ddm_shuffle_window: invalid argument");
         return DDM_E_ARG;
     }
     hipStream_t s = ddm::as_hip(stream);
-    Job j{R, Tsub, Tchunk, avail, P, W, pieces, info, J, E, perm_out, nullptr, 0, 0, nullptr};
+    Job j{R, Tpre, Tchunk, avail, P, W, pieces, info, J, E, perm_out, nullptr, 0, 0, nullptr, first};
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
+    hipLaunchKernelGGL(k_fsm_first, dim3(kSubPerChunk - 1), dim3(kFirstThreads), 0, s, j, (int)batch_len);
+    if (int rc = ddm::launch_status("ddm_shuffle_window/first")) return rc;
     hipLaunchKernelGGL(k_fsm_walk, dim3(1), dim3(64), walk_lds_bytes(batch_len), s, j, (int)batch_len);
     if (int rc = ddm::launch_status("ddm_shuffle_window/walk")) return rc;
     const int64_t blocks = std::min<int64_t>(max_pieces, 8192);
-    hipLaunchKernelGGL(k_fsm_replay, dim3((unsigned)blocks), dim3(64), replay_lds_bytes(batch_len), s, j,
-                       (int)batch_len);
+    hipLaunchKernelGGL(k_fsm_replay, dim3((unsigned)blocks), dim3(64), 0, s, j, (int)batch_len);
     if (int rc = ddm::launch_status("ddm_shuffle_window/replay")) return rc;
     hipLaunchKernelGGL(k_fsm_perms, dim3((unsigned)ddm::ceil_div(W, 256)), dim3(256), (size_t)256 * batch_len, s, j,
                        (int)batch_len);

@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
@@ -68,7 +68,7 @@ SIGNATURES = {
     "ddm_shuffle_generate": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
     "ddm_shuffle_tables": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp]),
     "ddm_shuffle_window": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
-                                          _vp, _vp]),
+                                          _vp, _vp, _vp]),
     "ddm_shuffle_pick": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
     "ddm_event_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
     "ddm_event_destroy": (ctypes.c_int, [_vp]),

@@ -32,7 +32,7 @@ from . import dfit, kernels
 from .forest import upload_forests
 from .params import OUTPUT_COLUMNS, DDMSettings, infer_x_features
 from .rng import MTStream
-from .shuffle import GpuShuffle, expected_draws_per_batch, perm_seeds_from_words
+from .shuffle import GpuShuffle, expected_draws_per_batch, fy_from_words, perm_seeds_from_words
 from .trainer import BatchForestTrainer
 
 # A window runs on ddm_scan_long when its carried detector is neither fresh nor trivial
@@ -172,7 +172,7 @@ class _Part:
     """Host-side epoch state of one partition in a BatchRunner."""
     __slots__ = ("i", "nb", "last_len", "n_full", "max_win", "base", "ev_base", "j", "P", "retrain", "train_rows",
                  "state", "win", "forest", "out", "done", "P_after_first", "g0", "b_end", "Wg", "tail",
-                 "P_tail_after", "seg_start", "pb", "staged", "rng_rows")
+                 "P_tail_after", "seg_start", "pb", "staged", "rng_rows", "words0", "ev")
 
     def blen(self, b):
         return self.last_len if b == self.nb - 1 else self.pb
@@ -182,6 +182,9 @@ class _Part:
         already be this epoch's first GPU-shuffled batch."""
         b_end = min(self.nb, self.j + min(self.win, self.max_win))
         return b_end == self.nb and self.last_len != pb and self.nb - 1 >= self.g0
+
+
+_HOST_TRACE = os.environ.get("DDM_HOST_TRACE", "") not in ("", "0")
 
 
 class BatchRunner:
@@ -328,6 +331,12 @@ class BatchRunner:
             cap = int(nb * expected_draws_per_batch(pb) * 1.2) + 64 * 1024
             self.shuffles.append(GpuShuffle(dev, pb, cap, mw, self.stream, self.gen_stream, self.tab_stream))
         self.stats = RunStats()
+        self._gen_rest = None
+        self.trace = [] if _HOST_TRACE else None     # (label, seconds since run start)
+
+    def _mark(self, label):
+        if self.trace is not None:
+            self.trace.append((label, time.perf_counter() - self._t_run))
 
     # -- helpers
     def _dptr(self, off, i, size):
@@ -344,13 +353,20 @@ class BatchRunner:
         """wants: [(partition index, draws needed)].  Partitions whose enqueued stream falls
         short get one batched generate launch plus their tables on the side stream, closed
         by one event; then (wait=True) the epoch stream waits for what it will read."""
-        reqs, tabs = [], []
+        reqs, tabs, jumps = [], [], []
         for i, upto in wants:
             sh = self.shuffles[i]
             if sh.chunks_for(upto) > sh.tab:
-                req, need = sh.gen_request(upto)
+                req, need = sh.gen_request(upto, jumps)
                 reqs.extend(req)
                 tabs.append((i, need))
+        if jumps:
+            # segment start states of every partition: one ddm_mt_jump launch
+            rec = np.concatenate(jumps)
+            jt = kernels.PinnedTable(kernels.JUMP_DTYPE, len(rec), self.device)
+            jt.rec[:len(rec)] = rec
+            kernels.mt_jump(jt, len(rec), self.gen_stream)
+            self.gen_tables.append(jt)
         if reqs:
             table = kernels.PinnedTable(kernels.GEN_DTYPE, len(reqs), self.device)   # read by the async copy
             for k, (st, R, cnt) in enumerate(reqs):
@@ -394,14 +410,18 @@ class BatchRunner:
         rows_dev = []
         unstaged = [ps for ps in need if ps.staged is None]
         for ps in unstaged:
-            self.shuffles[ps.i].ensure(ps.P + n_words)
+            if ps.words0 is None:
+                self.shuffles[ps.i].ensure(ps.P + n_words)
+        sync = False
         with torch.cuda.stream(self.stream):
             for k, ps in enumerate(need):
                 if ps.staged is not None:           # everything came back with the epoch
                     rows_dev.append(None)
                     continue
                 sh = self.shuffles[ps.i]
-                self.words_h[k].copy_(sh.R[ps.P:ps.P + n_words], non_blocking=True)
+                if ps.words0 is None:
+                    self.words_h[k].copy_(sh.R[ps.P:ps.P + n_words], non_blocking=True)
+                    sync = True
                 part = self.parts[ps.i]
                 if part.host_X32 is None:
                     idx_h = torch.from_numpy(np.asarray(ps.train_rows, dtype=np.int64)).pin_memory()
@@ -411,9 +431,11 @@ class BatchRunner:
                     xh.copy_(part.X.t().index_select(0, idx), non_blocking=True)
                     yh.copy_(part.y.index_select(0, idx), non_blocking=True)
                     rows_dev.append((xh, yh, idx_h))
+                    sync = True
                 else:
                     rows_dev.append(None)
-        if unstaged:
+        self._enqueue_rest()                   # the first epoch: behind its refit inputs
+        if sync:
             self.stream.synchronize()
         t1 = time.perf_counter()
         st.refit_readback_s += t1 - t0
@@ -438,7 +460,12 @@ class BatchRunner:
                 # batch j's shuffle is already in perm_all and the seeds came back staged
                 seeds, P1, P2 = ps.staged[3], ps.staged[4], ps.staged[5]
             else:
-                words = ps.staged[2] if ps.staged is not None else self.words_h[k].numpy().view(np.uint32)
+                if ps.staged is not None:
+                    words = ps.staged[2]
+                elif ps.words0 is not None:
+                    words, ps.words0 = ps.words0, None
+                else:
+                    words = self.words_h[k].numpy().view(np.uint32)
                 L = ps.blen(ps.j)
                 r = perm_seeds_from_words(words, L, T)
                 if r is None:                                   # rejections ran past the read-back
@@ -580,10 +607,15 @@ class BatchRunner:
         s, st, pb = self.s, self.stats, self.s.per_batch
         if len(rngs) != len(self.parts):
             raise ValueError("one MT19937 stream per partition")
+        self._t_run = time.perf_counter()
+        self._gen_rest = None
+        if self.trace is not None:
+            self.trace = []
         pss = []
         for i, part in enumerate(self.parts):
             ps = _Part()
             ps.pb = pb
+            ps.words0 = None
             ps.i, ps.nb, ps.base, ps.ev_base, ps.max_win = i, self.nbs[i], self.bases[i], self.ev_bases[i], \
                 self.max_wins[i]
             if ps.nb == 0:
@@ -610,32 +642,65 @@ class BatchRunner:
             self.gen_tables = []
             total = max(int(ps.nb * expected_draws_per_batch(pb) * 1.02) for ps in pss)
             upto = 1 << 19
-            while True:
-                self._ensure_all([(ps.i, min(upto, int(ps.nb * expected_draws_per_batch(pb) * 1.02))) for ps in pss],
-                                 wait=False)
-                if upto >= total:
-                    break
-                upto = min(total, upto + min(upto, GEN_PIECE_MAX))
+            # the first words of every stream (batch 0's shuffle, then the first fit's seeds
+            # and batch 1's shuffle) come back in ONE copy queued on the generation stream
+            # right behind the first piece, ahead of the jumps and the later pieces
+            n0 = max(64, 3 * pb) + 3 * pb + s.n_estimators + 64
+            head_h = torch.empty((len(pss), n0), dtype=torch.int32, pin_memory=True)
+            head_ev = None
+            self._mark("head buffer")
+            self._ensure_all([(ps.i, min(upto, int(ps.nb * expected_draws_per_batch(pb) * 1.02))) for ps in pss],
+                             wait=False)
+            with torch.cuda.stream(self.gen_stream):
+                for k, ps in enumerate(pss):
+                    head_h[k].copy_(self.shuffles[ps.i].R[:n0], non_blocking=True)
+            head_ev = torch.cuda.Event()
+            head_ev.record(self.gen_stream)
+            # the rest of the streams (jumps, later pieces) is enqueued once the first epoch's
+            # refit inputs are on their way (_enqueue_rest), so they are not queued behind it
+            self._gen_rest = (upto, total, pss)
             if self.timing:
                 st.prep_s += time.perf_counter() - tp
-            for ps in pss:
-                perm0, ps.P = self.shuffles[ps.i].host_perm(0, ps.blen(0))   # batches[0].sample (:187)
+            self._mark("first piece + head copy enqueued")
+            head_ev.synchronize()
+            self._mark("head copy done")
+            heads = head_h.numpy().view(np.uint32)
+            for k, ps in enumerate(pss):
+                r = fy_from_words(heads[k, :n0 - (3 * pb + s.n_estimators + 64)], ps.blen(0))
+                ps.words0 = None
+                if r is None:                                   # rejections ran past the read-back
+                    perm0, ps.P = self.shuffles[ps.i].host_perm(0, ps.blen(0))
+                else:
+                    perm0, ps.P = r                             # batches[0].sample (:187)
+                    ps.words0 = heads[k, ps.P:ps.P + 3 * pb + s.n_estimators + 64].copy()
                 started.append(ps)
                 if ps.nb < 2:
                     raise ValueError("No objects to concatenate")  # pd.concat([]) (:212)
                 ps.train_rows = perm0.astype(np.int64)
-                ps.out = np.full((ps.nb - 1, 2), -1, dtype=np.int64)
+                ps.ev = []                       # (batch rows, column, positions) of every event
                 ps.state = kernels.fresh_states(1)
                 ps.forest, ps.retrain, ps.j, ps.done = None, True, 1, False
                 ps.staged = None
                 ps.win = max(1, s.window_batches)
                 ps.seg_start = 1
+            # the dense per-batch result (DDM_Process.py:212 concatenates one row per batch:
+            # 1.25M rows per C3 partition) is filled with -1 on pool threads while the epochs
+            # run (numpy releases the GIL for the fill); the events go in at the end
+            pool = self._pool()
+            out_f = [pool.submit(np.full, (ps.nb - 1, 2), -1, np.int64) for ps in pss]
+            self._mark("batch-0 shuffles")
             while True:
                 live = [ps for ps in pss if not ps.done]
                 if not live:
                     break
                 self._epoch(live)
-            return [ps.out for ps in pss]
+            outs = []
+            for ps, f in zip(pss, out_f):
+                out = f.result()
+                for r, c, v in ps.ev:
+                    out[r, c] = v
+                outs.append(out)
+            return outs
         finally:
             for ps in started:
                 ns = self.shuffles[ps.i].numpy_state(ps.P)
@@ -646,6 +711,23 @@ class BatchRunner:
             self.gen_stream.synchronize()
             self.tab_stream.synchronize()
 
+    def _enqueue_rest(self):
+        """The partitions' whole streams, in growing pieces on the side streams (the first
+        piece is enqueued by run())."""
+        if self._gen_rest is None:
+            return
+        tp = time.perf_counter()
+        upto, total, pss = self._gen_rest
+        self._gen_rest = None
+        pb = self.s.per_batch
+        while upto < total:
+            upto = min(total, upto + min(upto, GEN_PIECE_MAX))
+            self._ensure_all([(ps.i, min(upto, int(ps.nb * expected_draws_per_batch(pb) * 1.02))) for ps in pss],
+                             wait=False)
+        if self.timing:
+            self.stats.prep_s += time.perf_counter() - tp
+        self._mark("generation enqueued")
+
     def _epoch(self, live):
         s, st, pb, stream = self.s, self.stats, self.s.per_batch, self.stream
         t0 = time.perf_counter()
@@ -653,7 +735,10 @@ class BatchRunner:
         need = [ps for ps in live if ps.retrain]
         for ps in live:
             ps.P_after_first = None
+        self._mark("epoch")
         work = self._refit_prep(need) if need else []
+        self._enqueue_rest()
+        self._mark("refit prep")
         for ps in live:
             if ps not in need:
                 ps.g0 = ps.j
@@ -673,7 +758,7 @@ class BatchRunner:
         self._ensure_all([(ps.i, ps.P + self.shuffles[ps.i].window_draws(ps.Wg) + self.n_words) for ps in live])
         if shuf:
             max_W = max(ps.Wg for ps in shuf)
-            max_pieces = max(2 + self.shuffles[ps.i].window_draws(ps.Wg) // 8192 for ps in shuf)
+            max_pieces = max(2 + 64 + self.shuffles[ps.i].window_draws(ps.Wg) // 8192 for ps in shuf)
         tails = [ps for ps in live if ps.tail]
         shuffled = False
         if tails:
@@ -725,11 +810,13 @@ class BatchRunner:
             self.ctrl_d[:self.o_stage].copy_(self.ctrl_h[:self.o_stage], non_blocking=True)
         if shuf and not shuffled:
             kernels.shuffle_window_batch(self.jobs, len(shuf), max_W, max_pieces, pb, stream, self.t_shuf)
+        self._mark("tables + upload")
         if late_fit:
             # the window shuffles do not depend on the new forests: they run on the GPU
             # while the host fits them
             self._refit_fit(work)
             self._segment_table(live)
+            self._mark("host fits")
         kernels.forest_predict_batch(self.segs, len(live), pb, stream, self.t_pred)
         if self.predict_log is not None:
             self.predict_log.append((self.segs.rec[:len(live)].copy(), len(live), pb))
@@ -755,7 +842,9 @@ class BatchRunner:
                 self.t_fit[1].record(stream)
         with torch.cuda.stream(stream):
             self.ctrl_h.copy_(self.ctrl_d, non_blocking=True)
+        self._mark("launched")
         stream.synchronize()
+        self._mark("synchronized")
         if self.timing:
             st.predict_ms += self.t_pred.elapsed_ms()
             st.scan_ms += self.t_scan.elapsed_ms()
@@ -796,13 +885,13 @@ class BatchRunner:
                 for c in range(2):
                     hit = np.nonzero(ev[:, c] >= 0)[0]
                     b = ps.j + hit
-                    ps.out[b - 1, c] = b * pb + ev[hit, c].astype(np.int64)
+                    ps.ev.append((b - 1, c, b * pb + ev[hit, c].astype(np.int64)))
             elif nev:
                 rec = self._sview("ev", ps.i, np.int32, 3 * self.max_events)[:3 * int(info[1])].reshape(-1, 3)
                 b = ps.j + rec[:, 0].astype(np.int64)
                 for c in range(2):
                     hit = rec[:, 1 + c] >= 0
-                    ps.out[b[hit] - 1, c] = b[hit] * pb + rec[hit, 1 + c].astype(np.int64)
+                    ps.ev.append((b[hit] - 1, c, b[hit] * pb + rec[hit, 1 + c].astype(np.int64)))
             picked = int(self.pick_h[ps.i]) if ps.Wg else -1
             # RNG position right after the last consumed batch shuffle
             if stop >= 0:

@@ -26,10 +26,11 @@ SEG_DTYPE = np.dtype([("X", "<u8"), ("ld", "<i8"), ("y", "<u8"), ("perm", "<u8")
                       ("cf_tab_words", "<i4"), ("pad", "<i4")])
 SEG_FIRST_ERR_PRESET = 1
 assert SEG_DTYPE.itemsize == 176
-JOB_DTYPE = np.dtype([("R", "<u8"), ("Tsub", "<u8"), ("Tchunk", "<u8"), ("avail", "<i8"), ("P", "<i8"), ("W", "<i8"),
+JOB_DTYPE = np.dtype([("R", "<u8"), ("Tpre", "<u8"), ("Tchunk", "<u8"), ("avail", "<i8"), ("P", "<i8"), ("W", "<i8"),
                       ("pieces", "<u8"), ("info", "<u8"), ("J", "<u8"), ("E", "<u8"), ("perm_out", "<u8"),
-                      ("stop", "<u8"), ("pick_offset", "<i8"), ("pick_last", "<i8"), ("pick_out", "<u8")])
-assert JOB_DTYPE.itemsize == 120
+                      ("stop", "<u8"), ("pick_offset", "<i8"), ("pick_last", "<i8"), ("pick_out", "<u8"),
+                      ("first", "<u8")])
+assert JOB_DTYPE.itemsize == 128
 GEN_DTYPE = np.dtype([("state", "<u8"), ("R", "<u8"), ("n", "<i8")])
 STAGE_DTYPE = np.dtype([("X", "<u8"), ("ld", "<i8"), ("y", "<u8"), ("perm", "<u8"), ("base", "<i8"), ("ev", "<u8"),
                         ("stop", "<u8"), ("pick", "<u8"), ("R", "<u8"), ("j", "<i8"), ("g0", "<i8"), ("nb", "<i8"),

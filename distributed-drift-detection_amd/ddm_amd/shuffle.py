@@ -120,8 +120,10 @@ class GpuShuffle:
         self.max_window = int(max_window)
         self.mt = torch.zeros(625, dtype=torch.int32, device=device)
         self._alloc(max(2 * CHUNK, int(capacity_draws)))
-        self.max_pieces = 4 + (self.max_window * L * 3) // CHUNK
+        # the window's first piece, the sub-chunks of the chunk holding its start, then chunks
+        self.max_pieces = 4 + CHUNK // SUB + (self.max_window * L * 3) // CHUNK
         self.pieces = torch.empty(self.max_pieces * 16, dtype=torch.uint8, device=device)
+        self.first = torch.empty((CHUNK // SUB) * self.S, dtype=torch.int16, device=device)
         self.info = torch.zeros(3, dtype=torch.int64, device=device)
         self.J = torch.zeros(self.max_window * L, dtype=torch.uint8, device=device)
         self.E = torch.zeros(self.max_window, dtype=torch.int64, device=device)
@@ -132,22 +134,21 @@ class GpuShuffle:
         self.init_key = None
         self.init_pos = 624
         self.seg = None
-        self.jump_scratch = None
         self.n_seg = self.jumped = 0
         self._keep = []          # pinned job tables read by in-flight async copies
 
     def _alloc(self, cap):
         cap = (cap + CHUNK - 1) // CHUNK * CHUNK
         R = torch.empty(cap, dtype=torch.int32, device=self.device)
-        Ts = torch.empty(cap // SUB * self.S, dtype=torch.int16, device=self.device)
+        Tp = torch.empty(cap // SUB * self.S, dtype=torch.int32, device=self.device)   # prefix tables [chunk][64][S]
         Tc = torch.empty(cap // CHUNK * self.S, dtype=torch.int32, device=self.device)
         if getattr(self, "R", None) is not None and self.gen:
             torch.cuda.synchronize(self.device)          # rare: growth past the initial estimate
             R[:self.gen].copy_(self.R[:self.gen])
-            Ts[:self.tab * (CHUNK // SUB) * self.S].copy_(self.Tsub[:self.tab * (CHUNK // SUB) * self.S])
+            Tp[:self.tab * (CHUNK // SUB) * self.S].copy_(self.Tpre[:self.tab * (CHUNK // SUB) * self.S])
             Tc[:self.tab * self.S].copy_(self.Tchunk[:self.tab * self.S])
             torch.cuda.synchronize(self.device)
-        self.R, self.Tsub, self.Tchunk, self.cap = R, Ts, Tc, cap
+        self.R, self.Tpre, self.Tchunk, self.cap = R, Tp, Tc, cap
 
     def reset(self, rng):
         """Draw 0 of the device stream = the next draw of `rng` (an MTStream)."""
@@ -193,8 +194,10 @@ class GpuShuffle:
     def _segments_for(self, draws):
         return max(1, (int(draws) - (624 - self.init_pos)) // JUMP + 1)
 
-    def _jump_to(self, n_seg):
-        """Start states of segments [jumped, n_seg) on gen_stream (ddm_mt_jump, one launch)."""
+    def _jump_to(self, n_seg, out=None):
+        """Start states of segments [jumped, n_seg) on gen_stream (ddm_mt_jump, one launch);
+        with `out` (a list) the JUMP_DTYPE records are appended to it instead, for one
+        launch over many partitions."""
         if n_seg <= self.jumped:
             return
         if n_seg > self.seg.shape[0]:
@@ -204,23 +207,29 @@ class GpuShuffle:
                 seg[:self.seg.shape[0]].copy_(self.seg)
             self.seg = seg
         nj = n_seg - self.jumped
-        if self.jump_scratch is None or self.jump_scratch.shape[0] < nj:
-            torch.cuda.synchronize(self.device)
-            self.jump_scratch = torch.empty((nj, kernels.JUMP_SCRATCH_WORDS), dtype=torch.int32, device=self.device)
         polys = kernels.mt_jump_polys(JUMP, n_seg - 1, self.device)
+        segs = np.arange(self.jumped, n_seg, dtype=np.uint64)
+        rec = np.empty(nj, dtype=kernels.JUMP_DTYPE)
+        rec["key"] = self.mt.data_ptr()
+        rec["poly"] = polys.data_ptr() + (segs - 1) * (8 * kernels.POLY_WORDS)
+        rec["out"] = self.seg.data_ptr() + segs * (4 * self.seg.shape[1])
+        rec["scratch"] = 0                  # the jump's word sequence lives in LDS
+        self.jumped = n_seg
+        if out is not None:
+            out.append(rec)
+            return
         tab = kernels.PinnedTable(kernels.JUMP_DTYPE, nj, self.device)
-        for k, s in enumerate(range(self.jumped, n_seg)):
-            tab.rec[k] = (self.mt.data_ptr(), polys[s - 1].data_ptr(), self.seg[s].data_ptr(),
-                          self.jump_scratch[k].data_ptr())
+        tab.rec[:nj] = rec
         kernels.mt_jump(tab, nj, self.gen_stream)
         self._keep.append(tab)
-        self.jumped = n_seg
 
-    def gen_request(self, upto):
+    def gen_request(self, upto, jumps=None):
         """Grow R to cover draws [0, upto) plus one chunk; returns the (state, R, n) generate
         jobs still to launch on gen_stream (one per segment the new draws touch; every
         segment's state slot continues where its previous piece stopped) and the chunk count
-        the tables must reach."""
+        the tables must reach.  Segment start states still missing are jumped to on
+        gen_stream first, or (jumps: a list) their records are appended for the caller's
+        one launch, which must precede the generate jobs."""
         need_chunks = self.chunks_for(upto)
         target = need_chunks * CHUNK
         if target > self.cap:
@@ -229,7 +238,7 @@ class GpuShuffle:
         if target > self.gen:
             s_last = self._segments_for(target - 1) - 1
             if s_last >= 1:                 # every segment of the expected stream at once
-                self._jump_to(max(s_last + 1, self.n_seg))
+                self._jump_to(max(s_last + 1, self.n_seg), jumps)
             s = self._segments_for(self.gen) - 1 if self.gen else 0
             while s <= s_last:
                 lo, hi = max(self.gen, self.seg_start(s)), min(target, self.seg_start(s + 1))
@@ -244,7 +253,7 @@ class GpuShuffle:
         caller makes tab_stream wait for gen_stream when they differ)."""
         if need_chunks > self.tab:
             check(lib.ddm_shuffle_tables(self.R.data_ptr(), self.tab, need_chunks - self.tab, self.L,
-                                         self.Tsub.data_ptr(), self.Tchunk.data_ptr(), self._tp()),
+                                         self.Tpre.data_ptr(), self.Tchunk.data_ptr(), self._tp()),
                   "ddm_shuffle_tables")
             self.tab = need_chunks
 
@@ -290,15 +299,16 @@ class GpuShuffle:
     def job_tuple(self, P, W, perm_out_ptr, stop_ptr=0, pick_offset=0, pick_last=0, pick_out_ptr=0):
         """fill_job's record as a tuple in kernels.JOB_DTYPE field order."""
         assert 0 <= W <= self.max_window
-        return (self.R.data_ptr(), self.Tsub.data_ptr(), self.Tchunk.data_ptr(), self.waited * CHUNK, int(P), int(W),
+        return (self.R.data_ptr(), self.Tpre.data_ptr(), self.Tchunk.data_ptr(), self.waited * CHUNK, int(P), int(W),
                 self.pieces.data_ptr(), self.info.data_ptr(), self.J.data_ptr(), self.E.data_ptr(), int(perm_out_ptr),
-                int(stop_ptr), int(pick_offset), int(pick_last), int(pick_out_ptr))
+                int(stop_ptr), int(pick_offset), int(pick_last), int(pick_out_ptr), self.first.data_ptr())
 
     def fill_job(self, rec, P, W, perm_out_ptr, stop_ptr=0, pick_offset=0, pick_last=0, pick_out_ptr=0):
         """One ddm_shuffle_job record (kernels.JOB_DTYPE) for a window of W batches from draw P;
         R must already cover it (window_draws)."""
         assert 0 <= W <= self.max_window
-        rec["R"], rec["Tsub"], rec["Tchunk"] = self.R.data_ptr(), self.Tsub.data_ptr(), self.Tchunk.data_ptr()
+        rec["R"], rec["Tpre"], rec["Tchunk"] = self.R.data_ptr(), self.Tpre.data_ptr(), self.Tchunk.data_ptr()
+        rec["first"] = self.first.data_ptr()
         rec["avail"], rec["P"], rec["W"] = self.waited * CHUNK, int(P), int(W)
         rec["pieces"], rec["info"] = self.pieces.data_ptr(), self.info.data_ptr()
         rec["J"], rec["E"], rec["perm_out"] = self.J.data_ptr(), self.E.data_ptr(), int(perm_out_ptr)
@@ -311,10 +321,11 @@ class GpuShuffle:
         assert 0 < W <= self.max_window and perm_out.numel() >= W * self.L
         self.ensure(P + self.window_draws(W))
         ev = (None, None) if timer is None else (timer.ev[0], timer.ev[1])
-        check(lib.ddm_shuffle_window(self.R.data_ptr(), self.Tsub.data_ptr(), self.Tchunk.data_ptr(),
+        check(lib.ddm_shuffle_window(self.R.data_ptr(), self.Tpre.data_ptr(), self.Tchunk.data_ptr(),
                                      self.waited * CHUNK, int(P), int(W), self.L, self.pieces.data_ptr(),
                                      self.max_pieces, self.info.data_ptr(), self.J.data_ptr(), self.E.data_ptr(),
-                                     perm_out.data_ptr(), self._sp(), *ev), "ddm_shuffle_window")
+                                     perm_out.data_ptr(), self.first.data_ptr(), self._sp(), *ev),
+              "ddm_shuffle_window")
 
     def pick(self, stop_ptr, W, offset, last, out_ptr):
         check(lib.ddm_shuffle_pick(stop_ptr, self.E.data_ptr(), int(W), int(offset), int(last), out_ptr, self._sp()),

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 11
+#define DDM_AMD_ABI_VERSION 12
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -309,31 +309,35 @@ int ddm_words_perm_seeds(const uint32_t* words, int64_t n_words, int32_t L, int3
  * followed by pos; it is advanced in place (one workgroup, 624-word blocks in LDS). */
 int ddm_shuffle_generate(uint32_t* mt_state, uint32_t* R, int64_t n, ddm_stream_t stream);
 
-/* FSM tables for chunks [chunk0, chunk0+nchunk) of R: Tsub uint16 [sub][batch_len-1],
- * Tchunk uint32 [chunk][batch_len-1] (end interval | batches completed << 8). */
+/* FSM tables for chunks [chunk0, chunk0+nchunk) of R, for a chunk entered in interval
+ * state s (1..batch_len-1): Tpre uint32 [chunk][64][batch_len-1] = interval state after
+ * sub-chunks 0..k | batches completed since the chunk start << 8, and Tchunk uint32
+ * [chunk][batch_len-1] = Tpre[chunk][63]. */
 int ddm_shuffle_tables(const uint32_t* R, int64_t chunk0, int64_t nchunk, int32_t batch_len,
-                       uint16_t* Tsub, uint32_t* Tchunk, ddm_stream_t stream);
+                       uint32_t* Tpre, uint32_t* Tchunk, ddm_stream_t stream);
 
 /* Shuffles of W consecutive batches whose first draw is R[P] (a batch boundary):
  * perm_out[b*batch_len + k] (uint8) and E[b] = index of the draw completing batch b.
  * avail = draws covered by tables (multiple of DDM_SHUFFLE_CHUNK); pieces (device,
- * >= max_pieces * 16 bytes) and J (device, W*batch_len bytes) are scratch; info
- * (device int64[3]) = {pieces, end draw, batches reached} (batches reached < W means
- * avail was too small). */
-int ddm_shuffle_window(const uint32_t* R, const uint16_t* Tsub, const uint32_t* Tchunk, int64_t avail,
+ * >= max_pieces * 16 bytes, max_pieces >= 66 + W*batch_len*3/DDM_SHUFFLE_CHUNK), J
+ * (device, W*batch_len bytes) and first (device, 64*(batch_len-1) uint16: tables of the
+ * chunk holding P) are scratch; info (device int64[3]) = {pieces, end draw, batches
+ * reached} (batches reached < W means avail was too small). */
+int ddm_shuffle_window(const uint32_t* R, const uint32_t* Tpre, const uint32_t* Tchunk, int64_t avail,
                        int64_t P, int64_t W, int32_t batch_len, void* pieces, int64_t max_pieces,
-                       int64_t* info, uint8_t* J, int64_t* E, uint8_t* perm_out, ddm_stream_t stream,
-                       ddm_event_t ev_begin, ddm_event_t ev_end);
+                       int64_t* info, uint8_t* J, int64_t* E, uint8_t* perm_out, uint16_t* first,
+                       ddm_stream_t stream, ddm_event_t ev_begin, ddm_event_t ev_end);
 
 /* Batched forms (one job per partition, device array of jobs; W = 0 skips a job). */
 typedef struct ddm_gen_job { uint32_t* mt_state; uint32_t* R; int64_t n; } ddm_gen_job;
 typedef struct ddm_shuffle_job {
-    const uint32_t* R; const uint16_t* Tsub; const uint32_t* Tchunk;
+    const uint32_t* R; const uint32_t* Tpre; const uint32_t* Tchunk;
     int64_t avail, P, W;
     void* pieces; int64_t* info; uint8_t* J; int64_t* E; uint8_t* perm_out;
     const int32_t* stop;            /* ddm_shuffle_pick_batch: scan stop flag (may be NULL) */
     int64_t pick_offset, pick_last; /* pick E[(stop >= 0 ? stop : pick_last) - pick_offset] */
     int64_t* pick_out;              /* may be NULL: no pick for this job                   */
+    uint16_t* first;                /* scratch, 64*(batch_len-1) uint16 (see ddm_shuffle_window) */
 } ddm_shuffle_job;
 
 int ddm_shuffle_generate_batch(const ddm_gen_job* jobs_dev, int32_t n_jobs, ddm_stream_t stream);
@@ -346,7 +350,8 @@ int ddm_shuffle_generate_batch(const ddm_gen_job* jobs_dev, int32_t n_jobs, ddm_
  * ddm_mt_jump (device): per job, out[0..623] = the MT19937 state (numpy key layout,
  *   pos 624) T^e(key) for the polynomial x^e mod phi in poly, and out[624] = 624.  The
  *   lower 31 bits of out[0] are not part of the state (never read by the generator).
- *   scratch: DDM_MT_JUMP_SCRATCH_WORDS device words per job.
+ *   scratch: unused, may be NULL (the word sequence x_0 .. x_{623 + deg} of
+ *   DDM_MT_JUMP_SCRATCH_WORDS words lives in the workgroup's LDS).
  *   Replaces nothing in the reference: the streams are those of DDM_Process.py:187,190,102. */
 #define DDM_MT_POLY_WORDS 312
 #define DDM_MT_JUMP_SCRATCH_WORDS 21216

@@ -127,3 +127,38 @@ def test_raw_stream_default_segments():
     rs.randint(0, 2**32, 77, dtype=np.uint64)
     want = rs.randint(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
     assert np.array_equal(got, want), int(np.argmax(got != want))
+
+
+def _host_prefix(words, L, chunks):
+    """Tpre[c][k][s-1] by direct simulation: every start state through the chunk's draws."""
+    S = L - 1
+    masks = np.array([0] + [(1 << int(s).bit_length()) - 1 for s in range(1, S + 1)], dtype=np.uint64)
+    out = np.zeros((chunks, 64, S), dtype=np.uint32)
+    for c in range(chunks):
+        st = np.arange(1, S + 1)
+        done = np.zeros(S, dtype=np.int64)
+        for k in range(64):
+            for v in words[c * 8192 + k * 128: c * 8192 + (k + 1) * 128].astype(np.uint64):
+                acc = (v & masks[st]) <= st
+                wrap = acc & (st == 1)
+                done += wrap
+                st = np.where(wrap, S, np.where(acc, st - 1, st))
+            out[c, k] = st | (done << 8)
+    return out
+
+
+@pytest.mark.parametrize("L", [100, 2, 37, 256])
+def test_prefix_tables_equal_direct_simulation(L):
+    """k_fsm_prefix (coupled trajectories merged) == every start state simulated alone."""
+    sh = _mk(L, cap=1 << 17)
+    mt = MTStream.from_seed(1234 + L)
+    sh.reset(mt)
+    chunks = 3
+    sh.ensure(chunks * 8192)
+    torch.cuda.synchronize()
+    words = sh.words(0, chunks * 8192).copy()
+    want = _host_prefix(words, L, chunks)
+    got = sh.Tpre[:chunks * 64 * (L - 1)].cpu().numpy().view(np.uint32).reshape(chunks, 64, L - 1)
+    assert np.array_equal(got, want)
+    tc = sh.Tchunk[:chunks * (L - 1)].cpu().numpy().view(np.uint32).reshape(chunks, L - 1)
+    assert np.array_equal(tc, want[:, 63])
