@@ -209,9 +209,11 @@ __device__ __forceinline__ void fsm_step(uint32_t v, uint32_t& s, uint32_t& d, u
 // over the 128 draws (LDS rows, 16-byte reads), merges the ones that met (LDS atomicMin
 // on the end state picks the survivor), renumbers the survivors in order, and writes
 // every start state's entry through its trajectory index plus a done offset.  After the
-// first sub-chunks ~16 trajectories per chunk remain, one pass of 256 lanes for all 16
+// first sub-chunks ~16 trajectories per chunk remain, one pass of 128 lanes for all 8
 // chunks: ~6x fewer FSM steps than stepping every start state through every sub-chunk.
-constexpr int kPreChunks = 16;
+// (8 chunks and 2 waves per workgroup: ~20 KB of LDS, so 8 workgroups share a CU.)
+constexpr int kPreChunks = 8;
+constexpr int kPreThreads = 128;    // 8 chunks x ~16 trajectories once they have coupled
 constexpr int kPreRow = kSub + 4;   // LDS row stride in words: 16-byte rows, the chunks' rows in distinct banks
 
 size_t prefix_lds_bytes(int L) {
@@ -219,13 +221,22 @@ size_t prefix_lds_bytes(int L) {
     return (size_t)kPreChunks * kPreRow * 4 + (size_t)kPreChunks * (S + 1) * 4 + NP * (6 * 2 + 4 * 1);
 }
 
-__global__ __launch_bounds__(256) void k_fsm_prefix(const uint32_t* __restrict__ R, int64_t chunk0, int64_t nchunk,
-                                                    int L, uint32_t* __restrict__ Tpre, uint32_t* __restrict__ Tchunk) {
+struct TabJob {
+    const uint32_t* R;
+    int64_t chunk0, nchunk;
+    uint32_t* Tpre;
+    uint32_t* Tchunk;
+};
+
+__device__ void fsm_prefix(const uint32_t* __restrict__ R, int64_t chunk0, int64_t nchunk, int L,
+                           uint32_t* __restrict__ Tpre, uint32_t* __restrict__ Tchunk, int64_t blk) {
     extern __shared__ __attribute__((aligned(16))) uint32_t pre_lds[];
-    __shared__ int wsum[4];
+    constexpr int kW = kPreThreads / 64;
+    __shared__ int wsum[kW];
     __shared__ int n_sh;
     const int S = L - 1, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int64_t cb = chunk0 + (int64_t)blockIdx.x * kPreChunks;
+    const int64_t cb = chunk0 + blk * kPreChunks;
+    if (cb >= chunk0 + nchunk) return;
     const int nc = (int)min((int64_t)kPreChunks, chunk0 + nchunk - cb);
     const int NP = kPreChunks * S;
     uint32_t* draws = pre_lds;                                              // [16][kPreRow]
@@ -241,7 +252,7 @@ __global__ __launch_bounds__(256) void k_fsm_prefix(const uint32_t* __restrict__
     uint8_t* ch = st2 + NP;
     uint8_t* ch2 = ch + NP;
     const int ns = nc * S;
-    for (int e = tid; e < ns; e += 256) {
+    for (int e = tid; e < ns; e += kPreThreads) {
         st[e] = (uint8_t)(e % S + 1);
         dn[e] = 0;
         ch[e] = (uint8_t)(e / S);
@@ -251,14 +262,14 @@ __global__ __launch_bounds__(256) void k_fsm_prefix(const uint32_t* __restrict__
     if (tid == 0) n_sh = ns;
     for (int k = 0; k < kSubPerChunk; ++k) {
         __syncthreads();
-        for (int e = tid; e < nc * (kSub / 4); e += 256) {
+        for (int e = tid; e < nc * (kSub / 4); e += kPreThreads) {
             const int c = e / (kSub / 4), q = e % (kSub / 4);
             *reinterpret_cast<uint4*>(draws + c * kPreRow + 4 * q) =
                 *reinterpret_cast<const uint4*>(R + (cb + c) * kChunk + (int64_t)k * kSub + 4 * q);
         }
         __syncthreads();
         const int n = n_sh;
-        for (int p = tid; p < n; p += 256) {
+        for (int p = tid; p < n; p += kPreThreads) {
             uint32_t s = st[p], d = dn[p];
             const uint32_t* row = draws + ch[p] * kPreRow;
 #pragma unroll 4
@@ -273,12 +284,12 @@ __global__ __launch_bounds__(256) void k_fsm_prefix(const uint32_t* __restrict__
             dn2[p] = (uint16_t)d;
             ch2[p] = ch[p];
         }
-        for (int e = tid; e < nc * (S + 1); e += 256) owner[e] = 0x7fffffff;
+        for (int e = tid; e < nc * (S + 1); e += kPreThreads) owner[e] = 0x7fffffff;
         __syncthreads();
-        for (int p = tid; p < n; p += 256) atomicMin(&owner[ch2[p] * (S + 1) + st2[p]], p);
+        for (int p = tid; p < n; p += kPreThreads) atomicMin(&owner[ch2[p] * (S + 1) + st2[p]], p);
         __syncthreads();
         // survivors: the first trajectory of each (chunk, end state), renumbered in order
-        const int per = (n + 255) / 256;
+        const int per = (n + kPreThreads - 1) / kPreThreads;
         const int p0 = min(n, tid * per), p1 = min(n, p0 + per);
         int cnt = 0;
         for (int p = p0; p < p1; ++p) cnt += owner[ch2[p] * (S + 1) + st2[p]] == p ? 1 : 0;
@@ -295,9 +306,9 @@ __global__ __launch_bounds__(256) void k_fsm_prefix(const uint32_t* __restrict__
         int idx = base + inc - cnt;
         for (int p = p0; p < p1; ++p)
             if (owner[ch2[p] * (S + 1) + st2[p]] == p) nidx[p] = (int16_t)idx++;
-        if (tid == 255) n_sh = base + inc;
+        if (tid == kPreThreads - 1) n_sh = base + inc;
         __syncthreads();
-        for (int p = tid; p < n; p += 256) {
+        for (int p = tid; p < n; p += kPreThreads) {
             const int o = owner[ch2[p] * (S + 1) + st2[p]];
             if (o != p) {
                 nidx[p] = nidx[o];
@@ -308,7 +319,7 @@ __global__ __launch_bounds__(256) void k_fsm_prefix(const uint32_t* __restrict__
         }
         __syncthreads();
         // every start state's entry; then its trajectory after the merge
-        for (int e = tid; e < ns; e += 256) {
+        for (int e = tid; e < ns; e += kPreThreads) {
             const int i = cls[e], o = off[e];
             const uint32_t val = (uint32_t)st2[i] | ((uint32_t)((int)dn2[i] + o) << 8);
             const int64_t c = cb + e / S;
@@ -318,7 +329,7 @@ __global__ __launch_bounds__(256) void k_fsm_prefix(const uint32_t* __restrict__
             cls[e] = nidx[i];
             off[e] = (int16_t)(o + dlt[i]);
         }
-        for (int p = tid; p < n; p += 256)
+        for (int p = tid; p < n; p += kPreThreads)
             if (owner[ch2[p] * (S + 1) + st2[p]] == p) {
                 const int q = nidx[p];
                 st[q] = st2[p];
@@ -326,6 +337,17 @@ __global__ __launch_bounds__(256) void k_fsm_prefix(const uint32_t* __restrict__
                 ch[q] = ch2[p];
             }
     }
+}
+
+__global__ __launch_bounds__(kPreThreads) void k_fsm_prefix(const uint32_t* __restrict__ R, int64_t chunk0,
+                                                            int64_t nchunk, int L, uint32_t* __restrict__ Tpre,
+                                                            uint32_t* __restrict__ Tchunk) {
+    fsm_prefix(R, chunk0, nchunk, L, Tpre, Tchunk, blockIdx.x);
+}
+
+__global__ __launch_bounds__(kPreThreads) void k_fsm_prefix_batch(const TabJob* __restrict__ jobs, int L) {
+    const TabJob j = jobs[blockIdx.y];
+    fsm_prefix(j.R, j.chunk0, j.nchunk, L, j.Tpre, j.Tchunk, blockIdx.x);
 }
 
 struct Job {
@@ -708,9 +730,24 @@ extern "C" int ddm_shuffle_tables(const uint32_t* R, int64_t chunk0, int64_t nch
     }
     if (nchunk == 0) return 0;
     const int64_t blocks = ddm::ceil_div(nchunk, (int64_t)kPreChunks);
-    hipLaunchKernelGGL(k_fsm_prefix, dim3((unsigned)blocks), dim3(256), prefix_lds_bytes(batch_len), ddm::as_hip(stream),
-                       R, chunk0, nchunk, (int)batch_len, Tpre, Tchunk);
+    hipLaunchKernelGGL(k_fsm_prefix, dim3((unsigned)blocks), dim3(kPreThreads), prefix_lds_bytes(batch_len),
+                       ddm::as_hip(stream), R, chunk0, nchunk, (int)batch_len, Tpre, Tchunk);
     return ddm::launch_status("ddm_shuffle_tables");
+}
+
+extern "C" int ddm_shuffle_tables_batch(const ddm_table_job* jobs_dev, int32_t n_jobs, int64_t max_chunks,
+                                        int32_t batch_len, ddm_stream_t stream) {
+    if (!jobs_dev || n_jobs < 0 || max_chunks < 0 || batch_len < 2 || batch_len > 256) {
+        ddm::set_error("ddm_shuffle_tables_batch: invalid argument");
+        return DDM_E_ARG;
+    }
+    if (n_jobs == 0 || max_chunks == 0) return 0;
+    static_assert(sizeof(TabJob) == sizeof(ddm_table_job), "TabJob must mirror ddm_table_job");
+    const int64_t blocks = ddm::ceil_div(max_chunks, (int64_t)kPreChunks);
+    hipLaunchKernelGGL(k_fsm_prefix_batch, dim3((unsigned)blocks, (unsigned)n_jobs), dim3(kPreThreads),
+                       prefix_lds_bytes(batch_len), ddm::as_hip(stream), reinterpret_cast<const TabJob*>(jobs_dev),
+                       (int)batch_len);
+    return ddm::launch_status("ddm_shuffle_tables_batch");
 }
 
 extern "C" int ddm_shuffle_window(const uint32_t* R, const uint32_t* Tpre, const uint32_t* Tchunk, int64_t avail,

@@ -67,6 +67,7 @@ SIGNATURES = {
     "ddm_shuffle_pick_batch": (ctypes.c_int, [_vp, _i32, _vp]),
     "ddm_shuffle_generate": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
     "ddm_shuffle_tables": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp]),
+    "ddm_shuffle_tables_batch": (ctypes.c_int, [_vp, _i32, _i64, _i32, _vp]),
     "ddm_shuffle_window": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
                                           _vp, _vp, _vp]),
     "ddm_shuffle_pick": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),

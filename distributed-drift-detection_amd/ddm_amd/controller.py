@@ -32,7 +32,7 @@ from . import dfit, kernels
 from .forest import upload_forests
 from .params import OUTPUT_COLUMNS, DDMSettings, infer_x_features
 from .rng import MTStream
-from .shuffle import GpuShuffle, expected_draws_per_batch, fy_from_words, perm_seeds_from_words
+from .shuffle import CHUNK, GpuShuffle, expected_draws_per_batch, fy_from_words, perm_seeds_from_words, untemper_state
 from .trainer import BatchForestTrainer
 
 # A window runs on ddm_scan_long when its carried detector is neither fresh nor trivial
@@ -278,6 +278,7 @@ class BatchRunner:
             o += self.stage_stride[key] * n
         self.ctrl_bytes = o
         self.ctrl_h = torch.zeros(self.ctrl_bytes, dtype=torch.uint8, pin_memory=True)
+        self._views = {}
         self.ctrl_d = torch.zeros(self.ctrl_bytes, dtype=torch.uint8, device=dev)
         c = self.ctrl_h.numpy()
         self.first_h = c[self.o_first:self.o_first + 8 * n].view(np.int64)
@@ -346,8 +347,14 @@ class BatchRunner:
         return self.ctrl_d.data_ptr() + self.stage_off[key] + self.stage_stride[key] * i
 
     def _sview(self, key, i, dtype, count):
-        a = self.stage_off[key] + self.stage_stride[key] * i
-        return self.ctrl_h.numpy()[a:a + np.dtype(dtype).itemsize * count].view(dtype)
+        """View of partition i's staging slot `key` in the pinned slab (memoised: the slab
+        never moves)."""
+        k = (key, i, dtype, count)
+        v = self._views.get(k)
+        if v is None:
+            a = self.stage_off[key] + self.stage_stride[key] * i
+            v = self._views[k] = self.ctrl_h.numpy()[a:a + np.dtype(dtype).itemsize * count].view(dtype)
+        return v
 
     def _ensure_all(self, wants, wait=True):
         """wants: [(partition index, draws needed)].  Partitions whose enqueued stream falls
@@ -377,8 +384,16 @@ class BatchRunner:
             g = torch.cuda.Event()
             g.record(self.gen_stream)
             self.tab_stream.wait_event(g)
+            recs = []
             for i, need in tabs:
-                self.shuffles[i].tables_to(need)
+                self.shuffles[i].tables_to(need, recs)
+            if recs:
+                # every partition's new chunks: one ddm_shuffle_tables_batch launch
+                tt = kernels.PinnedTable(kernels.TAB_DTYPE, len(recs), self.device)
+                tt.rec[:len(recs)] = np.array(recs, dtype=kernels.TAB_DTYPE)
+                kernels.shuffle_tables_batch(tt, len(recs), max(r[2] for r in recs), self.s.per_batch,
+                                             self.tab_stream)
+                self.gen_tables.append(tt)
             ev = torch.cuda.Event()
             ev.record(self.tab_stream)
             for i, _ in tabs:
@@ -527,53 +542,100 @@ class BatchRunner:
             ex.shutdown(wait=True)
             self._executor = None
 
+    # -- per-epoch tables: per-partition template records (the static fields), of which an
+    #    epoch takes the live partitions' rows and sets the fields that move
+    def _templates(self):
+        if getattr(self, "_tmpl", None) is not None:
+            return self._tmpl
+        n, pb, T = len(self.parts), self.s.per_batch, self.s.n_estimators
+        perm, err, ev = self.perm_all.data_ptr(), self.err_all.data_ptr(), self.ev_d.data_ptr()
+        seg = np.zeros(n, dtype=kernels.SEG_DTYPE)
+        stg = np.zeros(n, dtype=kernels.STAGE_DTYPE)
+        job = np.zeros(n, dtype=kernels.JOB_DTYPE)
+        for i, part in enumerate(self.parts):
+            Xp, ld, yp, F = part.X.data_ptr(), part.X.shape[1], part.y.data_ptr(), part.X.shape[0]
+            seg[i]["X"], seg[i]["ld"], seg[i]["y"], seg[i]["perm"], seg[i]["err"] = Xp, ld, yp, perm, err
+            seg[i]["first_err"], seg[i]["row_base"] = self._dptr(self.o_first, i, 8), self.bases[i]
+            seg[i]["flags"] = kernels.SEG_FIRST_ERR_PRESET
+            r = stg[i]
+            r["X"], r["ld"], r["y"], r["perm"], r["base"] = Xp, ld, yp, perm, self.bases[i]
+            r["ev"], r["stop"], r["pick"] = ev + 8 * self.ev_bases[i], self._dptr(self.o_stop, i, 4), \
+                self._dptr(self.o_pick, i, 8)
+            r["nb"], r["pb"], r["last_len"], r["n_features"] = self.nbs[i], pb, part.n - (self.nbs[i] - 1) * pb, F
+            r["n_words"], r["max_events"], r["n_trees"] = self.n_words, self.max_events, T
+            r["x_out"], r["y_out"], r["w_out"] = self._sptr("x", i), self._sptr("y", i), self._sptr("w", i)
+            r["info_out"], r["ev_out"], r["perm_w"], r["seeds_out"] = self._sptr("info", i), self._sptr("ev", i), \
+                perm, self._sptr("seeds", i)
+            sh = self.shuffles[i]
+            q = job[i]
+            q["pieces"], q["info"], q["J"], q["E"] = sh.pieces.data_ptr(), sh.info.data_ptr(), sh.J.data_ptr(), \
+                sh.E.data_ptr()
+            q["first"], q["pick_out"] = sh.first.data_ptr(), self._dptr(self.o_pick, i, 8)
+        self._tmpl = {"seg": seg, "stage": stg, "job": job, "forest": [None] * n, "ptrs": [None] * n,
+                      "dfit": np.array(self.dfit_rows, dtype=dfit.DFIT_DTYPE) if self.dfit_rows else None,
+                      "stop": np.array([self._dptr(self.o_stop, i, 4) for i in range(n)], dtype=np.uint64)}
+        return self._tmpl
+
+    def _stream_ptrs(self, live):
+        """Refresh the R / table pointers of partitions whose stream buffers were regrown."""
+        t = self._templates()
+        for ps in live:
+            p = self.shuffles[ps.i].ptrs
+            if t["ptrs"][ps.i] is not p:
+                t["ptrs"][ps.i] = p
+                t["job"][ps.i]["R"], t["job"][ps.i]["Tpre"], t["job"][ps.i]["Tchunk"] = p
+                t["stage"][ps.i]["R"] = p[0]
+        return t
+
     def _segment_table(self, live):
         """ddm_predict_segment records (forest predict) of this epoch."""
-        pb = self.s.per_batch
-        rows = []
-        perm, err = self.perm_all.data_ptr(), self.err_all.data_ptr()
+        t = self._templates()
+        seg = t["seg"]
         for ps in live:
-            part, d = self.parts[ps.i], ps.forest.desc
-            p0 = ps.base + ps.j * pb
-            p1 = ps.base + (ps.b_end - 1) * pb + ps.blen(ps.b_end - 1)
-            rows.append((part.X.data_ptr(), part.X.shape[1], part.y.data_ptr(), perm, err, 0,
-                         self._dptr(self.o_first, ps.i, 8), p0, p1, d.nodes, d.roots, d.leaf_value or 0, d.classes,
-                         d.n_trees, d.n_classes, d.n_nodes, d.pure, ps.base, 0, 0, d.cforest or 0, d.cf_slots,
-                         d.cf_vote_regs, d.cf_leaves, kernels.SEG_FIRST_ERR_PRESET, d.cf_tab_words, 0))
-        self.segs.rec[:len(rows)] = np.array(rows, dtype=kernels.SEG_DTYPE)
+            if t["forest"][ps.i] is not ps.forest:          # a new forest: its descriptor fields
+                t["forest"][ps.i] = ps.forest
+                d, r = ps.forest.desc, seg[ps.i]
+                r["nodes"], r["roots"], r["leaf_value"], r["classes"] = d.nodes, d.roots, d.leaf_value or 0, d.classes
+                r["n_trees"], r["n_classes"], r["n_nodes"], r["pure"] = d.n_trees, d.n_classes, d.n_nodes, d.pure
+                r["cforest"], r["cf_slots"], r["cf_vote_regs"] = d.cforest or 0, d.cf_slots, d.cf_vote_regs
+                r["cf_leaves"], r["cf_tab_words"] = d.cf_leaves, d.cf_tab_words
+        idx = [ps.i for ps in live]
+        rec = seg[idx]
+        rec["pos_begin"] = [ps.rng_rows[0] for ps in live]
+        rec["pos_end"] = [ps.rng_rows[1] for ps in live]
+        self.segs.rec[:len(idx)] = rec
 
     def _stage_table(self, live):
-        """ddm_stage_job records of this epoch (csrc/stage.hip), built as tuples and
-        stored with one structured-array assignment."""
-        pb, T = self.s.per_batch, self.s.n_estimators
-        perm, ev = self.perm_all.data_ptr(), self.ev_d.data_ptr()
-        rows = []
-        for ps in live:
-            part = self.parts[ps.i]
-            rows.append((part.X.data_ptr(), part.X.shape[1], part.y.data_ptr(), perm, ps.base, ev + 8 * ps.ev_base,
-                         self._dptr(self.o_stop, ps.i, 4), self._dptr(self.o_pick, ps.i, 8),
-                         self.shuffles[ps.i].R.data_ptr(), ps.j, ps.g0, ps.nb, ps.b_end,
-                         -1 if ps.P_after_first is None else ps.P_after_first,
-                         -1 if ps.P_tail_after is None else ps.P_tail_after, pb, ps.last_len, part.X.shape[0],
-                         self.n_words, int(bool(ps.tail)), self.max_events, self._sptr("x", ps.i),
-                         self._sptr("y", ps.i), self._sptr("w", ps.i), self._sptr("info", ps.i),
-                         self._sptr("ev", ps.i), perm, self._sptr("seeds", ps.i), T, 0))
-        self.stage_jobs.rec[:len(rows)] = np.array(rows, dtype=kernels.STAGE_DTYPE)
+        """ddm_stage_job records of this epoch (csrc/stage.hip)."""
+        t = self._stream_ptrs(live)
+        rec = t["stage"][[ps.i for ps in live]]
+        rec["j"] = [ps.j for ps in live]
+        rec["g0"] = [ps.g0 for ps in live]
+        rec["b_end"] = [ps.b_end for ps in live]
+        rec["p_after_first"] = [-1 if ps.P_after_first is None else ps.P_after_first for ps in live]
+        rec["p_tail_after"] = [-1 if ps.P_tail_after is None else ps.P_tail_after for ps in live]
+        rec["tail"] = [1 if ps.tail else 0 for ps in live]
+        self.stage_jobs.rec[:len(live)] = rec
 
     def _jobs_for(self, live, with_stop, upload=True):
         """Fill the job table for partitions with device shuffles this epoch."""
-        rows = []
+        t = self._stream_ptrs(live)
         pb = self.s.per_batch
-        for ps in live:
-            out_ptr = self.perm_all.data_ptr() + self.bases[ps.i] + ps.g0 * pb
-            if with_stop:
-                rows.append(self.shuffles[ps.i].job_tuple(ps.P, ps.Wg, out_ptr, self._dptr(self.o_stop, ps.i, 4),
-                                                          ps.g0 - ps.j, ps.b_end - 1 - ps.j,
-                                                          self._dptr(self.o_pick, ps.i, 8)))
-            else:                                # end of the window's GPU batches (tail epochs)
-                rows.append(self.shuffles[ps.i].job_tuple(ps.P, ps.Wg, out_ptr, 0, 0, ps.Wg - 1,
-                                                          self._dptr(self.o_pick, ps.i, 8)))
-        self.jobs.rec[:len(rows)] = np.array(rows, dtype=kernels.JOB_DTYPE)
+        idx = [ps.i for ps in live]
+        rec = t["job"][idx]
+        rec["avail"] = [self.shuffles[ps.i].waited * CHUNK for ps in live]
+        rec["P"] = [ps.P for ps in live]
+        rec["W"] = [ps.Wg for ps in live]
+        rec["perm_out"] = [self.perm_all.data_ptr() + self.bases[ps.i] + ps.g0 * pb for ps in live]
+        if with_stop:
+            rec["stop"] = t["stop"][idx]
+            rec["pick_offset"] = [ps.g0 - ps.j for ps in live]
+            rec["pick_last"] = [ps.b_end - 1 - ps.j for ps in live]
+        else:                                # end of the window's GPU batches (tail epochs)
+            rec["stop"] = 0
+            rec["pick_offset"] = 0
+            rec["pick_last"] = [ps.Wg - 1 for ps in live]
+        self.jobs.rec[:len(idx)] = rec
         if upload:
             self.jobs.upload(len(live), self.stream)
 
@@ -700,16 +762,34 @@ class BatchRunner:
                 for r, c, v in ps.ev:
                     out[r, c] = v
                 outs.append(out)
+            self._mark("outputs")
             return outs
         finally:
+            # every stream's numpy state after its last draw: one read-back for all
+            plans = [(ps, self.shuffles[ps.i].state_plan(ps.P)) for ps in started]
+            need = [(ps, start, pos) for ps, (start, pos) in plans if start is not None]
+            states = {ps.i: pos for ps, (start, pos) in plans if start is None}
+            if need:
+                for ps, start, _ in need:
+                    self.shuffles[ps.i].ensure(start + 624)
+                buf = torch.empty((len(need), 624), dtype=torch.int32, pin_memory=True)
+                with torch.cuda.stream(self.stream):
+                    for k, (ps, start, _) in enumerate(need):
+                        buf[k].copy_(self.shuffles[ps.i].R[start:start + 624], non_blocking=True)
+                self.stream.synchronize()
+                words = buf.numpy().view(np.uint32)
+                for k, (ps, _, pos) in enumerate(need):
+                    states[ps.i] = untemper_state(words[k], pos)
             for ps in started:
-                ns = self.shuffles[ps.i].numpy_state(ps.P)
+                ns = states[ps.i]
                 rngs[ps.i].key[:] = ns[1]
                 rngs[ps.i].pos.value = ns[2]
+            self._mark("rng states")
             # pieces of the streams may still be generated / tabulated ahead on the side
             # streams: nothing may write into this runner's buffers once the caller can free them
             self.gen_stream.synchronize()
             self.tab_stream.synchronize()
+            self._mark("side streams drained")
 
     def _enqueue_rest(self):
         """The partitions' whole streams, in growing pieces on the side streams (the first
@@ -804,7 +884,7 @@ class BatchRunner:
             self._jobs_for(shuf, with_stop=True, upload=False)
         self._stage_table(live)
         if self.dfit_rows:
-            self.dfit_jobs.rec[:len(live)] = np.array([self.dfit_rows[ps.i] for ps in live], dtype=dfit.DFIT_DTYPE)
+            self.dfit_jobs.rec[:len(live)] = self._templates()["dfit"][[ps.i for ps in live]]
         self.first_h[:] = -1                    # the predict kernels' first-error slots
         with torch.cuda.stream(stream):
             self.ctrl_d[:self.o_stage].copy_(self.ctrl_h[:self.o_stage], non_blocking=True)

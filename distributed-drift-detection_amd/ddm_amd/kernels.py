@@ -32,6 +32,7 @@ JOB_DTYPE = np.dtype([("R", "<u8"), ("Tpre", "<u8"), ("Tchunk", "<u8"), ("avail"
                       ("first", "<u8")])
 assert JOB_DTYPE.itemsize == 128
 GEN_DTYPE = np.dtype([("state", "<u8"), ("R", "<u8"), ("n", "<i8")])
+TAB_DTYPE = np.dtype([("R", "<u8"), ("chunk0", "<i8"), ("nchunk", "<i8"), ("Tpre", "<u8"), ("Tchunk", "<u8")])
 STAGE_DTYPE = np.dtype([("X", "<u8"), ("ld", "<i8"), ("y", "<u8"), ("perm", "<u8"), ("base", "<i8"), ("ev", "<u8"),
                         ("stop", "<u8"), ("pick", "<u8"), ("R", "<u8"), ("j", "<i8"), ("g0", "<i8"), ("nb", "<i8"),
                         ("b_end", "<i8"), ("p_after_first", "<i8"), ("p_tail_after", "<i8"), ("pb", "<i4"),
@@ -77,6 +78,13 @@ def epoch_stage(table, n_jobs, stream, upload=True):
         table.upload(n_jobs, stream)
     check(lib.ddm_epoch_stage(table.d.data_ptr(), int(n_jobs), ctypes.c_void_p(stream.cuda_stream)),
           "ddm_epoch_stage")
+
+
+def shuffle_tables_batch(table, n_jobs, max_chunks, batch_len, stream):
+    """Prefix tables of every job in a PinnedTable of TAB_DTYPE, one launch."""
+    table.upload(n_jobs, stream)
+    check(lib.ddm_shuffle_tables_batch(table.d.data_ptr(), int(n_jobs), int(max_chunks), int(batch_len),
+                                       ctypes.c_void_p(stream.cuda_stream)), "ddm_shuffle_tables_batch")
 
 
 def shuffle_generate_batch(table, n_jobs, stream):

@@ -47,6 +47,11 @@ def _untemper(y):
     return (u & 0xffffffff).astype(np.uint32)
 
 
+def untemper_state(words, pos):
+    """numpy's ('MT19937', key, pos) from 624 tempered stream words."""
+    return ("MT19937", _untemper(words), int(pos), 0, 0.0)
+
+
 def _temper(y):
     y = y.astype(np.uint64)
     y ^= y >> 11
@@ -149,6 +154,7 @@ class GpuShuffle:
             Tc[:self.tab * self.S].copy_(self.Tchunk[:self.tab * self.S])
             torch.cuda.synchronize(self.device)
         self.R, self.Tpre, self.Tchunk, self.cap = R, Tp, Tc, cap
+        self.ptrs = (R.data_ptr(), Tp.data_ptr(), Tc.data_ptr())    # changes only here
 
     def reset(self, rng):
         """Draw 0 of the device stream = the next draw of `rng` (an MTStream)."""
@@ -248,13 +254,18 @@ class GpuShuffle:
             self.gen = target
         return reqs, need_chunks
 
-    def tables_to(self, need_chunks):
+    def tables_to(self, need_chunks, out=None):
         """Tabulate up to need_chunks on tab_stream (ordered after the words they read: the
-        caller makes tab_stream wait for gen_stream when they differ)."""
+        caller makes tab_stream wait for gen_stream when they differ); with `out` (a list)
+        the TAB_DTYPE record is appended for the caller's one launch instead."""
         if need_chunks > self.tab:
-            check(lib.ddm_shuffle_tables(self.R.data_ptr(), self.tab, need_chunks - self.tab, self.L,
-                                         self.Tpre.data_ptr(), self.Tchunk.data_ptr(), self._tp()),
-                  "ddm_shuffle_tables")
+            if out is not None:
+                out.append((self.R.data_ptr(), self.tab, need_chunks - self.tab, self.Tpre.data_ptr(),
+                            self.Tchunk.data_ptr()))
+            else:
+                check(lib.ddm_shuffle_tables(self.R.data_ptr(), self.tab, need_chunks - self.tab, self.L,
+                                             self.Tpre.data_ptr(), self.Tchunk.data_ptr(), self._tp()),
+                      "ddm_shuffle_tables")
             self.tab = need_chunks
 
     def mark_ready(self, event):
@@ -357,13 +368,19 @@ class GpuShuffle:
                 return r[0], P + r[1]
             n *= 2
 
-    def numpy_state(self, X):
-        """numpy's ('MT19937', key, pos) after X draws of this stream."""
+    def state_plan(self, X):
+        """(None, state) when numpy's state after X draws needs no stream words, else
+        (start, pos): the state is the untempered words [start, start+624) at pos."""
         first = 624 - self.init_pos
         if X <= first:
-            return ("MT19937", self.init_key.copy(), self.init_pos + int(X), 0, 0.0)
+            return None, ("MT19937", self.init_key.copy(), self.init_pos + int(X), 0, 0.0)
         r = int(X) - first
         q = (r - 1) // 624
-        start = first + q * 624
-        key = _untemper(self.words(start, 624))
-        return ("MT19937", key, r - q * 624, 0, 0.0)
+        return first + q * 624, r - q * 624
+
+    def numpy_state(self, X):
+        """numpy's ('MT19937', key, pos) after X draws of this stream."""
+        start, pos = self.state_plan(X)
+        if start is None:
+            return pos
+        return ("MT19937", _untemper(self.words(start, 624)), pos, 0, 0.0)

@@ -315,6 +315,13 @@ int ddm_shuffle_generate(uint32_t* mt_state, uint32_t* R, int64_t n, ddm_stream_
  * [chunk][batch_len-1] = Tpre[chunk][63]. */
 int ddm_shuffle_tables(const uint32_t* R, int64_t chunk0, int64_t nchunk, int32_t batch_len,
                        uint32_t* Tpre, uint32_t* Tchunk, ddm_stream_t stream);
+/* The same for many streams in one launch (jobs_dev: device array; max_chunks >= every
+ * job's nchunk). */
+typedef struct ddm_table_job {
+    const uint32_t* R; int64_t chunk0, nchunk; uint32_t* Tpre; uint32_t* Tchunk;
+} ddm_table_job;
+int ddm_shuffle_tables_batch(const ddm_table_job* jobs_dev, int32_t n_jobs, int64_t max_chunks,
+                             int32_t batch_len, ddm_stream_t stream);
 
 /* Shuffles of W consecutive batches whose first draw is R[P] (a batch boundary):
  * perm_out[b*batch_len + k] (uint8) and E[b] = index of the draw completing batch b.

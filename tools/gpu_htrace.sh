@@ -12,4 +12,5 @@ prev = 0.0
 for k, (l, x) in enumerate(t[:60]):
     print(f'{x*1e3:9.2f} +{(x-prev)*1e3:7.2f} {l}'); prev = x
 print('...', len(t), 'marks, end', round(t[-1][1]*1e3, 2), 'ms')
+for l, x in t[-4:]: print(f'{x*1e3:9.2f} {l}')
 "
