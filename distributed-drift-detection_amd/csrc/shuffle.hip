@@ -412,6 +412,8 @@ __global__ __launch_bounds__(kFirstThreads) void k_fsm_first_batch(const Job* __
     fsm_first(j, L);
 }
 
+constexpr int kWalkThreads = 256;    // stage the table rows; lane 0 walks them
+
 // From draw P at a batch boundary: draw by draw to the next sub-chunk boundary, then by
 // the first-chunk tables (k_fsm_first) to the chunk boundary, then chunk by chunk (Tchunk)
 // until W batches are done.  Table rows are staged in LDS (all lanes load, lane 0 walks),
@@ -421,7 +423,7 @@ __global__ __launch_bounds__(kFirstThreads) void k_fsm_first_batch(const Job* __
 __device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restrict__ first,
                          const uint32_t* __restrict__ Tchunk, int64_t P, int64_t W, int L, int64_t avail,
                          ChunkStart* __restrict__ out, int64_t* __restrict__ info) {
-    extern __shared__ uint32_t tab[];   // [64][S] chunk rows; phase A: draws + first-chunk rows
+    extern __shared__ __attribute__((aligned(16))) uint32_t tab[];   // [64][S] chunk rows; phase A: draws + first-chunk rows
     __shared__ int64_t sh_pos, sh_batch, sh_k;
     __shared__ uint32_t sh_s;
     const int S = L - 1;
@@ -432,10 +434,8 @@ __device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restr
     const int n_subrows = (int)max((int64_t)0, (chunk_end - sub_end) / kSub);
     uint32_t* a_draws = tab;
     uint16_t* a_first = reinterpret_cast<uint16_t*>(tab + kSub);
-#pragma unroll 2
-    for (int k = threadIdx.x; k < n_draws; k += 64) a_draws[k] = R[P + k];
-#pragma unroll 8
-    for (int e = threadIdx.x; e < n_subrows * S; e += 64) a_first[e] = first[q0 * S + e];
+    for (int k = threadIdx.x; k < n_draws; k += kWalkThreads) a_draws[k] = R[P + k];
+    for (int e = threadIdx.x; e < n_subrows * S; e += kWalkThreads) a_first[e] = first[q0 * S + e];
     __syncthreads();
     if (threadIdx.x == 0) {
         int64_t pos = P, batch = 0, k = 0;
@@ -472,15 +472,22 @@ __device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restr
         const int64_t c0 = pos0 / kChunk;
         const int nload = (int)min((int64_t)64, (avail - pos0) / kChunk);
         __syncthreads();
-#pragma unroll 8
-        for (int e = threadIdx.x; e < nload * S; e += 64) tab[e] = Tchunk[c0 * S + e];
+        // the rows of 64 chunks (64*S words) with 16-byte loads from the aligned word at or
+        // before the first one (Tchunk is 16-byte aligned and padded by 4 words)
+        const int o = (int)((c0 * S) & 3);
+        {
+            const uint4* src = reinterpret_cast<const uint4*>(Tchunk + c0 * S - o);
+            const int n4 = (nload * S + o + 3) / 4;
+#pragma unroll 4
+            for (int e = threadIdx.x; e < n4; e += kWalkThreads) reinterpret_cast<uint4*>(tab)[e] = src[e];
+        }
         __syncthreads();
         if (threadIdx.x == 0) {
             int64_t pos = pos0, batch = sh_batch, k = sh_k;
             uint32_t s = sh_s;
             for (int c = 0; c < nload && batch < W; ++c) {
                 out[k++] = ChunkStart{pos, (int32_t)s, (int32_t)batch};
-                const uint32_t e = tab[c * S + (s - 1)];
+                const uint32_t e = tab[o + c * S + (s - 1)];
                 s = e & 0xffu;
                 batch += e >> 8;
                 pos += kChunk;
@@ -499,11 +506,11 @@ __device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restr
     }
 }
 
-__global__ __launch_bounds__(64) void k_fsm_walk(Job j, int L) {
+__global__ __launch_bounds__(kWalkThreads) void k_fsm_walk(Job j, int L) {
     fsm_walk(j.R, j.first, j.Tchunk, j.P, j.W, L, j.avail, reinterpret_cast<ChunkStart*>(j.pieces), j.info);
 }
 
-__global__ __launch_bounds__(64) void k_fsm_walk_batch(const Job* __restrict__ jobs, int L) {
+__global__ __launch_bounds__(kWalkThreads) void k_fsm_walk_batch(const Job* __restrict__ jobs, int L) {
     const Job j = jobs[blockIdx.x];
     if (j.W <= 0) return;
     fsm_walk(j.R, j.first, j.Tchunk, j.P, j.W, L, j.avail, reinterpret_cast<ChunkStart*>(j.pieces), j.info);
@@ -626,7 +633,7 @@ __global__ void k_pick_batch(const Job* __restrict__ jobs, int n) {
 }
 
 size_t walk_lds_bytes(int L) {
-    return std::max((size_t)64 * (L - 1) * sizeof(uint32_t),
+    return std::max((size_t)(64 * (L - 1) + 4) * sizeof(uint32_t),
                     kSub * sizeof(uint32_t) + (size_t)kSubPerChunk * (L - 1) * sizeof(uint16_t));
 }
 
@@ -661,7 +668,7 @@ extern "C" int ddm_shuffle_window_batch(const ddm_shuffle_job* jobs_dev, int32_t
     hipLaunchKernelGGL(k_fsm_first_batch, dim3(kSubPerChunk - 1, (unsigned)n_jobs), dim3(kFirstThreads), 0, s, jobs,
                        (int)batch_len);
     if (int rc = ddm::launch_status("ddm_shuffle_window_batch/first")) return rc;
-    hipLaunchKernelGGL(k_fsm_walk_batch, dim3((unsigned)n_jobs), dim3(64), walk_lds_bytes(batch_len), s, jobs,
+    hipLaunchKernelGGL(k_fsm_walk_batch, dim3((unsigned)n_jobs), dim3(kWalkThreads), walk_lds_bytes(batch_len), s, jobs,
                        (int)batch_len);
     if (int rc = ddm::launch_status("ddm_shuffle_window_batch/walk")) return rc;
     const int64_t pblocks = std::max<int64_t>(1, std::min<int64_t>(max_pieces, 2048));
@@ -765,7 +772,7 @@ extern "C" int ddm_shuffle_window(const uint32_t* R, const uint32_t* Tpre, const
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
     hipLaunchKernelGGL(k_fsm_first, dim3(kSubPerChunk - 1), dim3(kFirstThreads), 0, s, j, (int)batch_len);
     if (int rc = ddm::launch_status("ddm_shuffle_window/first")) return rc;
-    hipLaunchKernelGGL(k_fsm_walk, dim3(1), dim3(64), walk_lds_bytes(batch_len), s, j, (int)batch_len);
+    hipLaunchKernelGGL(k_fsm_walk, dim3(1), dim3(kWalkThreads), walk_lds_bytes(batch_len), s, j, (int)batch_len);
     if (int rc = ddm::launch_status("ddm_shuffle_window/walk")) return rc;
     const int64_t blocks = std::min<int64_t>(max_pieces, 8192);
     hipLaunchKernelGGL(k_fsm_replay, dim3((unsigned)blocks), dim3(64), 0, s, j, (int)batch_len);

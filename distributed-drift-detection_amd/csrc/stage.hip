@@ -17,7 +17,7 @@
 
 namespace {
 
-constexpr int kStageThreads = 256;
+constexpr int kStageThreads = 1024;
 constexpr int kStageWords = 1024;   // stream words in LDS for one shuffle + the seeds
 
 struct Job {
@@ -89,7 +89,9 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
         __syncthreads();
         int before = total;
         for (int w = 0; w < wv; ++w) before += counts[w];
-        const int round = counts[0] + counts[1] + counts[2] + counts[3];
+        int round = 0;
+#pragma unroll
+        for (int w = 0; w < kStageThreads / 64; ++w) round += counts[w];
         int k = before + incl - c;
         while (bits && k < jb.max_events) {
             const int s = __builtin_ctz(bits);
@@ -149,34 +151,60 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     }
     const int Lj = j == jb.nb - 1 ? jb.last_len : jb.pb;
     for (int w = t; w < kStageWords; w += kStageThreads) words[w] = jb.R[P + w];
+    for (int i = t; i < Lj; i += kStageThreads) perm[i] = (uint8_t)i;
     __syncthreads();
-    if (t == 0) {
+    if (wv == 0) {
+        // legacy permutation(Lj), then randint(2**31 - 1) x n_trees, by the first wave: each
+        // interval's accepted draw is the first lane of a ballot over the next 64 words
         int k = 0;
         bool good = true;
-        for (int i = 0; i < Lj; ++i) perm[i] = (uint8_t)i;
-        for (int i = Lj - 1; i >= 1 && good; --i) {         // legacy permutation(Lj)
+        for (int i = Lj - 1; i >= 1 && good; --i) {
             const uint32_t mask = 0xffffffffu >> __builtin_clz((uint32_t)i);
-            uint32_t v;
-            do {
+            for (;;) {
                 if (k >= kStageWords) { good = false; break; }
-                v = words[k++] & mask;
-            } while (v > (uint32_t)i);
-            if (!good) break;
-            const uint8_t tmp = perm[i];
-            perm[i] = perm[v];
-            perm[v] = tmp;
+                const int w = k + lane;
+                const uint32_t v = w < kStageWords ? (words[w] & mask) : 0xffffffffu;
+                const uint64_t b = __ballot(v <= (uint32_t)i);
+                if (b) {
+                    const int f = __builtin_ctzll(b);
+                    const int jv = __shfl((int)v, f, 64);
+                    k += f + 1;
+                    if (lane == 0) {                                 // the swap, in order
+                        const uint8_t tmp = perm[i];
+                        perm[i] = perm[jv];
+                        perm[jv] = tmp;
+                    }
+                    break;
+                }
+                k += 64;
+            }
         }
-        pos[0] = P + k;
-        for (int tr = 0; tr < jb.n_trees && good; ++tr) {  // randint(2**31 - 1) x n_trees
-            uint32_t v;
-            do {
-                if (k >= kStageWords) { good = false; break; }
-                v = words[k++] & 0x7fffffffu;
-            } while (v > 0x7ffffffeu);
-            if (good) jb.seeds_out[tr] = (int64_t)v;
+        if (lane == 0) pos[0] = P + k;
+        int got = 0;                                                 // seeds drawn so far
+        while (good && got < jb.n_trees) {
+            if (k >= kStageWords) { good = false; break; }
+            const int w = k + lane;
+            const uint32_t v = w < kStageWords ? (words[w] & 0x7fffffffu) : 0xffffffffu;
+            const bool acc = v <= 0x7ffffffeu;
+            const uint64_t b = __ballot(acc);
+            const int before = __popcll(b & ((1ull << lane) - 1ull));
+            if (acc && got + before < jb.n_trees) jb.seeds_out[got + before] = (int64_t)v;
+            const int need = jb.n_trees - got;
+            const int nb = __popcll(b);
+            if (nb >= need) {                                        // the need-th accepted word ends it
+                uint64_t bb = b;
+                for (int q = 1; q < need; ++q) bb &= bb - 1;
+                k += __builtin_ctzll(bb) + 1;
+                got = jb.n_trees;
+            } else {
+                got += nb;
+                k += 64;
+            }
         }
-        pos[1] = P + k;
-        ok = good ? 1 : 0;
+        if (lane == 0) {
+            pos[1] = P + k;
+            ok = good ? 1 : 0;
+        }
     }
     __syncthreads();
     if (!ok) {

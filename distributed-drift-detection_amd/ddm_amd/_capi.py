@@ -42,6 +42,18 @@ class DdmForest(ctypes.Structure):
 assert ctypes.sizeof(DdmState) == 56 and ctypes.sizeof(DdmParams) == 24 and ctypes.sizeof(DdmForest) == 72
 
 _vp, _i32, _i64, _u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
+
+
+class DdmEpoch(ctypes.Structure):
+    """ddm_epoch (include/ddm_amd.h): one BatchRunner epoch for ddm_epoch_launch."""
+    _fields_ = [("stream", _vp), ("ctrl_d", _vp), ("ctrl_h", _vp), ("upload_bytes", _i64), ("download_bytes", _i64),
+                ("shuffle_jobs", _vp), ("n_shuffle", _i32), ("per_batch", _i32), ("max_W", _i64),
+                ("max_pieces", _i64), ("segs_h", _vp), ("segs_d", _vp), ("n_segs", _i32), ("n_stage", _i32),
+                ("err", _vp), ("offsets", _vp), ("ends", _vp), ("n_streams", _i64), ("params", _vp),
+                ("state", _vp), ("first_nz", _vp), ("batch_base", _vp), ("n_batches_total", _i64),
+                ("ev_out", _vp), ("stop", _vp), ("nev", _vp), ("perm_map", _vp), ("long_off", _vp),
+                ("long_end", _vp), ("long_max_rows", _i64), ("long_scratch", _vp), ("stage_jobs", _vp),
+                ("dfit_jobs", _vp), ("n_dfit", _i32), ("max_trees", _i32), ("ev", _vp * 10)]
 _f32, _pi32 = ctypes.c_float, ctypes.POINTER(ctypes.c_int32)
 
 # name -> (restype, argtypes); every symbol include/ddm_amd.h declares.
@@ -68,12 +80,15 @@ SIGNATURES = {
     "ddm_shuffle_generate": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
     "ddm_shuffle_tables": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp]),
     "ddm_shuffle_tables_batch": (ctypes.c_int, [_vp, _i32, _i64, _i32, _vp]),
+    "ddm_epoch_launch": (ctypes.c_int, [_vp]),
+    "ddm_epoch_struct_bytes": (_i64, []),
     "ddm_shuffle_window": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
                                           _vp, _vp, _vp]),
     "ddm_shuffle_pick": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
     "ddm_event_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
     "ddm_event_destroy": (ctypes.c_int, [_vp]),
     "ddm_event_elapsed_ms": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(ctypes.c_float)]),
+    "ddm_event_record": (ctypes.c_int, [_vp, _vp]),
     "ddm_mt_perms": (ctypes.c_int, [_vp, _pi32, _vp, _i64, _vp, _vp]),
     "ddm_mt_randint31": (ctypes.c_int, [_vp, _pi32, _i64, _vp]),
     "ddm_mt_skip": (ctypes.c_int, [_vp, _pi32, _i64]),
@@ -107,6 +122,8 @@ def _load():
         fn.restype, fn.argtypes = res, args
     if lib.ddm_abi_version() != ABI_VERSION:
         raise ImportError(f"libddm_amd.so ABI {lib.ddm_abi_version()} != {ABI_VERSION}")
+    if lib.ddm_epoch_struct_bytes() != ctypes.sizeof(DdmEpoch):
+        raise ImportError("ddm_epoch layout differs from the ctypes binding")
     return lib
 
 

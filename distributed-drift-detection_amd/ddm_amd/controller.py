@@ -21,6 +21,7 @@ shuffle and the refit's 100 tree seeds are read from the stream on the host, the
 forest is refit natively on batch d, and the next window starts at d+1.  Work past d
 is discarded, so total predict work stays within ~2x the rows.
 """
+import ctypes
 import os
 import time
 
@@ -29,6 +30,7 @@ import pandas as pd
 import torch
 
 from . import dfit, kernels
+from ._capi import DdmEpoch, check, lib
 from .forest import upload_forests
 from .params import OUTPUT_COLUMNS, DDMSettings, infer_x_features
 from .rng import MTStream
@@ -185,6 +187,7 @@ class _Part:
 
 
 _HOST_TRACE = os.environ.get("DDM_HOST_TRACE", "") not in ("", "0")
+_FRESH = kernels.fresh_states(1)[0]
 
 
 class BatchRunner:
@@ -279,6 +282,10 @@ class BatchRunner:
         self.ctrl_bytes = o
         self.ctrl_h = torch.zeros(self.ctrl_bytes, dtype=torch.uint8, pin_memory=True)
         self._views = {}
+        a = self.stage_off["info"]
+        self._info_all = np.lib.stride_tricks.as_strided(      # every partition's staging info
+            self.ctrl_h.numpy()[a:a + self.stage_stride["info"] * n].view(np.int64), shape=(n, 7),
+            strides=(self.stage_stride["info"], 8), writeable=False)
         self.ctrl_d = torch.zeros(self.ctrl_bytes, dtype=torch.uint8, device=dev)
         c = self.ctrl_h.numpy()
         self.first_h = c[self.o_first:self.o_first + 8 * n].view(np.int64)
@@ -315,8 +322,7 @@ class BatchRunner:
                 self.dfit_bufs.append(b)
                 self.dfit_rows.append(b.record(self._sptr("x", i), self._sptr("y", i), self._sptr("seeds", i),
                                                self._sptr("dfit", i), gate=info, gate2=info + 48))
-        self.t_fit = ((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                      if timing and refit == "device" else None)
+        self.t_fit = kernels.LaunchTimer() if timing and refit == "device" else None
         # the partitions' MT19937 streams are generated and tabulated on a side stream, in
         # pieces, while the epochs run (GpuShuffle.wait_for orders the consumers)
         self.gen_stream = gen_stream or torch.cuda.Stream(dev)
@@ -333,6 +339,7 @@ class BatchRunner:
             self.shuffles.append(GpuShuffle(dev, pb, cap, mw, self.stream, self.gen_stream, self.tab_stream))
         self.stats = RunStats()
         self._gen_rest = None
+        self._E = self._epoch_desc()
         self.trace = [] if _HOST_TRACE else None     # (label, seconds since run start)
 
     def _mark(self, label):
@@ -572,6 +579,8 @@ class BatchRunner:
                 sh.E.data_ptr()
             q["first"], q["pick_out"] = sh.first.data_ptr(), self._dptr(self.o_pick, i, 8)
         self._tmpl = {"seg": seg, "stage": stg, "job": job, "forest": [None] * n, "ptrs": [None] * n,
+                      "forest_view": seg[["nodes", "roots", "leaf_value", "classes", "n_trees", "n_classes", "n_nodes",
+                                          "pure", "cforest", "cf_slots", "cf_vote_regs", "cf_leaves", "cf_tab_words"]],
                       "dfit": np.array(self.dfit_rows, dtype=dfit.DFIT_DTYPE) if self.dfit_rows else None,
                       "stop": np.array([self._dptr(self.o_stop, i, 4) for i in range(n)], dtype=np.uint64)}
         return self._tmpl
@@ -591,14 +600,13 @@ class BatchRunner:
         """ddm_predict_segment records (forest predict) of this epoch."""
         t = self._templates()
         seg = t["seg"]
+        fv = t["forest_view"]
         for ps in live:
             if t["forest"][ps.i] is not ps.forest:          # a new forest: its descriptor fields
                 t["forest"][ps.i] = ps.forest
-                d, r = ps.forest.desc, seg[ps.i]
-                r["nodes"], r["roots"], r["leaf_value"], r["classes"] = d.nodes, d.roots, d.leaf_value or 0, d.classes
-                r["n_trees"], r["n_classes"], r["n_nodes"], r["pure"] = d.n_trees, d.n_classes, d.n_nodes, d.pure
-                r["cforest"], r["cf_slots"], r["cf_vote_regs"] = d.cforest or 0, d.cf_slots, d.cf_vote_regs
-                r["cf_leaves"], r["cf_tab_words"] = d.cf_leaves, d.cf_tab_words
+                d = ps.forest.desc
+                fv[ps.i] = (d.nodes, d.roots, d.leaf_value or 0, d.classes, d.n_trees, d.n_classes, d.n_nodes, d.pure,
+                            d.cforest or 0, d.cf_slots, d.cf_vote_regs, d.cf_leaves, d.cf_tab_words)
         idx = [ps.i for ps in live]
         rec = seg[idx]
         rec["pos_begin"] = [ps.rng_rows[0] for ps in live]
@@ -791,6 +799,31 @@ class BatchRunner:
             self.tab_stream.synchronize()
             self._mark("side streams drained")
 
+    def _epoch_desc(self):
+        """The ddm_epoch record of this runner (ddm_epoch_launch): the buffers never move, so
+        every epoch only sets the counts and sizes."""
+        E = DdmEpoch()
+        base = self.ctrl_d.data_ptr()
+        E.stream = self.stream.cuda_stream
+        E.ctrl_d, E.ctrl_h = base, self.ctrl_h.data_ptr()
+        E.upload_bytes, E.download_bytes = self.o_stage, self.ctrl_bytes
+        E.shuffle_jobs, E.per_batch = self.jobs.d.data_ptr(), self.s.per_batch
+        E.segs_h, E.segs_d = self.segs.h.data_ptr(), self.segs.d.data_ptr()
+        E.err, E.offsets, E.ends = self.err_all.data_ptr(), base + self.o_off, base + self.o_end
+        E.n_streams = len(self.parts)
+        E.params = ctypes.addressof(self.params)
+        E.state, E.first_nz, E.batch_base = base + self.o_state, base + self.o_first, base + self.o_bbase
+        E.n_batches_total, E.ev_out = self.ev_total, self.ev_d.data_ptr()
+        E.stop, E.nev, E.perm_map = base + self.o_stop, base + self.o_nev, self.perm_all.data_ptr()
+        E.long_off, E.long_end, E.long_scratch = base + self.o_loff, base + self.o_lend, self.long_scratch.data_ptr()
+        E.stage_jobs, E.dfit_jobs = self.stage_jobs.d.data_ptr(), self.dfit_jobs.d.data_ptr()
+        E.max_trees = self.s.n_estimators
+        if self.timing:
+            for k, t in enumerate((self.t_shuf, self.t_pred, self.t_scan, self.t_long, self.t_fit)):
+                if t is not None:
+                    E.ev[2 * k], E.ev[2 * k + 1] = t.ev[0].value, t.ev[1].value
+        return E
+
     def _enqueue_rest(self):
         """The partitions' whole streams, in growing pieces on the side streams (the first
         piece is enqueued by run())."""
@@ -867,7 +900,7 @@ class BatchRunner:
             ps.rng_rows = (p0, p1)
             self.off_h[ps.i], self.end_h[ps.i] = p0, p1
             # a refitting partition starts a fresh DDM (:136-139), whenever its fit runs
-            self.state_h[ps.i] = kernels.fresh_states(1)[0] if ps.retrain else ps.state[0]
+            self.state_h[ps.i] = _FRESH if ps.retrain else ps.state[0]
             if not ps.retrain and p1 - p0 >= LONG_SCAN_MIN_ROWS and carried_exact(ps.state[0]):
                 self.loff_h[ps.i], self.lend_h[ps.i] = p0, p1
                 self.end_h[ps.i] = p0            # nothing for the one-lane scan
@@ -886,6 +919,23 @@ class BatchRunner:
         if self.dfit_rows:
             self.dfit_jobs.rec[:len(live)] = self._templates()["dfit"][[ps.i for ps in live]]
         self.first_h[:] = -1                    # the predict kernels' first-error slots
+        if not late_fit and not shuffled:
+            # the whole epoch in one native call (csrc/epoch.hip)
+            E = self._E
+            E.n_shuffle = len(shuf)
+            E.max_W, E.max_pieces = (max_W, max_pieces) if shuf else (0, 0)
+            E.n_segs = E.n_stage = len(live)
+            E.long_max_rows = long_rows
+            E.n_dfit = len(live) if self.dfit_rows else 0
+            if self.predict_log is not None:
+                self.predict_log.append((self.segs.rec[:len(live)].copy(), len(live), pb))
+            self._mark("tables + upload")
+            check(lib.ddm_epoch_launch(ctypes.byref(E)), "ddm_epoch_launch")
+            self._mark("launched")
+            stream.synchronize()
+            self._mark("synchronized")
+            self._epoch_after(live, st, pb, shuf, long_rows, t1, host)
+            return
         with torch.cuda.stream(stream):
             self.ctrl_d[:self.o_stage].copy_(self.ctrl_h[:self.o_stage], non_blocking=True)
         if shuf and not shuffled:
@@ -916,15 +966,21 @@ class BatchRunner:
         if self.dfit_rows:
             # the refits of the partitions that changed, on the rows the staging gathered
             if self.t_fit is not None:
-                self.t_fit[0].record(stream)
+                check(lib.ddm_event_record(self.t_fit.ev[0], ctypes.c_void_p(stream.cuda_stream)), "event record")
             dfit.fit_device(self.dfit_jobs.d, len(live), self.s.n_estimators, stream)
             if self.t_fit is not None:
-                self.t_fit[1].record(stream)
+                check(lib.ddm_event_record(self.t_fit.ev[1], ctypes.c_void_p(stream.cuda_stream)), "event record")
         with torch.cuda.stream(stream):
             self.ctrl_h.copy_(self.ctrl_d, non_blocking=True)
         self._mark("launched")
         stream.synchronize()
         self._mark("synchronized")
+        self._epoch_after(live, st, pb, shuf, long_rows, t1, host)
+
+    def _epoch_after(self, live, st, pb, shuf, long_rows, t1, host):
+        """Everything after an epoch's read-back: timings, events, RNG positions, the next
+        windows."""
+        s, stream = self.s, self.stream
         if self.timing:
             st.predict_ms += self.t_pred.elapsed_ms()
             st.scan_ms += self.t_scan.elapsed_ms()
@@ -932,20 +988,22 @@ class BatchRunner:
                 st.scan_ms += self.t_long.elapsed_ms()
             if shuf:
                 st.shuffle_ms += self.t_shuf.elapsed_ms()
-            if self.t_fit is not None:
-                st.dfit_ms += self.t_fit[0].elapsed_time(self.t_fit[1])
+            if self.t_fit is not None and self.dfit_rows:
+                st.dfit_ms += self.t_fit.elapsed_ms()
+        # the control block as Python ints, one conversion per array
+        stops, nevs, picks = self.stop_h.tolist(), self.nev_h.tolist(), self.pick_h.tolist()
+        infos = self._info_all.tolist()
         # read-backs beyond the staging (more events than it holds): rare
         pending = False
         for ps in live:
-            stop, nev = int(self.stop_h[ps.i]), int(self.nev_h[ps.i])
+            stop, nev = stops[ps.i], nevs[ps.i]
             ps_last = ps.j + stop if stop >= 0 else ps.b_end - 1
             p0, p1 = ps.rng_rows
             st.predicted_rows += p1 - p0
             if self.timing:
                 st.predict_bytes += (p1 - p0) * (4 * ps.forest.features_read + 6)
                 st.scan_rows += min(p1, ps.base + (ps_last + 1) * pb) - p0
-            info = self._sview("info", ps.i, np.int64, 7)
-            if nev and info[2]:
+            if nev and infos[ps.i][2]:
                 k, e0 = ps_last - ps.j + 1, ps.ev_base
                 with torch.cuda.stream(stream):
                     self.ev_h[e0:e0 + k].copy_(self.ev_d[e0:e0 + k], non_blocking=True)
@@ -956,9 +1014,9 @@ class BatchRunner:
         st.gpu_s += t2 - t1
         st.epochs += 1
         for ps in live:
-            stop, nev = int(self.stop_h[ps.i]), int(self.nev_h[ps.i])
+            stop, nev = stops[ps.i], nevs[ps.i]
             last = ps.j + stop if stop >= 0 else ps.b_end - 1
-            info = self._sview("info", ps.i, np.int64, 7)
+            info = infos[ps.i]
             if nev and info[2]:                     # overflowed the staging: full rows
                 k, e0 = last - ps.j + 1, ps.ev_base
                 ev = self.ev_h[e0:e0 + k].numpy()
@@ -967,12 +1025,13 @@ class BatchRunner:
                     b = ps.j + hit
                     ps.ev.append((b - 1, c, b * pb + ev[hit, c].astype(np.int64)))
             elif nev:
-                rec = self._sview("ev", ps.i, np.int32, 3 * self.max_events)[:3 * int(info[1])].reshape(-1, 3)
-                b = ps.j + rec[:, 0].astype(np.int64)
-                for c in range(2):
-                    hit = rec[:, 1 + c] >= 0
-                    ps.ev.append((b[hit] - 1, c, b[hit] * pb + rec[hit, 1 + c].astype(np.int64)))
-            picked = int(self.pick_h[ps.i]) if ps.Wg else -1
+                rec = self._sview("ev", ps.i, np.int32, 3 * self.max_events)[:3 * info[1]].tolist()
+                for q in range(0, len(rec), 3):
+                    b = ps.j + rec[q]
+                    for c in range(2):
+                        if rec[q + 1 + c] >= 0:
+                            ps.ev.append((b - 1, c, b * pb + rec[q + 1 + c]))
+            picked = picks[ps.i] if ps.Wg else -1
             # RNG position right after the last consumed batch shuffle
             if stop >= 0:
                 d = ps.j + stop
@@ -982,21 +1041,21 @@ class BatchRunner:
                     ps.P = ps.P_tail_after
                 else:
                     ps.P = picked + 1
-                if int(info[0]) != ps.P or int(info[3]) != d:
-                    raise RuntimeError(f"partition {ps.i}: staging disagrees (P {int(info[0])} vs {ps.P}, "
-                                       f"batch {int(info[3])} vs {d})")
+                if info[0] != ps.P or info[3] != d:
+                    raise RuntimeError(f"partition {ps.i}: staging disagrees (P {info[0]} vs {ps.P}, "
+                                       f"batch {info[3]} vs {d})")
                 L = ps.blen(d)
-                drawn = int(info[6]) == 1           # batch d+1's shuffle and the seeds, on the device
+                drawn = info[6] == 1                # batch d+1's shuffle and the seeds, on the device
                 res = self._sview("dfit", ps.i, np.int64, dfit.RESULT_WORDS) if self.dfit_rows else None
                 if drawn and res is not None and int(res[0]) == 0:
-                    ps.staged = ("device", int(info[4]), int(info[5]), res.copy())
+                    ps.staged = ("device", info[4], info[5], res.copy())
                 else:
                     F_i = ps_feats(self.parts[ps.i])
                     ps.staged = (self._sview("x", ps.i, np.float32, L * F_i).reshape(L, -1).copy(),
                                  self._sview("y", ps.i, np.int32, L).astype(np.int64),
                                  None if drawn else self._sview("w", ps.i, np.uint32, self.n_words).copy(),
                                  self._sview("seeds", ps.i, np.int64, self.s.n_estimators).copy() if drawn else None,
-                                 int(info[4]), int(info[5]))
+                                 info[4], info[5])
                 ps.retrain = True
                 # adaptive speculation: the next concept likely lasts about as long as this
                 # one, so the next window covers it with 1/8 to spare (one epoch per drift

@@ -146,7 +146,7 @@ class GpuShuffle:
         cap = (cap + CHUNK - 1) // CHUNK * CHUNK
         R = torch.empty(cap, dtype=torch.int32, device=self.device)
         Tp = torch.empty(cap // SUB * self.S, dtype=torch.int32, device=self.device)   # prefix tables [chunk][64][S]
-        Tc = torch.empty(cap // CHUNK * self.S, dtype=torch.int32, device=self.device)
+        Tc = torch.empty(cap // CHUNK * self.S + 4, dtype=torch.int32, device=self.device)   # + 16-byte over-read
         if getattr(self, "R", None) is not None and self.gen:
             torch.cuda.synchronize(self.device)          # rare: growth past the initial estimate
             R[:self.gen].copy_(self.R[:self.gen])

@@ -275,6 +275,7 @@ int ddm_scan_long(const uint8_t* err, const int64_t* stream_off, const int64_t* 
  * ElapsedTime; elapsed needs both events completed, e.g. after a stream sync). */
 int ddm_event_create(ddm_event_t* ev);
 int ddm_event_destroy(ddm_event_t ev);
+int ddm_event_record(ddm_event_t ev, ddm_stream_t stream);
 int ddm_event_elapsed_ms(ddm_event_t begin, ddm_event_t end, float* ms);
 
 /* ---- host-side MT19937 (numpy legacy RandomState layout: key[624], pos) ---------- */
@@ -478,6 +479,29 @@ int64_t ddm_rf_device_scratch_bytes(int32_t L, int32_t F, int32_t n_trees, int32
 /* Fits every job (device table of n_jobs records) on `stream`; max_trees bounds the
  * jobs' n_trees (grid size).  Asynchronous: results land in each job's result[]. */
 int ddm_rf_fit_device(const ddm_dfit_job* jobs_dev, int32_t n_jobs, int32_t max_trees, ddm_stream_t stream);
+
+/* ---- epoch executor (csrc/epoch.hip) -------------------------------------------- */
+/* One call enqueues a BatchRunner epoch on `stream`: ctrl_d[0, upload_bytes) <- ctrl_h
+ * (pinned), ddm_shuffle_window_batch (n_shuffle > 0), ddm_forest_predict_batch (n_segs >
+ * 0), ddm_scan_streams (mode 0), ddm_scan_long (long_max_rows > 0), ddm_shuffle_pick_batch,
+ * ddm_epoch_stage (n_stage > 0), ddm_rf_fit_device (n_dfit > 0), then ctrl_h[0,
+ * download_bytes) <- ctrl_d.  ev (may hold NULLs): begin/end pairs around the shuffles,
+ * predict, scan, long scan and refits.  Replaces the per-launch calls the controller
+ * makes for DDM_Process.py:187-210 (one batch loop iteration per partition and batch). */
+typedef struct ddm_epoch {
+    ddm_stream_t stream;
+    void* ctrl_d; void* ctrl_h; int64_t upload_bytes, download_bytes;
+    const ddm_shuffle_job* shuffle_jobs; int32_t n_shuffle, per_batch; int64_t max_W, max_pieces;
+    const ddm_predict_segment* segs_h; ddm_predict_segment* segs_d; int32_t n_segs, n_stage;
+    const uint8_t* err; const int64_t* offsets; const int64_t* ends; int64_t n_streams;
+    const ddm_params* params; ddm_state* state; const uint64_t* first_nz; const int64_t* batch_base;
+    int64_t n_batches_total; int32_t* ev_out; int32_t* stop; int64_t* nev; const uint8_t* perm_map;
+    const int64_t* long_off; const int64_t* long_end; int64_t long_max_rows; void* long_scratch;
+    const ddm_stage_job* stage_jobs; const ddm_dfit_job* dfit_jobs; int32_t n_dfit, max_trees;
+    ddm_event_t ev[10];
+} ddm_epoch;
+int ddm_epoch_launch(const ddm_epoch* e);
+int64_t ddm_epoch_struct_bytes(void);   /* sizeof(ddm_epoch), for binding checks */
 
 /* ---- synthetic inputs (benchmark configs) ------------------------- */
 
