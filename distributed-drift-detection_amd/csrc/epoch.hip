@@ -3,8 +3,10 @@
 //   control-block upload -> window shuffles -> forest predict -> DDM scan (one lane per
 //   stream, plus ddm_scan_long for long carried windows) -> RNG pick -> staging ->
 //   device refits -> control-block read-back.
-// Nothing is decided here (the host plans every window from the read-back); the point is
-// to replace ~10 separate binding calls and stream switches per epoch by one.
+// Nothing is decided here; the point is to replace ~10 separate binding calls and stream
+// switches per epoch by one.  When the staging planned the next windows (next_jobs), their
+// shuffles run on a side stream beside the device refits, so the next epoch can start
+// with its forest predict.
 #include "common.h"
 
 extern "C" int ddm_epoch_launch(const ddm_epoch* e) {
@@ -34,10 +36,22 @@ extern "C" int ddm_epoch_launch(const ddm_epoch* e) {
                                    e->state, e->batch_base, e->ev_out, e->stop, e->nev, 0, e->perm_map,
                                    e->long_scratch, e->stream, e->ev[6], e->ev[7]))
             return rc;
-    if (e->n_shuffle > 0)
-        if (int rc = ddm_shuffle_pick_batch(e->shuffle_jobs, e->n_shuffle, e->stream)) return rc;
+    if (e->n_pick > 0)
+        if (int rc = ddm_shuffle_pick_batch(e->pick_jobs, e->n_pick, e->stream)) return rc;
     if (e->n_stage > 0)
         if (int rc = ddm_epoch_stage(e->stage_jobs, e->n_stage, e->stream)) return rc;
+    const bool fork = e->n_next > 0 && e->next_jobs && e->side_stream && e->fork_ev && e->join_ev;
+    if (fork) {
+        // the next windows' shuffles (planned by the staging) beside the refits
+        hipStream_t side = ddm::as_hip(e->side_stream);
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(e->fork_ev), s), "fork")) return rc;
+        if (int rc = ddm::hip_status(hipStreamWaitEvent(side, reinterpret_cast<hipEvent_t>(e->fork_ev), 0), "fork"))
+            return rc;
+        if (int rc = ddm_shuffle_window_batch(e->next_jobs, e->n_next, e->next_max_W, e->next_max_pieces, e->per_batch,
+                                              e->side_stream, nullptr, nullptr))
+            return rc;
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(e->join_ev), side), "join")) return rc;
+    }
     if (e->n_dfit > 0) {
         if (e->ev[8])
             if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(e->ev[8]), s), "event record"))
@@ -47,6 +61,9 @@ extern "C" int ddm_epoch_launch(const ddm_epoch* e) {
             if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(e->ev[9]), s), "event record"))
                 return rc;
     }
+    if (fork)
+        if (int rc = ddm::hip_status(hipStreamWaitEvent(s, reinterpret_cast<hipEvent_t>(e->join_ev), 0), "join"))
+            return rc;
     if (e->download_bytes)
         if (int rc = ddm::hip_status(hipMemcpyAsync(e->ctrl_h, e->ctrl_d, (size_t)e->download_bytes,
                                                     hipMemcpyDeviceToHost, s), "ddm_epoch_launch/read-back"))

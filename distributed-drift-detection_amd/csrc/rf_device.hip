@@ -188,7 +188,9 @@ __device__ __forceinline__ int wave_scan_i(int v, int lane) {
 }
 
 // ---- k_dfit_prep --------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_dfit_prep(const Job* __restrict__ jobs) {
+constexpr int kPrepThreads = 1024;         // presort tasks: every (feature, row) pair
+
+__global__ __launch_bounds__(kPrepThreads) void k_dfit_prep(const Job* __restrict__ jobs) {
     const Job jb = jobs[blockIdx.x];
     const int t = threadIdx.x;
     __shared__ int32_t s_y[kMaxL];
@@ -216,7 +218,7 @@ __global__ __launch_bounds__(256) void k_dfit_prep(const Job* __restrict__ jobs)
     uint8_t* yidx = jb.scratch + lo.yidx;
     uint8_t* order = jb.scratch + lo.order;
     if (t < L) s_y[t] = jb.y[t];
-    for (int e = t; e < L * F; e += 256)
+    for (int e = t; e < L * F; e += kPrepThreads)
         if (jb.X[e] != jb.X[e]) s_nan = 1;
     __syncthreads();
     // classes_ = np.unique(y): first occurrences ranked by value
@@ -249,12 +251,12 @@ __global__ __launch_bounds__(256) void k_dfit_prep(const Job* __restrict__ jobs)
     for (int f0 = 0; f0 < F; f0 += G) {
         const int g = min(G, F - f0);
         __syncthreads();
-        for (int e = t; e < L * g; e += 256) {
+        for (int e = t; e < L * g; e += kPrepThreads) {
             const int r = e / g, k = e % g;
             s_tile[k * L + r] = jb.X[(int64_t)r * F + f0 + k];
         }
         __syncthreads();
-        for (int e = t; e < L * g; e += 256) {
+        for (int e = t; e < L * g; e += kPrepThreads) {
             const int k = e / L, i = e % L;
             const float* col = s_tile + k * L;
             const float x = col[i];
@@ -1044,7 +1046,7 @@ extern "C" int ddm_rf_fit_device(const ddm_dfit_job* jobs_dev, int32_t n_jobs, i
     if (n_jobs == 0) return 0;
     hipStream_t s = ddm::as_hip(stream);
     const Job* jobs = reinterpret_cast<const Job*>(jobs_dev);
-    hipLaunchKernelGGL(k_dfit_prep, dim3((unsigned)n_jobs), dim3(256), 0, s, jobs);
+    hipLaunchKernelGGL(k_dfit_prep, dim3((unsigned)n_jobs), dim3(kPrepThreads), 0, s, jobs);
     if (int rc = ddm::launch_status("ddm_rf_fit_device/prep")) return rc;
     hipLaunchKernelGGL(k_dfit_trees, dim3((unsigned)ddm::ceil_div(max_trees, kWaves), (unsigned)n_jobs),
                        dim3(64 * kWaves), 0, s, jobs);

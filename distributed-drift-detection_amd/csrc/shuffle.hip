@@ -424,6 +424,10 @@ __device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restr
                          const uint32_t* __restrict__ Tchunk, int64_t P, int64_t W, int L, int64_t avail,
                          ChunkStart* __restrict__ out, int64_t* __restrict__ info) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab[];   // [64][S] chunk rows; phase A: draws + first-chunk rows
+#ifdef DDM_WALK_PROFILE
+    const uint64_t t_start = wall_clock64();
+    uint64_t t_p0 = 0, t_p1 = 0, t_ld = 0;
+#endif
     __shared__ int64_t sh_pos, sh_batch, sh_k;
     __shared__ uint32_t sh_s;
     const int S = L - 1;
@@ -435,59 +439,94 @@ __device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restr
     uint32_t* a_draws = tab;
     uint16_t* a_first = reinterpret_cast<uint16_t*>(tab + kSub);
     for (int k = threadIdx.x; k < n_draws; k += kWalkThreads) a_draws[k] = R[P + k];
-    for (int e = threadIdx.x; e < n_subrows * S; e += kWalkThreads) a_first[e] = first[q0 * S + e];
+    const int of = (q0 * S) & 7;                      // 16-byte loads from the aligned element before
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(first + q0 * S - of);
+        const int n8 = n_subrows > 0 ? (n_subrows * S + of + 7) / 8 : 0;
+        for (int e = threadIdx.x; e < n8; e += kWalkThreads) reinterpret_cast<uint4*>(a_first)[e] = src[e];
+    }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int64_t pos = P, batch = 0, k = 0;
+    if (threadIdx.x < 64) {
+        // draw by draw to the sub-chunk boundary, by the first wave: the next accepted draw
+        // of the current interval is the first lane of a ballot over the next 64 draws
+        const int lane = threadIdx.x;
+        int64_t pos = P, batch = 0;
         uint32_t s = (uint32_t)S;
-        out[k++] = ChunkStart{pos, (int32_t)s, 0};
-        while (batch < W && pos < sub_end) {
-            const uint32_t v = a_draws[pos - P];
-            ++pos;
-            if ((v & imask(s)) <= s) {
+        for (int64_t base = P; batch < W && base < sub_end; base += 64) {
+            // this lane's draw of the 64-draw window stays in a register; every accepted
+            // draw is one ballot
+            const bool in = base + lane < sub_end;
+            const uint32_t v = in ? a_draws[base - P + lane] : 0u;
+            int from = 0;
+            pos = min(sub_end, base + 64);
+            for (;;) {
+                const uint64_t acc = __ballot(in && lane >= from && (v & imask(s)) <= s);
+                if (!acc) break;
+                const int f = __builtin_ctzll(acc);
+                from = f + 1;
                 if (s == 1) {
                     s = (uint32_t)S;
-                    ++batch;
+                    if (++batch >= W) {
+                        pos = base + f + 1;
+                        break;
+                    }
                 } else {
                     --s;
                 }
             }
         }
-        while (batch < W && pos % kChunk != 0 && pos + kSub <= avail) {
-            out[k++] = ChunkStart{pos, (int32_t)s, (int32_t)batch};
-            const uint32_t e = a_first[((pos - sub_end) / kSub) * S + (s - 1)];
-            s = e & 0xffu;
-            batch += e >> 8;
-            pos += kSub;
+#ifdef DDM_WALK_PROFILE
+        t_p0 = wall_clock64();
+#endif
+        if (lane == 0) {                      // the rest of the walk is serial
+            int64_t k = 0;
+            out[k++] = ChunkStart{P, (int32_t)S, 0};
+            while (batch < W && pos % kChunk != 0 && pos + kSub <= avail) {
+                out[k++] = ChunkStart{pos, (int32_t)s, (int32_t)batch};
+                const uint32_t e = a_first[of + ((pos - sub_end) / kSub) * S + (s - 1)];
+                s = e & 0xffu;
+                batch += e >> 8;
+                pos += kSub;
+            }
+            sh_pos = pos;
+            sh_batch = batch;
+            sh_k = k;
+            sh_s = s;
         }
-        sh_pos = pos;
-        sh_batch = batch;
-        sh_k = k;
-        sh_s = s;
+#ifdef DDM_WALK_PROFILE
+        t_p1 = wall_clock64();
+#endif
     }
     __syncthreads();
-    for (;;) {
-        const int64_t pos0 = sh_pos;
-        if (sh_batch >= W || pos0 + kChunk > avail) break;
-        const int64_t c0 = pos0 / kChunk;
-        const int nload = (int)min((int64_t)64, (avail - pos0) / kChunk);
-        __syncthreads();
-        // the rows of 64 chunks (64*S words) with 16-byte loads from the aligned word at or
-        // before the first one (Tchunk is 16-byte aligned and padded by 4 words)
+    // chunk by chunk: the rows of up to 64 chunks per LDS buffer; waves 1-3 load the next
+    // buffer while lane 0 walks the current one
+    const int stride = (64 * S + 4 + 3) & ~3;
+    auto load_rows = [&](uint32_t* buf, int64_t c0, int n, int t0) {
+        // 16-byte loads from the aligned word at or before row c0 (Tchunk is 16-byte aligned
+        // and padded by 4 words)
         const int o = (int)((c0 * S) & 3);
-        {
-            const uint4* src = reinterpret_cast<const uint4*>(Tchunk + c0 * S - o);
-            const int n4 = (nload * S + o + 3) / 4;
-#pragma unroll 4
-            for (int e = threadIdx.x; e < n4; e += kWalkThreads) reinterpret_cast<uint4*>(tab)[e] = src[e];
-        }
-        __syncthreads();
+        const uint4* src = reinterpret_cast<const uint4*>(Tchunk + c0 * S - o);
+        const int n4 = (n * S + o + 3) / 4;
+        for (int e = (int)threadIdx.x - t0; e < n4; e += kWalkThreads - t0) reinterpret_cast<uint4*>(buf)[e] = src[e];
+    };
+    const int64_t covered = avail / kChunk;
+    int64_t c_load = sh_pos / kChunk;
+    int nload = (sh_batch < W && sh_pos % kChunk == 0) ? (int)max((int64_t)0, min((int64_t)64, covered - c_load)) : 0;
+    if (nload > 0) load_rows(tab, c_load, nload, 0);
+    __syncthreads();
+    int cur = 0;
+    while (nload > 0) {
+        const int64_t c_next = c_load + nload;
+        const int nnext = (int)max((int64_t)0, min((int64_t)64, covered - c_next));
+        uint32_t* now = tab + cur * stride;
+        if (threadIdx.x >= 64 && nnext > 0) load_rows(tab + (cur ^ 1) * stride, c_next, nnext, 64);
         if (threadIdx.x == 0) {
-            int64_t pos = pos0, batch = sh_batch, k = sh_k;
+            const int o = (int)((c_load * S) & 3);
+            int64_t pos = sh_pos, batch = sh_batch, k = sh_k;
             uint32_t s = sh_s;
             for (int c = 0; c < nload && batch < W; ++c) {
                 out[k++] = ChunkStart{pos, (int32_t)s, (int32_t)batch};
-                const uint32_t e = tab[o + c * S + (s - 1)];
+                const uint32_t e = now[o + c * S + (s - 1)];
                 s = e & 0xffu;
                 batch += e >> 8;
                 pos += kChunk;
@@ -498,11 +537,22 @@ __device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restr
             sh_s = s;
         }
         __syncthreads();
+        if (sh_batch >= W) break;
+        c_load = c_next;
+        nload = nnext;
+        cur ^= 1;
     }
     if (threadIdx.x == 0) {
         info[0] = sh_k;
         info[1] = sh_pos;
         info[2] = sh_batch;
+#ifdef DDM_WALK_PROFILE
+        const uint64_t t_end = wall_clock64();
+        info[3] = (int64_t)(t_p0 - t_start);
+        info[4] = (int64_t)(t_p1 - t_start);
+        info[5] = (int64_t)(t_end - t_start);
+        info[6] = (int64_t)t_ld;
+#endif
     }
 }
 
@@ -523,30 +573,50 @@ __global__ __launch_bounds__(kWalkThreads) void k_fsm_walk_batch(const Job* __re
 // of batch b < W record J[b*L + s] = v & mask(s) and, when s == 1, E[b] = draw index.
 constexpr int kReplayBatch = 16;
 
+__device__ __forceinline__ void replay_step(uint32_t v, int64_t q, uint32_t& s, int64_t& b, uint32_t S, int L,
+                                            uint8_t* __restrict__ J, int64_t* __restrict__ E) {
+    const uint32_t m = v & imask(s);
+    if (m <= s) {
+        J[b * L + s] = (uint8_t)m;
+        if (s == 1) {
+            E[b] = q;
+            s = S;
+            ++b;
+        } else {
+            --s;
+        }
+    }
+}
+
 __device__ __forceinline__ void replay_range(const uint32_t* __restrict__ R, int64_t beg, int64_t fin, uint32_t s,
                                              int64_t b, int64_t W, int L, uint8_t* __restrict__ J,
                                              int64_t* __restrict__ E) {
     const uint32_t S = (uint32_t)(L - 1);
+    if (fin - beg == kSub && (beg & 3) == 0) {
+        // a whole sub-chunk: 64 words at a time in flight (sixteen 16-byte loads)
+        const uint4* src = reinterpret_cast<const uint4*>(R + beg);
+        for (int h = 0; h < kSub / 64 && b < W; ++h) {
+            uint4 v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = src[16 * h + k];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int64_t q = beg + 64 * h + 4 * k;
+                if (b < W) replay_step(v[k].x, q, s, b, S, L, J, E);
+                if (b < W) replay_step(v[k].y, q + 1, s, b, S, L, J, E);
+                if (b < W) replay_step(v[k].z, q + 2, s, b, S, L, J, E);
+                if (b < W) replay_step(v[k].w, q + 3, s, b, S, L, J, E);
+            }
+        }
+        return;
+    }
     for (int64_t q0 = beg; q0 < fin && b < W; q0 += kReplayBatch) {
         uint32_t v[kReplayBatch];
 #pragma unroll
         for (int k = 0; k < kReplayBatch; ++k) v[k] = R[min(q0 + k, fin - 1)];
 #pragma unroll
-        for (int k = 0; k < kReplayBatch; ++k) {
-            if (q0 + k < fin && b < W) {
-                const uint32_t m = v[k] & imask(s);
-                if (m <= s) {
-                    J[b * L + s] = (uint8_t)m;
-                    if (s == 1) {
-                        E[b] = q0 + k;
-                        s = S;
-                        ++b;
-                    } else {
-                        --s;
-                    }
-                }
-            }
-        }
+        for (int k = 0; k < kReplayBatch; ++k)
+            if (q0 + k < fin && b < W) replay_step(v[k], q0 + k, s, b, S, L, J, E);
     }
 }
 
@@ -633,7 +703,7 @@ __global__ void k_pick_batch(const Job* __restrict__ jobs, int n) {
 }
 
 size_t walk_lds_bytes(int L) {
-    return std::max((size_t)(64 * (L - 1) + 4) * sizeof(uint32_t),
+    return std::max((size_t)2 * ((64 * (L - 1) + 4 + 3) & ~3) * sizeof(uint32_t),
                     kSub * sizeof(uint32_t) + (size_t)kSubPerChunk * (L - 1) * sizeof(uint16_t));
 }
 

@@ -40,8 +40,61 @@ struct Job {
     uint8_t* perm_w;
     int64_t* seeds_out;
     int32_t n_trees, pad;
+    int64_t p_now, win, max_win, seg_start, n_full, min_win, next_avail, dpb_x1024;
+    int64_t* plan_out;
+    ddm_shuffle_job* next_job;
 };
 static_assert(sizeof(Job) == sizeof(ddm_stage_job), "Job must mirror ddm_stage_job");
+
+// The next window as BatchRunner._epoch_after + _epoch would set it (controller.py), for
+// the common cases only: a change whose batch d+1 shuffle and seeds were drawn here (the
+// refit goes through, on the device or the host, from the draw after the seeds), or no
+// change at all; windows reaching a short last batch stay with the host.  Written by one
+// thread; W = 0 when not planned.
+__device__ void plan_next(const Job& jb, int32_t stop, bool drawn, int64_t p_seeds) {
+    int64_t jn, Pn, g0n, winn;
+    bool ok = true;
+    if (stop >= 0) {
+        const int64_t d = jb.j + stop;
+        jn = d + 1;
+        Pn = p_seeds;
+        g0n = jn + 1;
+        const int64_t seg = d - jb.seg_start + 1;
+        winn = max(jb.min_win, seg + seg / 8);
+        ok = drawn;
+    } else {
+        jn = jb.b_end;
+        ok = jb.tail == 0;
+        const int64_t Wg = max((int64_t)0, min(jb.b_end, jb.n_full) - jb.g0);
+        Pn = Wg > 0 ? *jb.pick + 1 : (jb.p_after_first >= 0 ? jb.p_after_first : jb.p_now);
+        g0n = jn;
+        winn = jb.win * 2;
+    }
+    int64_t Wn = 0, bn = 0;
+    if (jn < jb.nb) {
+        bn = min(jb.nb, jn + min(winn, jb.max_win));
+        Wn = max((int64_t)0, min(bn, jb.n_full) - g0n);
+        if (bn == jb.nb && jb.last_len != jb.pb && jb.nb - 1 >= g0n) ok = false;   // a host-shuffled tail
+        // the draws the window may need (the host's window_draws, rounded up) are tabulated
+        if (Pn + (Wn * jb.dpb_x1024 * 115 + 102399) / 102400 + 4 * 8192 > jb.next_avail) ok = false;
+    } else {
+        ok = false;
+    }
+    if (!ok) Wn = 0;
+    int64_t* po = jb.plan_out;
+    po[0] = Pn;
+    po[1] = Wn;
+    po[2] = g0n;
+    po[3] = bn;
+    po[4] = jn;
+    po[5] = ok ? 1 : 0;
+    if (jb.next_job) {
+        jb.next_job->P = Pn;
+        jb.next_job->W = Wn;
+        jb.next_job->perm_out = const_cast<uint8_t*>(jb.perm) + jb.base + g0n * jb.pb;
+        jb.next_job->avail = jb.next_avail;
+    }
+}
 
 __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__ jobs) {
     __shared__ int counts[kStageThreads / 64];
@@ -113,6 +166,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
         if (t == 0) {
             jb.info_out[0] = -1;
             jb.info_out[3] = -1;
+            if (jb.plan_out) plan_next(jb, stop, false, -1);
         }
         return;
     }
@@ -146,7 +200,10 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     __shared__ int ok;
     const int64_t j = d + 1;
     if (!jb.R || !jb.perm_w || !jb.seeds_out || j >= jb.nb) {
-        if (t == 0) jb.info_out[6] = 0;
+        if (t == 0) {
+            jb.info_out[6] = 0;
+            if (jb.plan_out) plan_next(jb, stop, false, -1);
+        }
         return;
     }
     const int Lj = j == jb.nb - 1 ? jb.last_len : jb.pb;
@@ -208,7 +265,10 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     }
     __syncthreads();
     if (!ok) {
-        if (t == 0) jb.info_out[6] = 0;
+        if (t == 0) {
+            jb.info_out[6] = 0;
+            if (jb.plan_out) plan_next(jb, stop, false, -1);
+        }
         return;
     }
     for (int i = t; i < Lj; i += kStageThreads) jb.perm_w[jb.base + j * jb.pb + i] = perm[i];
@@ -216,6 +276,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
         jb.info_out[4] = pos[0];
         jb.info_out[5] = pos[1];
         jb.info_out[6] = 1;
+        if (jb.plan_out) plan_next(jb, stop, true, pos[1]);
     }
 }
 

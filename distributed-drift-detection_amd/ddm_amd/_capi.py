@@ -10,7 +10,8 @@ import os
 
 import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
+# DDM_AMD_LIB: an alternative build of the same library (e.g. an instrumented one)
+LIB_PATH = os.environ.get("DDM_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
 ABI_VERSION = 12
 
 DDM_E_ARG = 1001
@@ -53,7 +54,9 @@ class DdmEpoch(ctypes.Structure):
                 ("state", _vp), ("first_nz", _vp), ("batch_base", _vp), ("n_batches_total", _i64),
                 ("ev_out", _vp), ("stop", _vp), ("nev", _vp), ("perm_map", _vp), ("long_off", _vp),
                 ("long_end", _vp), ("long_max_rows", _i64), ("long_scratch", _vp), ("stage_jobs", _vp),
-                ("dfit_jobs", _vp), ("n_dfit", _i32), ("max_trees", _i32), ("ev", _vp * 10)]
+                ("dfit_jobs", _vp), ("n_dfit", _i32), ("max_trees", _i32), ("ev", _vp * 10),
+                ("pick_jobs", _vp), ("n_pick", _i32), ("n_next", _i32), ("next_jobs", _vp), ("next_max_W", _i64),
+                ("next_max_pieces", _i64), ("side_stream", _vp), ("fork_ev", _vp), ("join_ev", _vp)]
 _f32, _pi32 = ctypes.c_float, ctypes.POINTER(ctypes.c_int32)
 
 # name -> (restype, argtypes); every symbol include/ddm_amd.h declares.

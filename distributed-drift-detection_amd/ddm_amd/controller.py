@@ -158,11 +158,11 @@ def sklearn_refit(settings):
 class RunStats:
     __slots__ = ("epochs", "refits", "predicted_rows", "refit_s", "gpu_s", "host_s", "predict_ms", "predict_bytes",
                  "scan_ms", "scan_rows", "shuffle_ms", "sklearn_refits", "refit_fit_s", "refit_readback_s",
-                 "prep_s", "dfit_ms", "device_refits", "long_scans")
+                 "prep_s", "dfit_ms", "device_refits", "long_scans", "preshuffled")
 
     def __init__(self):
         self.epochs = self.refits = self.predicted_rows = self.predict_bytes = self.scan_rows = 0
-        self.sklearn_refits = self.device_refits = self.long_scans = 0
+        self.sklearn_refits = self.device_refits = self.long_scans = self.preshuffled = 0
         self.refit_s = self.gpu_s = self.host_s = self.predict_ms = self.scan_ms = self.shuffle_ms = 0.0
         self.refit_fit_s = self.refit_readback_s = self.prep_s = self.dfit_ms = 0.0
 
@@ -267,12 +267,18 @@ class BatchRunner:
         self.max_events = 64
         # ranges of the partitions routed to ddm_scan_long this epoch (empty for the others)
         self.o_loff, self.o_lend = 108 * k, 116 * k
+        # shuffle-job tables: the epoch's windows (the pick reads them), a copy without the
+        # windows the previous epoch shuffled already, and the next windows the staging
+        # plans (one slot per partition, written by the device)
+        jb = _round_up(n * kernels.JOB_DTYPE.itemsize, 256)
         self.o_jobs = _round_up(self.o_lend + 8 * k, 256)
-        self.o_stage_tab = self.o_jobs + _round_up(n * kernels.JOB_DTYPE.itemsize, 256)
+        self.o_sjobs = self.o_jobs + jb
+        self.o_njobs = self.o_sjobs + jb
+        self.o_stage_tab = self.o_njobs + jb
         self.o_dfit_tab = self.o_stage_tab + _round_up(n * kernels.STAGE_DTYPE.itemsize, 256)
         self.o_stage = self.o_dfit_tab + _round_up(n * dfit.DFIT_DTYPE.itemsize, 256)
         sz = {"x": 4 * 256 * F, "y": 4 * 256, "w": 4 * self.n_words, "info": 64, "ev": 12 * self.max_events,
-              "seeds": 8 * self.s.n_estimators, "dfit": 8 * dfit.RESULT_WORDS}
+              "seeds": 8 * self.s.n_estimators, "dfit": 8 * dfit.RESULT_WORDS, "plan": 48}
         self.stage_off, self.stage_stride = {}, {}
         o = self.o_stage
         for key, nbytes in sz.items():
@@ -286,6 +292,10 @@ class BatchRunner:
         self._info_all = np.lib.stride_tricks.as_strided(      # every partition's staging info
             self.ctrl_h.numpy()[a:a + self.stage_stride["info"] * n].view(np.int64), shape=(n, 7),
             strides=(self.stage_stride["info"], 8), writeable=False)
+        a = self.stage_off["plan"]
+        self._plan_all = np.lib.stride_tricks.as_strided(      # every partition's next-window plan
+            self.ctrl_h.numpy()[a:a + self.stage_stride["plan"] * n].view(np.int64), shape=(n, 6),
+            strides=(self.stage_stride["plan"], 8), writeable=False)
         self.ctrl_d = torch.zeros(self.ctrl_bytes, dtype=torch.uint8, device=dev)
         c = self.ctrl_h.numpy()
         self.first_h = c[self.o_first:self.o_first + 8 * n].view(np.int64)
@@ -308,6 +318,10 @@ class BatchRunner:
         self.segs = kernels.PinnedTable(kernels.SEG_DTYPE, n, dev)
         self.jobs = kernels.PinnedTable(kernels.JOB_DTYPE, n, dev, self.ctrl_h[self.o_jobs:],
                                         self.ctrl_d[self.o_jobs:])
+        self.sjobs = kernels.PinnedTable(kernels.JOB_DTYPE, n, dev, self.ctrl_h[self.o_sjobs:],
+                                         self.ctrl_d[self.o_sjobs:])
+        self.njobs = kernels.PinnedTable(kernels.JOB_DTYPE, n, dev, self.ctrl_h[self.o_njobs:],
+                                         self.ctrl_d[self.o_njobs:])
         self.stage_jobs = kernels.PinnedTable(kernels.STAGE_DTYPE, n, dev, self.ctrl_h[self.o_stage_tab:],
                                               self.ctrl_d[self.o_stage_tab:])
         # device refits: per partition its output buffers and its (static) job record,
@@ -339,6 +353,7 @@ class BatchRunner:
             self.shuffles.append(GpuShuffle(dev, pb, cap, mw, self.stream, self.gen_stream, self.tab_stream))
         self.stats = RunStats()
         self._gen_rest = None
+        self._forked = False          # the last epoch shuffled the next windows it planned
         self._E = self._epoch_desc()
         self.trace = [] if _HOST_TRACE else None     # (label, seconds since run start)
 
@@ -573,11 +588,18 @@ class BatchRunner:
             r["x_out"], r["y_out"], r["w_out"] = self._sptr("x", i), self._sptr("y", i), self._sptr("w", i)
             r["info_out"], r["ev_out"], r["perm_w"], r["seeds_out"] = self._sptr("info", i), self._sptr("ev", i), \
                 perm, self._sptr("seeds", i)
+            r["max_win"], r["n_full"], r["min_win"] = self.max_wins[i], self.nbs[i] - (1 if r["last_len"] != pb else 0), \
+                max(1, min(self.s.window_batches, self.s.drift_window_batches))
+            r["dpb_x1024"] = int(np.ceil(expected_draws_per_batch(pb) * 1024))
+            r["plan_out"], r["next_job"] = self._sptr("plan", i), self.njobs.d.data_ptr() + i * kernels.JOB_DTYPE.itemsize
             sh = self.shuffles[i]
             q = job[i]
             q["pieces"], q["info"], q["J"], q["E"] = sh.pieces.data_ptr(), sh.info.data_ptr(), sh.J.data_ptr(), \
                 sh.E.data_ptr()
             q["first"], q["pick_out"] = sh.first.data_ptr(), self._dptr(self.o_pick, i, 8)
+            nj = self.njobs.rec[i]                       # the next-window slot (static fields)
+            nj["pieces"], nj["info"], nj["J"], nj["E"], nj["first"] = q["pieces"], q["info"], q["J"], q["E"], q["first"]
+            nj["W"] = 0
         self._tmpl = {"seg": seg, "stage": stg, "job": job, "forest": [None] * n, "ptrs": [None] * n,
                       "forest_view": seg[["nodes", "roots", "leaf_value", "classes", "n_trees", "n_classes", "n_nodes",
                                           "pure", "cforest", "cf_slots", "cf_vote_regs", "cf_leaves", "cf_tab_words"]],
@@ -594,6 +616,8 @@ class BatchRunner:
                 t["ptrs"][ps.i] = p
                 t["job"][ps.i]["R"], t["job"][ps.i]["Tpre"], t["job"][ps.i]["Tchunk"] = p
                 t["stage"][ps.i]["R"] = p[0]
+                nj = self.njobs.rec[ps.i]
+                nj["R"], nj["Tpre"], nj["Tchunk"] = p
         return t
 
     def _segment_table(self, live):
@@ -623,6 +647,10 @@ class BatchRunner:
         rec["p_after_first"] = [-1 if ps.P_after_first is None else ps.P_after_first for ps in live]
         rec["p_tail_after"] = [-1 if ps.P_tail_after is None else ps.P_tail_after for ps in live]
         rec["tail"] = [1 if ps.tail else 0 for ps in live]
+        rec["p_now"] = [ps.P for ps in live]
+        rec["win"] = [ps.win for ps in live]
+        rec["seg_start"] = [ps.seg_start for ps in live]
+        rec["next_avail"] = [self.shuffles[ps.i].waited * CHUNK for ps in live]
         self.stage_jobs.rec[:len(live)] = rec
 
     def _jobs_for(self, live, with_stop, upload=True):
@@ -679,6 +707,7 @@ class BatchRunner:
             raise ValueError("one MT19937 stream per partition")
         self._t_run = time.perf_counter()
         self._gen_rest = None
+        self._forked = False
         if self.trace is not None:
             self.trace = []
         pss = []
@@ -818,11 +847,26 @@ class BatchRunner:
         E.long_off, E.long_end, E.long_scratch = base + self.o_loff, base + self.o_lend, self.long_scratch.data_ptr()
         E.stage_jobs, E.dfit_jobs = self.stage_jobs.d.data_ptr(), self.dfit_jobs.d.data_ptr()
         E.max_trees = self.s.n_estimators
+        E.next_jobs = self.njobs.d.data_ptr()
+        self.side_stream = torch.cuda.Stream(self.device, priority=-1)
+        E.side_stream = self.side_stream.cuda_stream
+        self._fork_ev, self._join_ev = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib.ddm_event_create(ctypes.byref(self._fork_ev)), "ddm_event_create")
+        check(lib.ddm_event_create(ctypes.byref(self._join_ev)), "ddm_event_create")
+        E.fork_ev, E.join_ev = self._fork_ev.value, self._join_ev.value
         if self.timing:
             for k, t in enumerate((self.t_shuf, self.t_pred, self.t_scan, self.t_long, self.t_fit)):
                 if t is not None:
                     E.ev[2 * k], E.ev[2 * k + 1] = t.ev[0].value, t.ev[1].value
         return E
+
+    def _next_bound(self, ps):
+        """The largest window the epoch after this one can give partition ps (the policy of
+        _epoch_after: 9/8 of the concept just closed after a change, twice the window
+        otherwise)."""
+        s = self.s
+        lo = max(1, min(s.window_batches, s.drift_window_batches))
+        return min(ps.max_win, max(lo, (ps.b_end - ps.seg_start) * 9 // 8 + 1, 2 * ps.win))
 
     def _enqueue_rest(self):
         """The partitions' whole streams, in growing pieces on the side streams (the first
@@ -866,17 +910,32 @@ class BatchRunner:
             ps.tail = ps.b_end == ps.nb and ps.last_len != pb and ps.nb - 1 >= ps.g0
             ps.P_tail_after = None
         shuf = [ps for ps in live if ps.Wg]
-        # stream coverage: the window's shuffles, and the words the staging reads after a
-        # change (from at most the window's last draw)
-        self._ensure_all([(ps.i, ps.P + self.shuffles[ps.i].window_draws(ps.Wg) + self.n_words) for ps in live])
-        if shuf:
-            max_W = max(ps.Wg for ps in shuf)
-            max_pieces = max(2 + 64 + self.shuffles[ps.i].window_draws(ps.Wg) // 8192 for ps in shuf)
+        # windows the previous epoch shuffled already (the staging planned them on the
+        # device and the executor ran them beside the refits): the plan must be this one
+        pre = set()
+        if self._forked and shuf:
+            plans = self._plan_all.tolist()
+            for ps in shuf:
+                pl = plans[ps.i]
+                if pl[5] == 1 and pl[0] == ps.P and pl[1] == ps.Wg and pl[2] == ps.g0:
+                    pre.add(ps.i)
+        # stream coverage: the window's shuffles, the words the staging reads after a change
+        # (from at most the window's last draw), and the largest next window
+        nxt = {ps.i: self._next_bound(ps) for ps in live}
+        self._ensure_all([(ps.i, ps.P + self.shuffles[ps.i].window_draws(ps.Wg) + self.n_words
+                           + self.shuffles[ps.i].window_draws(nxt[ps.i])) for ps in live])
+        rest = [ps for ps in shuf if ps.i not in pre]
+        max_W = max_pieces = 0
+        if rest:
+            max_W = max(ps.Wg for ps in rest)
+            max_pieces = max(2 + 64 + self.shuffles[ps.i].window_draws(ps.Wg) // 8192 for ps in rest)
         tails = [ps for ps in live if ps.tail]
         shuffled = False
         if tails:
             # the short last batch is shuffled on the host after the GPU batches before it
             if shuf:
+                max_W = max(ps.Wg for ps in shuf)
+                max_pieces = max(2 + 64 + self.shuffles[ps.i].window_draws(ps.Wg) // 8192 for ps in shuf)
                 self._jobs_for(shuf, with_stop=False)
                 kernels.shuffle_window_batch(self.jobs, len(shuf), max_W, max_pieces, pb, stream, self.t_shuf)
                 kernels.shuffle_pick_batch(self.jobs, len(shuf), stream)
@@ -922,8 +981,23 @@ class BatchRunner:
         if not late_fit and not shuffled:
             # the whole epoch in one native call (csrc/epoch.hip)
             E = self._E
-            E.n_shuffle = len(shuf)
-            E.max_W, E.max_pieces = (max_W, max_pieces) if shuf else (0, 0)
+            E.pick_jobs, E.n_pick = self.jobs.d.data_ptr(), len(shuf)
+            if pre and rest:                    # the shuffles skip the windows done already
+                self.sjobs.rec[:len(shuf)] = self.jobs.rec[:len(shuf)]
+                self.sjobs.rec["W"][[k for k, ps in enumerate(shuf) if ps.i in pre]] = 0
+                E.shuffle_jobs = self.sjobs.d.data_ptr()
+            else:
+                E.shuffle_jobs = self.jobs.d.data_ptr()
+            E.n_shuffle = len(shuf) if rest else 0
+            E.max_W, E.max_pieces = max_W, max_pieces
+            st.preshuffled += len(pre)
+            # the next windows: planned by the staging, shuffled beside the refits
+            live_ids = {ps.i for ps in live}
+            self.njobs.rec["W"][[i for i in range(len(self.parts)) if i not in live_ids]] = 0
+            E.n_next = len(self.parts)
+            E.next_max_W = max(nxt.values())
+            E.next_max_pieces = 2 + 64 + self.shuffles[live[0].i].window_draws(E.next_max_W) // 8192
+            self._forked = True
             E.n_segs = E.n_stage = len(live)
             E.long_max_rows = long_rows
             E.n_dfit = len(live) if self.dfit_rows else 0
@@ -934,8 +1008,9 @@ class BatchRunner:
             self._mark("launched")
             stream.synchronize()
             self._mark("synchronized")
-            self._epoch_after(live, st, pb, shuf, long_rows, t1, host)
+            self._epoch_after(live, st, pb, E.n_shuffle > 0, long_rows, t1, host)
             return
+        self._forked = False
         with torch.cuda.stream(stream):
             self.ctrl_d[:self.o_stage].copy_(self.ctrl_h[:self.o_stage], non_blocking=True)
         if shuf and not shuffled:
@@ -975,9 +1050,9 @@ class BatchRunner:
         self._mark("launched")
         stream.synchronize()
         self._mark("synchronized")
-        self._epoch_after(live, st, pb, shuf, long_rows, t1, host)
+        self._epoch_after(live, st, pb, bool(shuf), long_rows, t1, host)
 
-    def _epoch_after(self, live, st, pb, shuf, long_rows, t1, host):
+    def _epoch_after(self, live, st, pb, shuffled, long_rows, t1, host):
         """Everything after an epoch's read-back: timings, events, RNG positions, the next
         windows."""
         s, stream = self.s, self.stream
@@ -986,7 +1061,7 @@ class BatchRunner:
             st.scan_ms += self.t_scan.elapsed_ms()
             if long_rows:
                 st.scan_ms += self.t_long.elapsed_ms()
-            if shuf:
+            if shuffled:
                 st.shuffle_ms += self.t_shuf.elapsed_ms()
             if self.t_fit is not None and self.dfit_rows:
                 st.dfit_ms += self.t_fit.elapsed_ms()

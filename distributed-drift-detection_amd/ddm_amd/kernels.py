@@ -39,8 +39,10 @@ STAGE_DTYPE = np.dtype([("X", "<u8"), ("ld", "<i8"), ("y", "<u8"), ("perm", "<u8
                         ("last_len", "<i4"), ("n_features", "<i4"), ("n_words", "<i4"), ("tail", "<i4"),
                         ("max_events", "<i4"), ("x_out", "<u8"), ("y_out", "<u8"), ("w_out", "<u8"),
                         ("info_out", "<u8"), ("ev_out", "<u8"), ("perm_w", "<u8"), ("seeds_out", "<u8"),
-                        ("n_trees", "<i4"), ("pad", "<i4")])
-assert STAGE_DTYPE.itemsize == 208
+                        ("n_trees", "<i4"), ("pad", "<i4"), ("p_now", "<i8"), ("win", "<i8"), ("max_win", "<i8"),
+                        ("seg_start", "<i8"), ("n_full", "<i8"), ("min_win", "<i8"), ("next_avail", "<i8"),
+                        ("dpb_x1024", "<i8"), ("plan_out", "<u8"), ("next_job", "<u8")])
+assert STAGE_DTYPE.itemsize == 288
 
 
 class PinnedTable:

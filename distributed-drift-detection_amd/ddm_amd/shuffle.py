@@ -128,8 +128,8 @@ class GpuShuffle:
         # the window's first piece, the sub-chunks of the chunk holding its start, then chunks
         self.max_pieces = 4 + CHUNK // SUB + (self.max_window * L * 3) // CHUNK
         self.pieces = torch.empty(self.max_pieces * 16, dtype=torch.uint8, device=device)
-        self.first = torch.empty((CHUNK // SUB) * self.S, dtype=torch.int16, device=device)
-        self.info = torch.zeros(3, dtype=torch.int64, device=device)
+        self.first = torch.empty((CHUNK // SUB) * self.S + 8, dtype=torch.int16, device=device)   # + 16-byte over-read
+        self.info = torch.zeros(8, dtype=torch.int64, device=device)   # [3..7]: instrumented builds
         self.J = torch.zeros(self.max_window * L, dtype=torch.uint8, device=device)
         self.E = torch.zeros(self.max_window, dtype=torch.int64, device=device)
         self.words_h = torch.empty(4096, dtype=torch.int32, pin_memory=True)

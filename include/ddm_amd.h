@@ -400,6 +400,13 @@ typedef struct ddm_stage_job {
     uint8_t* perm_w;        /* perm array to receive batch d+1's shuffle (may be NULL)   */
     int64_t* seeds_out;     /* [n_trees] refit seeds drawn after it (may be NULL)        */
     int32_t n_trees, pad;
+    /* next-window plan (plan_out may be NULL): the controller's window policy applied on
+     * the device, so the next window's shuffles can run before the host has seen this
+     * epoch.  plan_out = {P, W (0: not planned), g0, b_end, j, planned}; next_job (may be
+     * NULL) = this partition's ddm_shuffle_job whose P, W, perm_out and avail are set. */
+    int64_t p_now, win, max_win, seg_start, n_full, min_win, next_avail, dpb_x1024;
+    int64_t* plan_out;
+    ddm_shuffle_job* next_job;
 } ddm_stage_job;
 
 int ddm_epoch_stage(const ddm_stage_job* jobs_dev, int32_t n_jobs, ddm_stream_t stream);
@@ -499,6 +506,13 @@ typedef struct ddm_epoch {
     const int64_t* long_off; const int64_t* long_end; int64_t long_max_rows; void* long_scratch;
     const ddm_stage_job* stage_jobs; const ddm_dfit_job* dfit_jobs; int32_t n_dfit, max_trees;
     ddm_event_t ev[10];
+    /* shuffle_jobs drive the shuffles, pick_jobs (all partitions with a window) the pick */
+    const ddm_shuffle_job* pick_jobs; int32_t n_pick, n_next;
+    /* the next windows' shuffles (n_next > 0): next_jobs planned by the staging, run on
+     * side_stream between fork_ev (after the staging) and join_ev (before the read-back),
+     * beside the device refits */
+    const ddm_shuffle_job* next_jobs; int64_t next_max_W, next_max_pieces;
+    ddm_stream_t side_stream; ddm_event_t fork_ev, join_ev;
 } ddm_epoch;
 int ddm_epoch_launch(const ddm_epoch* e);
 int64_t ddm_epoch_struct_bytes(void);   /* sizeof(ddm_epoch), for binding checks */
