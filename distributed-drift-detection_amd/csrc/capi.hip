@@ -37,6 +37,10 @@ extern "C" int ddm_event_record(ddm_event_t ev, ddm_stream_t stream) {
     return ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev), ddm::as_hip(stream)), "ddm_event_record");
 }
 
+extern "C" int ddm_event_synchronize(ddm_event_t ev) {
+    return ddm::hip_status(hipEventSynchronize(reinterpret_cast<hipEvent_t>(ev)), "ddm_event_synchronize");
+}
+
 extern "C" int ddm_event_elapsed_ms(ddm_event_t begin, ddm_event_t end, float* ms) {
     if (!ms) return DDM_E_ARG;
     return ddm::hip_status(hipEventElapsedTime(ms, reinterpret_cast<hipEvent_t>(begin), reinterpret_cast<hipEvent_t>(end)),

@@ -41,6 +41,7 @@ extern "C" int ddm_epoch_launch(const ddm_epoch* e) {
     if (e->n_stage > 0)
         if (int rc = ddm_epoch_stage(e->stage_jobs, e->n_stage, e->stream)) return rc;
     const bool fork = e->n_next > 0 && e->next_jobs && e->side_stream && e->fork_ev && e->join_ev;
+    const bool split = e->mid_ev != nullptr && e->download_bytes > 0;
     if (fork) {
         // the next windows' shuffles (planned by the staging) beside the refits
         hipStream_t side = ddm::as_hip(e->side_stream);
@@ -51,6 +52,14 @@ extern "C" int ddm_epoch_launch(const ddm_epoch* e) {
                                               e->side_stream, nullptr, nullptr))
             return rc;
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(e->join_ev), side), "join")) return rc;
+    }
+    if (split) {
+        // everything but the refit results goes back now (mid_ev); the host works on it
+        // while the refits and the next shuffles run
+        if (int rc = ddm::hip_status(hipMemcpyAsync(e->ctrl_h, e->ctrl_d, (size_t)e->download_bytes,
+                                                    hipMemcpyDeviceToHost, s), "ddm_epoch_launch/read-back"))
+            return rc;
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(e->mid_ev), s), "mid")) return rc;
     }
     if (e->n_dfit > 0) {
         if (e->ev[8])
@@ -64,10 +73,19 @@ extern "C" int ddm_epoch_launch(const ddm_epoch* e) {
     if (fork)
         if (int rc = ddm::hip_status(hipStreamWaitEvent(s, reinterpret_cast<hipEvent_t>(e->join_ev), 0), "join"))
             return rc;
-    if (e->download_bytes)
+    if (split) {
+        if (e->tail_bytes > 0)
+            if (int rc = ddm::hip_status(
+                    hipMemcpyAsync(static_cast<uint8_t*>(e->ctrl_h) + e->tail_off,
+                                   static_cast<const uint8_t*>(e->ctrl_d) + e->tail_off, (size_t)e->tail_bytes,
+                                   hipMemcpyDeviceToHost, s),
+                    "ddm_epoch_launch/refit read-back"))
+                return rc;
+    } else if (e->download_bytes) {
         if (int rc = ddm::hip_status(hipMemcpyAsync(e->ctrl_h, e->ctrl_d, (size_t)e->download_bytes,
                                                     hipMemcpyDeviceToHost, s), "ddm_epoch_launch/read-back"))
             return rc;
+    }
     return 0;
 }
 

@@ -656,21 +656,28 @@ __device__ __forceinline__ uint32_t vote_word(int c, int j) { return (c >> 2) ==
 
 constexpr int kPackThreads = 256;
 
-// Block-wide exclusive prefix sum of one int per thread (kPackThreads threads).
+// Block-wide exclusive prefix sum of one int per thread (kPackThreads threads): a wave
+// scan by shuffles, then the wave totals through LDS (two barriers).
 __device__ int block_scan_excl(int v, int* tmp, int& total) {
-    const int t = threadIdx.x;
-    tmp[t] = v;
-    __syncthreads();
-    for (int o = 1; o < kPackThreads; o <<= 1) {
-        const int u = t >= o ? tmp[t - o] : 0;
-        __syncthreads();
-        tmp[t] += u;
-        __syncthreads();
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    int inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += u;
     }
-    total = tmp[kPackThreads - 1];
-    const int r = tmp[t] - v;
+    if (lane == 63) tmp[wv] = inc;
     __syncthreads();
-    return r;
+    int base = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kPackThreads / 64; ++w) {
+        const int x = tmp[w];
+        base += w < wv ? x : 0;
+        all += x;
+    }
+    total = all;
+    __syncthreads();
+    return base + inc - v;
 }
 
 // ddm_forest_compile (forest_compile.cpp) for a pure forest given as creation-order tree

@@ -196,6 +196,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     // ---- batch j = d + 1: its shuffle, then the refit's tree seeds
     __shared__ uint32_t words[kStageWords];
     __shared__ uint8_t perm[256];
+    __shared__ uint8_t js[256];                 // the accepted j of every interval i
     __shared__ int64_t pos[2];
     __shared__ int ok;
     const int64_t j = d + 1;
@@ -208,7 +209,6 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     }
     const int Lj = j == jb.nb - 1 ? jb.last_len : jb.pb;
     for (int w = t; w < kStageWords; w += kStageThreads) words[w] = jb.R[P + w];
-    for (int i = t; i < Lj; i += kStageThreads) perm[i] = (uint8_t)i;
     __syncthreads();
     if (wv == 0) {
         // legacy permutation(Lj), then randint(2**31 - 1) x n_trees, by the first wave: each
@@ -226,11 +226,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
                     const int f = __builtin_ctzll(b);
                     const int jv = __shfl((int)v, f, 64);
                     k += f + 1;
-                    if (lane == 0) {                                 // the swap, in order
-                        const uint8_t tmp = perm[i];
-                        perm[i] = perm[jv];
-                        perm[jv] = tmp;
-                    }
+                    if (lane == 0) js[i] = (uint8_t)jv;               // swap i <-> jv, applied below
                     break;
                 }
                 k += 64;
@@ -271,6 +267,17 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
         }
         return;
     }
+    // the swaps, all elements at once: element e starts at position e and follows the
+    // transpositions i <-> js[i] for i = Lj-1 .. 1; it ends where Fisher-Yates puts it
+    if (t < Lj) {
+        int q = t;
+        for (int i = Lj - 1; i >= 1; --i) {
+            const int jv = js[i];
+            q = q == i ? jv : (q == jv ? i : q);
+        }
+        perm[q] = (uint8_t)t;
+    }
+    __syncthreads();
     for (int i = t; i < Lj; i += kStageThreads) jb.perm_w[jb.base + j * jb.pb + i] = perm[i];
     if (t == 0) {
         jb.info_out[4] = pos[0];

@@ -56,7 +56,8 @@ class DdmEpoch(ctypes.Structure):
                 ("long_end", _vp), ("long_max_rows", _i64), ("long_scratch", _vp), ("stage_jobs", _vp),
                 ("dfit_jobs", _vp), ("n_dfit", _i32), ("max_trees", _i32), ("ev", _vp * 10),
                 ("pick_jobs", _vp), ("n_pick", _i32), ("n_next", _i32), ("next_jobs", _vp), ("next_max_W", _i64),
-                ("next_max_pieces", _i64), ("side_stream", _vp), ("fork_ev", _vp), ("join_ev", _vp)]
+                ("next_max_pieces", _i64), ("side_stream", _vp), ("fork_ev", _vp), ("join_ev", _vp),
+                ("mid_ev", _vp), ("tail_off", _i64), ("tail_bytes", _i64)]
 _f32, _pi32 = ctypes.c_float, ctypes.POINTER(ctypes.c_int32)
 
 # name -> (restype, argtypes); every symbol include/ddm_amd.h declares.
@@ -92,6 +93,7 @@ SIGNATURES = {
     "ddm_event_destroy": (ctypes.c_int, [_vp]),
     "ddm_event_elapsed_ms": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(ctypes.c_float)]),
     "ddm_event_record": (ctypes.c_int, [_vp, _vp]),
+    "ddm_event_synchronize": (ctypes.c_int, [_vp]),
     "ddm_mt_perms": (ctypes.c_int, [_vp, _pi32, _vp, _i64, _vp, _vp]),
     "ddm_mt_randint31": (ctypes.c_int, [_vp, _pi32, _i64, _vp]),
     "ddm_mt_skip": (ctypes.c_int, [_vp, _pi32, _i64]),

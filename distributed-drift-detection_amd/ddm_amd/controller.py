@@ -174,7 +174,7 @@ class _Part:
     """Host-side epoch state of one partition in a BatchRunner."""
     __slots__ = ("i", "nb", "last_len", "n_full", "max_win", "base", "ev_base", "j", "P", "retrain", "train_rows",
                  "state", "win", "forest", "out", "done", "P_after_first", "g0", "b_end", "Wg", "tail",
-                 "P_tail_after", "seg_start", "pb", "staged", "rng_rows", "words0", "ev")
+                 "P_tail_after", "seg_start", "pb", "staged", "rng_rows", "words0", "ev", "P_seeds")
 
     def blen(self, b):
         return self.last_len if b == self.nb - 1 else self.pb
@@ -354,6 +354,8 @@ class BatchRunner:
         self.stats = RunStats()
         self._gen_rest = None
         self._forked = False          # the last epoch shuffled the next windows it planned
+        self._pending_sync = False    # the last epoch's refit results are still on their way
+        self._pending_forests = []
         self._E = self._epoch_desc()
         self.trace = [] if _HOST_TRACE else None     # (label, seconds since run start)
 
@@ -485,7 +487,12 @@ class BatchRunner:
                 ps.staged = None
                 ps.P = P2
                 ps.P_after_first = ps.P
-                ps.forest = dfit.DeviceFitForest(self.dfit_bufs[ps.i], res)
+                if res is None:                                 # the refit is still running
+                    ps.forest = None
+                    ps.P_seeds = P1
+                    self._pending_forests.append(ps)
+                else:
+                    ps.forest = dfit.DeviceFitForest(self.dfit_bufs[ps.i], res)
                 ps.retrain = False
                 ps.state = kernels.fresh_states(1)              # ddm = None -> new DDM (:136-139)
                 ps.g0 = ps.j + 1
@@ -708,6 +715,8 @@ class BatchRunner:
         self._t_run = time.perf_counter()
         self._gen_rest = None
         self._forked = False
+        self._pending_sync = False
+        self._pending_forests = []
         if self.trace is not None:
             self.trace = []
         pss = []
@@ -793,6 +802,7 @@ class BatchRunner:
                 if not live:
                     break
                 self._epoch(live)
+            self._finish_pending()
             outs = []
             for ps, f in zip(pss, out_f):
                 out = f.result()
@@ -848,12 +858,19 @@ class BatchRunner:
         E.stage_jobs, E.dfit_jobs = self.stage_jobs.d.data_ptr(), self.dfit_jobs.d.data_ptr()
         E.max_trees = self.s.n_estimators
         E.next_jobs = self.njobs.d.data_ptr()
-        self.side_stream = torch.cuda.Stream(self.device, priority=-1)
+        self.side_stream = torch.cuda.Stream(self.device, priority=0)    # below the refits (epoch stream)
         E.side_stream = self.side_stream.cuda_stream
         self._fork_ev, self._join_ev = ctypes.c_void_p(), ctypes.c_void_p()
         check(lib.ddm_event_create(ctypes.byref(self._fork_ev)), "ddm_event_create")
         check(lib.ddm_event_create(ctypes.byref(self._join_ev)), "ddm_event_create")
         E.fork_ev, E.join_ev = self._fork_ev.value, self._join_ev.value
+        if self.dfit_rows:
+            # split read-back: the host works on the epoch while the refits run
+            self._mid_ev = ctypes.c_void_p()
+            check(lib.ddm_event_create(ctypes.byref(self._mid_ev)), "ddm_event_create")
+            E.mid_ev = self._mid_ev.value
+            E.tail_off = self.stage_off["dfit"]
+            E.tail_bytes = self.stage_stride["dfit"] * len(self.parts)
         if self.timing:
             for k, t in enumerate((self.t_shuf, self.t_pred, self.t_scan, self.t_long, self.t_fit)):
                 if t is not None:
@@ -965,6 +982,7 @@ class BatchRunner:
                 self.end_h[ps.i] = p0            # nothing for the one-lane scan
                 long_rows = max(long_rows, p1 - p0)
                 st.long_scans += 1
+        self._finish_pending()                  # the forests of the previous epoch's refits
         if not late_fit:
             self._segment_table(live)
         t2 = time.perf_counter()
@@ -1006,9 +1024,17 @@ class BatchRunner:
             self._mark("tables + upload")
             check(lib.ddm_epoch_launch(ctypes.byref(E)), "ddm_epoch_launch")
             self._mark("launched")
-            stream.synchronize()
-            self._mark("synchronized")
-            self._epoch_after(live, st, pb, E.n_shuffle > 0, long_rows, t1, host)
+            if E.mid_ev:
+                # everything but the refit results is back: the host goes on (this epoch's
+                # events, the next epoch's tables) while the refits run
+                check(lib.ddm_event_synchronize(E.mid_ev), "ddm_event_synchronize")
+                self._mark("synchronized")
+                self._pending_sync = True
+                self._epoch_after(live, st, pb, E.n_shuffle > 0, long_rows, t1, host, deferred=True)
+            else:
+                stream.synchronize()
+                self._mark("synchronized")
+                self._epoch_after(live, st, pb, E.n_shuffle > 0, long_rows, t1, host)
             return
         self._forked = False
         with torch.cuda.stream(stream):
@@ -1052,7 +1078,37 @@ class BatchRunner:
         self._mark("synchronized")
         self._epoch_after(live, st, pb, bool(shuf), long_rows, t1, host)
 
-    def _epoch_after(self, live, st, pb, shuffled, long_rows, t1, host):
+    def _finish_pending(self):
+        """The previous epoch's read-back of the refit results (split read-back): wait for
+        it, then give the partitions whose refit ran on the device their forests (or, when
+        a device refit reports a status, refit them on the host from the staged batch)."""
+        if not self._pending_sync:
+            return
+        self.stream.synchronize()
+        self._pending_sync = False
+        self._mark("refits back")
+        st = self.stats
+        if self.timing and self.t_fit is not None:
+            st.dfit_ms += self.t_fit.elapsed_ms()
+        work = []
+        for ps in self._pending_forests:
+            res = self._sview("dfit", ps.i, np.int64, dfit.RESULT_WORDS)
+            if int(res[0]) == 0:
+                ps.forest = dfit.DeviceFitForest(self.dfit_bufs[ps.i], res.copy())
+            else:                                   # refit on the host, same batch and seeds
+                L = ps.blen(ps.j - 1)
+                F_i = ps_feats(self.parts[ps.i])
+                X32 = self._sview("x", ps.i, np.float32, L * F_i).reshape(L, -1).copy()
+                y = self._sview("y", ps.i, np.int32, L).astype(np.int64)
+                seeds = self._sview("seeds", ps.i, np.int64, self.s.n_estimators).copy()
+                work.append((ps, X32, y, seeds, ps.P_seeds))
+                st.refits -= 1
+                st.device_refits -= 1
+        self._pending_forests = []
+        if work:
+            self._refit_fit(work)
+
+    def _epoch_after(self, live, st, pb, shuffled, long_rows, t1, host, deferred=False):
         """Everything after an epoch's read-back: timings, events, RNG positions, the next
         windows."""
         s, stream = self.s, self.stream
@@ -1063,7 +1119,7 @@ class BatchRunner:
                 st.scan_ms += self.t_long.elapsed_ms()
             if shuffled:
                 st.shuffle_ms += self.t_shuf.elapsed_ms()
-            if self.t_fit is not None and self.dfit_rows:
+            if self.t_fit is not None and self.dfit_rows and not deferred:
                 st.dfit_ms += self.t_fit.elapsed_ms()
         # the control block as Python ints, one conversion per array
         stops, nevs, picks = self.stop_h.tolist(), self.nev_h.tolist(), self.pick_h.tolist()
@@ -1122,7 +1178,9 @@ class BatchRunner:
                 L = ps.blen(d)
                 drawn = info[6] == 1                # batch d+1's shuffle and the seeds, on the device
                 res = self._sview("dfit", ps.i, np.int64, dfit.RESULT_WORDS) if self.dfit_rows else None
-                if drawn and res is not None and int(res[0]) == 0:
+                if drawn and deferred and res is not None:
+                    ps.staged = ("device", info[4], info[5], None)   # results after the next tables
+                elif drawn and res is not None and int(res[0]) == 0:
                     ps.staged = ("device", info[4], info[5], res.copy())
                 else:
                     F_i = ps_feats(self.parts[ps.i])

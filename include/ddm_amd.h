@@ -276,6 +276,7 @@ int ddm_scan_long(const uint8_t* err, const int64_t* stream_off, const int64_t* 
 int ddm_event_create(ddm_event_t* ev);
 int ddm_event_destroy(ddm_event_t ev);
 int ddm_event_record(ddm_event_t ev, ddm_stream_t stream);
+int ddm_event_synchronize(ddm_event_t ev);
 int ddm_event_elapsed_ms(ddm_event_t begin, ddm_event_t end, float* ms);
 
 /* ---- host-side MT19937 (numpy legacy RandomState layout: key[624], pos) ---------- */
@@ -513,6 +514,9 @@ typedef struct ddm_epoch {
      * beside the device refits */
     const ddm_shuffle_job* next_jobs; int64_t next_max_W, next_max_pieces;
     ddm_stream_t side_stream; ddm_event_t fork_ev, join_ev;
+    /* split read-back (mid_ev != NULL): the slab right after the staging, then mid_ev,
+     * and after the refits only ctrl[tail_off, tail_off + tail_bytes) (their results) */
+    ddm_event_t mid_ev; int64_t tail_off, tail_bytes;
 } ddm_epoch;
 int ddm_epoch_launch(const ddm_epoch* e);
 int64_t ddm_epoch_struct_bytes(void);   /* sizeof(ddm_epoch), for binding checks */
