@@ -635,9 +635,12 @@ class BatchRunner:
         for ps in live:
             if t["forest"][ps.i] is not ps.forest:          # a new forest: its descriptor fields
                 t["forest"][ps.i] = ps.forest
-                d = ps.forest.desc
-                fv[ps.i] = (d.nodes, d.roots, d.leaf_value or 0, d.classes, d.n_trees, d.n_classes, d.n_nodes, d.pure,
-                            d.cforest or 0, d.cf_slots, d.cf_vote_regs, d.cf_leaves, d.cf_tab_words)
+                if isinstance(ps.forest, dfit.DeviceFitForest):
+                    fv[ps.i] = ps.forest.seg_fields()
+                else:
+                    d = ps.forest.desc
+                    fv[ps.i] = (d.nodes, d.roots, d.leaf_value or 0, d.classes, d.n_trees, d.n_classes, d.n_nodes,
+                                d.pure, d.cforest or 0, d.cf_slots, d.cf_vote_regs, d.cf_leaves, d.cf_tab_words)
         idx = [ps.i for ps in live]
         rec = seg[idx]
         rec["pos_begin"] = [ps.rng_rows[0] for ps in live]
@@ -982,9 +985,6 @@ class BatchRunner:
                 self.end_h[ps.i] = p0            # nothing for the one-lane scan
                 long_rows = max(long_rows, p1 - p0)
                 st.long_scans += 1
-        self._finish_pending()                  # the forests of the previous epoch's refits
-        if not late_fit:
-            self._segment_table(live)
         t2 = time.perf_counter()
         host += t2 - t1
         t1 = t2
@@ -996,7 +996,8 @@ class BatchRunner:
         if self.dfit_rows:
             self.dfit_jobs.rec[:len(live)] = self._templates()["dfit"][[ps.i for ps in live]]
         self.first_h[:] = -1                    # the predict kernels' first-error slots
-        if not late_fit and not shuffled:
+        native = not late_fit and not shuffled
+        if native:
             # the whole epoch in one native call (csrc/epoch.hip)
             E = self._E
             E.pick_jobs, E.n_pick = self.jobs.d.data_ptr(), len(shuf)
@@ -1016,6 +1017,11 @@ class BatchRunner:
             E.next_max_W = max(nxt.values())
             E.next_max_pieces = 2 + 64 + self.shuffles[live[0].i].window_draws(E.next_max_W) // 8192
             self._forked = True
+        # the previous epoch's refits are needed from here on (their forests predict now)
+        self._finish_pending()
+        if not late_fit:
+            self._segment_table(live)
+        if native:
             E.n_segs = E.n_stage = len(live)
             E.long_max_rows = long_rows
             E.n_dfit = len(live) if self.dfit_rows else 0

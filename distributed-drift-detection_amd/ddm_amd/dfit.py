@@ -52,6 +52,13 @@ class RefitBuffers:
                 self.k_cap, 0, self.scratch.data_ptr(), self.nodes.data_ptr(), self.roots.data_ptr(),
                 self.leaf_value.data_ptr(), self.classes.data_ptr(), self.blob.data_ptr(), self.blob.numel(), result)
 
+    def ptrs(self):
+        """(nodes, roots, leaf_value, classes, blob) device addresses (the buffers never move)."""
+        if getattr(self, "_ptrs", None) is None:
+            self._ptrs = (self.nodes.data_ptr(), self.roots.data_ptr(), self.leaf_value.data_ptr(),
+                          self.classes.data_ptr(), self.blob.data_ptr())
+        return self._ptrs
+
     def descriptor(self, res):
         """ddm_forest of the refit whose result row is `res` (status 0)."""
         pure = int(res[PURE])
@@ -70,7 +77,24 @@ class DeviceFitForest:
     def __init__(self, bufs, res):
         self.bufs = bufs
         self.res = np.array(res, dtype=np.int64)
-        self.desc = bufs.descriptor(self.res)
+        self._desc = None
+
+    @property
+    def desc(self):
+        if self._desc is None:
+            self._desc = self.bufs.descriptor(self.res)
+        return self._desc
+
+    def seg_fields(self):
+        """The forest fields of a ddm_predict_segment (kernels.SEG_DTYPE order: nodes, roots,
+        leaf_value, classes, n_trees, n_classes, n_nodes, pure, cforest, cf_slots,
+        cf_vote_regs, cf_leaves, cf_tab_words) without building the ctypes descriptor."""
+        b, r = self.bufs, self.res.tolist()
+        p = b.ptrs()
+        pure, blob = r[PURE], r[BLOB]
+        return (p[0], p[1], 0 if pure else p[2], p[3], b.T, r[CLASSES], r[NODES], pure, p[4] if blob else 0,
+                r[CF_SLOTS] if blob else 0, r[CF_VR] if blob else 0, r[CF_LEAVES] if blob else 0,
+                r[CF_TAB] if blob else 0)
 
     @property
     def compiled(self):
