@@ -886,7 +886,8 @@ class BatchRunner:
         otherwise)."""
         s = self.s
         lo = max(1, min(s.window_batches, s.drift_window_batches))
-        return min(ps.max_win, max(lo, (ps.b_end - ps.seg_start) * 9 // 8 + 1, 2 * ps.win))
+        return max(0, min(ps.max_win, ps.nb - ps.j,
+                          max(lo, (ps.b_end - ps.seg_start) * 9 // 8 + 1, 2 * ps.win)))
 
     def _enqueue_rest(self):
         """The partitions' whole streams, in growing pieces on the side streams (the first
@@ -941,9 +942,15 @@ class BatchRunner:
                     pre.add(ps.i)
         # stream coverage: the window's shuffles, the words the staging reads after a change
         # (from at most the window's last draw), and the largest next window
+        # (the next window's part stays inside the stream buffers: a window planned past
+        # the tabulated draws is simply not pre-shuffled)
         nxt = {ps.i: self._next_bound(ps) for ps in live}
-        self._ensure_all([(ps.i, ps.P + self.shuffles[ps.i].window_draws(ps.Wg) + self.n_words
-                           + self.shuffles[ps.i].window_draws(nxt[ps.i])) for ps in live])
+        wants = []
+        for ps in live:
+            sh = self.shuffles[ps.i]
+            cur = ps.P + sh.window_draws(ps.Wg) + self.n_words
+            wants.append((ps.i, max(cur, min(cur + sh.window_draws(nxt[ps.i]), sh.cap - 2 * CHUNK))))
+        self._ensure_all(wants)
         rest = [ps for ps in shuf if ps.i not in pre]
         max_W = max_pieces = 0
         if rest:
