@@ -389,8 +389,10 @@ class BatchRunner:
             sh = self.shuffles[i]
             if sh.chunks_for(upto) > sh.tab:
                 req, need = sh.gen_request(upto, jumps)
-                reqs.extend(req)
+                if len(req):
+                    reqs.append(req)
                 tabs.append((i, need))
+        self._mark("requests")
         if jumps:
             # segment start states of every partition: one ddm_mt_jump launch
             rec = np.concatenate(jumps)
@@ -398,10 +400,11 @@ class BatchRunner:
             jt.rec[:len(rec)] = rec
             kernels.mt_jump(jt, len(rec), self.gen_stream)
             self.gen_tables.append(jt)
+        self._mark("jumps")
         if reqs:
+            reqs = np.concatenate(reqs)
             table = kernels.PinnedTable(kernels.GEN_DTYPE, len(reqs), self.device)   # read by the async copy
-            for k, (st, R, cnt) in enumerate(reqs):
-                table.rec[k] = (st, R, cnt)
+            table.rec[:len(reqs)] = reqs
             kernels.shuffle_generate_batch(table, len(reqs), self.gen_stream)
             self.gen_tables.append(table)
         if tabs:
@@ -896,15 +899,19 @@ class BatchRunner:
             return
         tp = time.perf_counter()
         upto, total, pss = self._gen_rest
-        self._gen_rest = None
         pb = self.s.per_batch
-        while upto < total:
+        # two pieces per epoch: the epochs' own coverage requests (_ensure_all with wait)
+        # enqueue whatever a window needs first, so this only keeps generation ahead
+        for _ in range(2):
+            if upto >= total:
+                break
             upto = min(total, upto + min(upto, GEN_PIECE_MAX))
             self._ensure_all([(ps.i, min(upto, int(ps.nb * expected_draws_per_batch(pb) * 1.02))) for ps in pss],
                              wait=False)
+            self._mark(f"piece to {upto}")
+        self._gen_rest = (upto, total, pss) if upto < total else None
         if self.timing:
             self.stats.prep_s += time.perf_counter() - tp
-        self._mark("generation enqueued")
 
     def _epoch(self, live):
         s, st, pb, stream = self.s, self.stats, self.s.per_batch, self.stream

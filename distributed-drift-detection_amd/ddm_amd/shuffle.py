@@ -240,17 +240,21 @@ class GpuShuffle:
         target = need_chunks * CHUNK
         if target > self.cap:
             self._alloc(max(target, int(self.cap * 1.5)))
-        reqs = []
+        reqs = np.empty(0, dtype=kernels.GEN_DTYPE)
         if target > self.gen:
             s_last = self._segments_for(target - 1) - 1
             if s_last >= 1:                 # every segment of the expected stream at once
                 self._jump_to(max(s_last + 1, self.n_seg), jumps)
-            s = self._segments_for(self.gen) - 1 if self.gen else 0
-            while s <= s_last:
-                lo, hi = max(self.gen, self.seg_start(s)), min(target, self.seg_start(s + 1))
-                if lo < hi:
-                    reqs.append((self.seg[s].data_ptr(), self.R.data_ptr() + 4 * lo, hi - lo))
-                s += 1
+            s0 = self._segments_for(self.gen) - 1 if self.gen else 0
+            seg = np.arange(s0, s_last + 1, dtype=np.int64)
+            starts = np.where(seg == 0, 0, (624 - self.init_pos) + seg * JUMP)
+            ends = (624 - self.init_pos) + (seg + 1) * JUMP
+            lo, hi = np.maximum(self.gen, starts), np.minimum(target, ends)
+            keep = lo < hi
+            reqs = np.empty(int(keep.sum()), dtype=kernels.GEN_DTYPE)
+            reqs["state"] = self.seg.data_ptr() + seg[keep].astype(np.uint64) * (4 * self.seg.shape[1])
+            reqs["R"] = self.R.data_ptr() + 4 * lo[keep].astype(np.uint64)
+            reqs["n"] = hi[keep] - lo[keep]
             self.gen = target
         return reqs, need_chunks
 
@@ -291,10 +295,9 @@ class GpuShuffle:
         the consuming stream."""
         if self.chunks_for(upto) > self.tab:
             reqs, need_chunks = self.gen_request(upto)
-            if reqs:
+            if len(reqs):
                 table = kernels.PinnedTable(kernels.GEN_DTYPE, len(reqs), self.device)
-                for k, r in enumerate(reqs):
-                    table.rec[k] = r
+                table.rec[:len(reqs)] = reqs
                 kernels.shuffle_generate_batch(table, len(reqs), self.gen_stream)
                 self._keep.append(table)
             if self.tab_stream is not self.gen_stream:
