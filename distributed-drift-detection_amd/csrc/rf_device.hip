@@ -449,6 +449,9 @@ __device__ __forceinline__ void build_tree(const Job& jb, const Layout& lo, int 
     double* vals = reinterpret_cast<double*>(jb.scratch + lo.tvals) + tree * M * jb.k_cap;
     int32_t* meta = reinterpret_cast<int32_t*>(jb.scratch + lo.tmeta) + 4 * tree;
 
+#ifdef DDM_DFIT_PROFILE
+    const uint64_t t_a = wall_clock64();
+#endif
     // ---- RandomState(seed): init_genrand (serial), first block
     if (lane == 0) {
         uint32_t v = (uint32_t)jb.seeds[tree];
@@ -463,6 +466,9 @@ __device__ __forceinline__ void build_tree(const Job& jb, const Layout& lo, int 
     for (int k = lane; k < 624; k += 64) S.tw[k] = temper(S.mt[k]);
     for (int k = lane; k < L; k += 64) S.cnt[k] = 0;
     wave_sync();
+#ifdef DDM_DFIT_PROFILE
+    const uint64_t t_b = wall_clock64();
+#endif
     // splitter seed: first randint(0, 2**31 - 1) of the stream, not consumed
     uint32_t rstate = 0;
     for (int j0 = 0; j0 < 624; j0 += 64) {
@@ -500,6 +506,9 @@ __device__ __forceinline__ void build_tree(const Job& jb, const Layout& lo, int 
     for (int k = lane; k < L; k += 64) S.key[k] = S.cnt[k] > 0 ? 0 : -1;
     for (int f = lane; f < F; f += 64) S.feats[f] = (int16_t)f;
     wave_sync();
+#ifdef DDM_DFIT_PROFILE
+    const uint64_t t_c = wall_clock64();
+#endif
     const double wns = (double)L;               // weighted_n_samples = sum of the counts
     // ---- depth-first build (rf_fit.cpp Builder::build)
     int sp = 0, n_nodes = 0, n_leaves = 0, impure = 0;
@@ -610,6 +619,10 @@ __device__ __forceinline__ void build_tree(const Job& jb, const Layout& lo, int 
         meta[0] = n_nodes;
         meta[1] = n_leaves;
         meta[2] = impure;
+#ifdef DDM_DFIT_PROFILE
+        if (tree == 0)   // rng init | bootstrap | build, 10-ns ticks
+            jb.result[10] = (int64_t)((t_b - t_a) | ((t_c - t_b) << 16) | ((wall_clock64() - t_c) << 32));
+#endif
     }
 }
 
@@ -995,6 +1008,9 @@ __device__ void pack_tree(const TNode* tn, int m, int16_t* new_id, int16_t* queu
 
 __global__ __launch_bounds__(kPackThreads) void k_dfit_pack(const Job* __restrict__ jobs) {
     const Job jb = jobs[blockIdx.x];
+#ifdef DDM_DFIT_PROFILE
+    const uint64_t t_pack0 = wall_clock64();
+#endif
     if (jb.result[DDM_DFIT_STATUS] != 0) return;
     const int t = threadIdx.x;
     const int T = jb.n_trees, K = (int)jb.result[DDM_DFIT_CLASSES];
@@ -1020,9 +1036,15 @@ __global__ __launch_bounds__(kPackThreads) void k_dfit_pack(const Job* __restric
                   jb.k_cap, jb.leaf_value, lbase);
         jb.roots[t] = base;
     }
+#ifdef DDM_DFIT_PROFILE
+    const uint64_t t_p = wall_clock64();
+#endif
     int64_t bytes = 0;
     if (pure && jb.blob)
         bytes = compile_forest(tn, M, meta, T, jb.classes, K, jb.F, bfs, jb.blob, jb.blob_cap);
+#ifdef DDM_DFIT_PROFILE
+    if (t == 0) jb.result[11] = (int64_t)((t_p - t_pack0) | ((wall_clock64() - t_p) << 16));
+#endif
     if (t == 0) {
         jb.result[DDM_DFIT_NODES] = n_nodes;
         jb.result[DDM_DFIT_PURE] = pure ? 1 : 0;

@@ -1,0 +1,28 @@
+"""Phase times of the device refit (instrumented build: tools/build_variant.sh dprof
+rf_device.hip -DDDM_DFIT_PROFILE, then DDM_AMD_LIB=.../libddm_amd_dprof.so): a C3-like
+drift batch (100 rows x 27 features, two classes), 8 jobs of 100 trees."""
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, "distributed-drift-detection_amd")
+from ddm_amd.dfit import DeviceTrainer  # noqa: E402
+
+rng = np.random.default_rng(3)
+batches = []
+for k in range(8):
+    y = np.where(np.arange(100) < 60, 3, 4)
+    X = rng.random((100, 27), dtype=np.float32) + (y[:, None] == 4) * 0.5
+    batches.append((X.astype(np.float32), y, rng.integers(0, 2**31 - 1, 100)))
+tr = DeviceTrainer(100, 16, torch.device("cuda", 0))
+for rep in range(3):
+    t = time.perf_counter()
+    out = tr.fit_many(batches)
+    dt = time.perf_counter() - t
+    r = out[0][3]
+    a, p = int(r[10]), int(r[11])
+    print(f"fit_many {dt*1e3:.2f} ms; tree 0: rng init {(a & 0xffff)/100:.1f} us, bootstrap {((a >> 16) & 0xffff)/100:.1f} us, "
+          f"build {(a >> 32)/100:.1f} us; pack: bfs {(p & 0xffff)/100:.1f} us, compile {((p >> 16) & 0xffff)/100:.1f} us; "
+          f"nodes {int(r[2])}, blob {int(r[5])}")
