@@ -51,7 +51,7 @@ __global__ __launch_bounds__(64) void k_scan_long(
     __shared__ uint4 sbytes[kLongChunkMax / 16 + 1];
     __shared__ uint64_t smask[kLongChunkMax / 64];
     __shared__ int2 sev[64];
-    __shared__ double s_n[64], s_r[64];
+    __shared__ double s_tile[kTileScratch];
     __shared__ uint32_t stk;
     const int lane = threadIdx.x;
     if (lane == 0) stk = atomicAdd(ticket, 1u);
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(64) void k_scan_long(
         uint64_t m = smask[tile] >> sh;
         if (sh && tile + 1 < ntiles) m |= smask[tile + 1] << (64 - sh);
         if (cnt < 64) m &= (1ull << cnt) - 1;
-        const TileOut to = wave_tile(d, m, cnt, min_inst, wl, cl, s_n, s_r);
+        const TileOut to = wave_tile(d, m, cnt, min_inst, wl, cl, s_tile);
         const int kc = to.kc, last = to.last;
         const uint64_t W_ = to.warn;
         if (kc < 0 && W_ == 0) {                               // no event in the tile

@@ -34,10 +34,13 @@ struct TileOut {
     uint64_t warn;   // rows with in_warning_zone set (committed rows only are meaningful)
 };
 
-// s_n, s_r: this wave's 64-double LDS scratch each.  d must be uniform over the wave and
-// not in a pending change (the caller resets it first); rows >= cnt are ignored.
+// sc: this wave's LDS scratch of kTileScratch doubles (n, RN(1/n), x and p of every row).
+// d must be uniform over the wave and not in a pending change (the caller resets it first);
+// rows >= cnt are ignored.
+constexpr int kTileScratch = 4 * 64;
+
 __device__ __forceinline__ TileOut wave_tile(Det& d, uint64_t m, int cnt, int min_inst, double wl, double cl,
-                                             double* s_n, double* s_r) {
+                                             double* sc) {
     const int lane = threadIdx.x & 63;
     if (cnt < 64) m &= (1ull << cnt) - 1;
     if (det_trivial(d) && m == 0) {                 // zeros in the trivial state: only n moves
@@ -45,20 +48,44 @@ __device__ __forceinline__ TileOut wave_tile(Det& d, uint64_t m, int cnt, int mi
         d.warn = 0;
         return {-1, cnt - 1, 0ull};
     }
+    double* const s_n = sc;
+    double* const s_r = sc + 64;
+    double* const s_x = sc + 128;
+    double* const s_p = sc + 192;
     const double nl = (double)d.n + (double)lane;   // divisor of row lane
     const double rl = 1.0 / nl;                     // RN(1/n), as det_add_fast's rcp[] / 1.0 / n
-    s_n[lane] = nl;
-    s_r[lane] = rl;
+    // rows past cnt get n = 1, 1/n = 0: their step adds exactly 0 to p
+    s_n[lane] = lane < cnt ? nl : 1.0;
+    s_r[lane] = lane < cnt ? rl : 0.0;
+    s_x[lane] = (double)((m >> lane) & 1ull);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double p = d.p, myp = 0.0;
-#pragma unroll 8
-    for (int k = 0; k < cnt; ++k) {
-        const double x = (double)((m >> k) & 1ull);
-        p = p + div_rn(x - p, s_n[k], s_r[k]);
-        myp = lane == k ? p : myp;
+    // the chain, 8 rows at a time: 5 dependent fp64 operations per row, the group's operands
+    // read from LDS (broadcast) ahead of it, its p values written back by one lane after it
+    double p = d.p;
+    for (int k0 = 0; k0 < cnt; k0 += 8) {
+        double xs[8], ns[8], rs[8], ps[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            xs[u] = s_x[k0 + u];
+            ns[u] = s_n[k0 + u];
+            rs[u] = s_r[k0 + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            p = p + div_rn(xs[u] - p, ns[u], rs[u]);
+            ps[u] = p;
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s_p[k0 + u] = ps[u];
+        }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const double myp = lane < cnt ? s_p[lane] : 0.0;
     const double s = sqrt_q(div_rn(myp * (1.0 - myp), nl, rl));
     const bool gated = lane < cnt && (d.n + lane + 1 >= (int64_t)min_inst);
     const double ps = myp + s;
