@@ -15,10 +15,10 @@
 //      its successor;
 //   3. k_scan_batches_exact<1>  level-1 rescans: the successor of each unchanged batch
 //      from that batch's end state (what it is if the unchanged batch itself was fresh);
-//   4. k_scan_batches_list / k_scan_batches_fix  the streams with an unchanged batch or a
-//      carried-in detector: each is walked batch by batch over the flag bytes; the level-1
-//      records resolve the common case, longer carried chains run wave-cooperatively
-//      (wave_det.h).
+//   4. k_scan_batches_walk / k_scan_batches_chain  every stream: a fresh carry-in and a change
+//      in every batch is final; the others are walked batch by batch over the flag bytes
+//      (one lane per stream), the level-1 records resolving the common case; longer
+//      carried chains run in the chain kernel, one wave per stream (wave_det.h).
 // Every decision is the exact fp64 recurrence of det.h; the results equal ddm_scan_streams
 // in mode 1 and the C oracle bit for bit.
 #include "common.h"
@@ -213,6 +213,7 @@ struct QEntry {
 };
 
 constexpr int kClsThreads = 256;
+constexpr int kLQ = 128;                        // per-wave LDS queue of batches needing exact rows
 constexpr int kClsLoads = 9;                    // (64 * kMaxBatch + 15) / 16 + 1 chunks <= 9 * 64
 constexpr int kClsWords = kClsLoads * 64 / 4;   // the LDS bit image in u64 words
 
@@ -273,10 +274,19 @@ __global__ __launch_bounds__(kClsThreads) void k_scan_batches_classify(
     const uint8_t* __restrict__ err, int64_t n_items, int64_t L, int64_t nb, int64_t nbp, ddm_params P,
     int2* __restrict__ ev, uint8_t* __restrict__ flags, const uint8_t* __restrict__ pmap, int64_t qcap,
     uint32_t* __restrict__ need, bool use_pre, const uint16_t* __restrict__ ptab, const double4* __restrict__ pst,
-    QEntry* __restrict__ q, uint32_t* __restrict__ qcnt) {
+    QEntry* __restrict__ q, uint32_t* __restrict__ qcnt, int64_t* __restrict__ q1, uint32_t* __restrict__ q1cnt,
+    double2* __restrict__ pend, int steps, int pop_min) {
     __shared__ uint64_t img[kClsThreads / 64][kClsWords + 2];
+    __shared__ uint64_t lq_m0[kClsThreads / 64][kLQ], lq_m1[kClsThreads / 64][kLQ];
+    __shared__ int64_t lq_it[kClsThreads / 64][kLQ];
+    __shared__ int32_t lq_hdr[kClsThreads / 64][kLQ];
+    __shared__ double rcp[kBatchRcp];
+    for (int k = threadIdx.x; k < kBatchRcp; k += kClsThreads) rcp[k] = 1.0 / (double)(k > 0 ? k : 1);
+    __syncthreads();
     const int pb = (int)P.per_batch;
-    const bool shortcuts = P.min_num_instances == 3;
+    const int min_inst = P.min_num_instances;
+    const double wl = P.warning_level, cl = P.out_control_level;
+    const bool shortcuts = min_inst == 3;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t below = (1ull << lane) - 1;
@@ -288,6 +298,104 @@ __global__ __launch_bounds__(kClsThreads) void k_scan_batches_classify(
     const double inv_nb = 1.0 / (double)nb;
     const int delta = (int)(nb * pb - L);            // rows missing from a stream's last batch
     uint32_t count = 0;
+    // exact rows inside this pass: the wave's LDS queue (ring) of batches that need them and
+    // one batch per busy lane (wave-uniform ring state; overflow goes to the global queue)
+    uint32_t lq_head = 0, lq_count = 0, nq = 0;
+    int64_t* const wq1 = q1 + wave * qcap;
+    bool busy = false, popping = false;
+    SmallDet d;
+    small_fresh(d);
+    int ei = 0, eblen = 0, ewp = -1, ehdr = 0;
+    uint64_t em0 = 0, em1 = 0;
+    int64_t eit = 0;
+    const auto step_rows = [&]() {
+        // two exact rows of this lane's batch (as k_scan_batches_exact); a finished batch
+        // writes its result
+        bool enq = false;
+        if (busy) {
+            const bool two = ei + 1 < eblen;
+            const int n0 = d.n;
+            const double nd0 = (double)n0, r0 = rcp[n0], nd1 = (double)(n0 + 1), r1 = rcp[n0 + 1];
+            const double p0 = d.p + div_rn((double)mask_bit(em0, em1, ei) - d.p, nd0, r0);
+            const double p1 = p0 + div_rn((double)(two ? mask_bit(em0, em1, ei + 1) : 0) - p0, nd1, r1);
+            const double s0 = sqrt_q(div_rn(p0 * (1.0 - p0), nd0, r0));
+            const double s1 = sqrt_q(div_rn(p1 * (1.0 - p1), nd1, r1));
+            int r = small_test(d, p0, s0, min_inst, wl, cl);
+            if (r == 1 && ewp < 0) ewp = ei;
+            ++ei;
+            if (r != 2 && two) {
+                r = small_test(d, p1, s1, min_inst, wl, cl);
+                if (r == 1 && ewp < 0) ewp = ei;
+                ++ei;
+            }
+            if (r == 2 || ei >= eblen) {
+                const bool chg = r == 2;
+                const int64_t es = item_stream(eit, nb, inv_nb);
+                const int64_t ej = eit - es * nb;
+                const int64_t eb = es * L + ej * pb;
+                int w = ewp, c = chg ? ei - 1 : -1;
+                if (kPmap) {
+                    if (w >= 0) w = pmap[eb + w];
+                    if (c >= 0) c = pmap[eb + c];
+                }
+                if (!chg) {
+                    double2* const e = pend + 3 * eit;
+                    e[0] = make_double2(d.p, d.s);
+                    e[1] = make_double2(d.pmin, d.smin);
+                    e[2] = make_double2(d.psmin, (double)(2 * d.n + (r == 1 ? 1 : 0)));
+                    need[es] = 1u;
+                    enq = ej + 1 < nb;
+                }
+                ev[eit] = make_int2(w, c);
+                flags[es * nbp + ej] = (uint8_t)((chg ? 1 : 0) | ((chg || w >= 0) ? 2 : 0) | (chg ? 0 : 4) |
+                                                 lead_bits(em0, em1));
+                busy = false;
+            }
+        }
+        const uint64_t qm = __ballot(enq);
+        if (enq) wq1[nq + __popcll(qm & below)] = eit;
+        nq += (uint32_t)__popcll(qm);
+    };
+    // idle lanes take queued batches (lane order); returns the prefix-table index to look up
+    const auto pop = [&]() -> uint32_t {
+        popping = false;
+        const uint64_t idle_m = __ballot(!busy);
+        const int nidle = __popcll(idle_m);
+        uint32_t ix = 0;
+        if (lq_count > 0 && (nidle >= pop_min || nidle == 64)) {
+            const uint32_t take = min((uint32_t)nidle, lq_count);
+            const uint32_t rank = (uint32_t)__popcll(idle_m & below);
+            if (!busy && rank < take) {
+                const uint32_t sl = (lq_head + rank) & (kLQ - 1);
+                em0 = lq_m0[wv][sl];
+                em1 = lq_m1[wv][sl];
+                eit = lq_it[wv][sl];
+                ehdr = lq_hdr[wv][sl];
+                popping = true;
+                ix = (uint32_t)(em0 & (uint64_t)(kPreN - 1));
+            }
+            lq_head = (lq_head + take) & (kLQ - 1);
+            lq_count -= take;
+        }
+        return ix;
+    };
+    // a popped batch's starting detector (after the prefix rows when hdr says so)
+    const auto start = [&](const double4& t) {
+        if (popping) {
+            busy = true;
+            popping = false;
+            ei = ehdr >> 8;
+            ewp = (ehdr & 255) - 1;
+            d.p = ei ? t.x : 1.0;
+            d.s = 0.0;
+            d.pmin = ei ? t.y : __builtin_huge_val();
+            d.smin = ei ? t.z : __builtin_huge_val();
+            d.psmin = ei ? t.w : __builtin_huge_val();
+            d.n = ei + 1;
+            const int64_t es = item_stream(eit, nb, inv_nb);
+            eblen = (int)min((int64_t)pb, L - (eit - es * nb) * pb);
+        }
+    };
     // software pipeline: the next fill's loads are issued before this fill's decisions
     // and stores, so every wave keeps a fill in flight
     FillGeo g = fill_geo(wave, n_items, L, nb, nbp, pb, delta, inv_nb, lane);
@@ -333,6 +441,8 @@ __global__ __launch_bounds__(kClsThreads) void k_scan_batches_classify(
         const uint32_t ix = (uint32_t)(m0 & (uint64_t)(kPreN - 1));
         const uint32_t inf = ptab[ix];
         const double4 pt = pst[ix];
+        const uint32_t pix = steps > 0 ? pop() : 0u;
+        const double4 ppt = pst[pix];
         // C: the next fill's loads (the last iteration reloads its own fill)
         const int64_t fn = f + n_waves;
         const FillGeo gn = fill_geo(min(fn, nfill - 1), n_items, L, nb, nbp, pb, delta, inv_nb, lane);
@@ -368,7 +478,23 @@ __global__ __launch_bounds__(kClsThreads) void k_scan_batches_classify(
                 flags[g.f0 + g.ln + g.w * (int)(nbp - nb)] = fl;
             }
         }
-        const uint64_t xm = __ballot(exact);
+        start(ppt);
+        uint64_t xm = __ballot(exact);
+        if (steps > 0 && xm) {
+            // into the LDS queue while it has room (the prefix state is looked up at the pop)
+            const uint32_t room = kLQ - lq_count;
+            const uint32_t r = (uint32_t)__popcll(xm & below);
+            if (exact && r < room) {
+                const uint32_t sl = (lq_head + lq_count + r) & (kLQ - 1);
+                lq_m0[wv][sl] = m0;
+                lq_m1[wv][sl] = m1;
+                lq_it[wv][sl] = g.base + g.ln;
+                lq_hdr[wv][sl] = (pre && blen > kPre) ? ((wp + 1) | (kPre << 8)) : 0;
+                exact = false;
+            }
+            lq_count += min((uint32_t)__popcll(xm), room);
+            xm = __ballot(exact);
+        }
         if (exact) {
             // the detector after the prefix rows (no change there) when the batch is longer
             QEntry e;
@@ -385,9 +511,26 @@ __global__ __launch_bounds__(kClsThreads) void k_scan_batches_classify(
             wq[count + __popcll(xm & below)] = e;
         }
         count += (uint32_t)__popcll(xm);
+        // E: exact rows of the queued batches
+        for (int k = 0; k < steps; ++k) {
+            if (__ballot(busy) == 0ull) break;
+            step_rows();
+        }
         g = gn;
     }
-    if (lane == 0) qcnt[wave] = count;
+    // drain the LDS queue
+    if (steps > 0) {
+        for (;;) {
+            const uint32_t pix = pop();
+            start(pst[pix]);
+            if (__ballot(busy) == 0ull && lq_count == 0) break;
+            step_rows();
+        }
+    }
+    if (lane == 0) {
+        qcnt[wave] = count;
+        q1cnt[wave] = nq;
+    }
 }
 
 // Timing probe (DDM_SCAN_PROBE=1, results are NOT the scan's): the classify pass's reads,
@@ -396,7 +539,7 @@ __global__ __launch_bounds__(kClsThreads) void k_scan_batches_classify(
 template <int kLoads>
 __global__ __launch_bounds__(kClsThreads) void k_scan_batches_probe(
     const uint8_t* __restrict__ err, int64_t n_items, int64_t L, int64_t nb, int64_t nbp, ddm_params P,
-    int2* __restrict__ ev, uint32_t* __restrict__ qcnt) {
+    int2* __restrict__ ev, uint32_t* __restrict__ qcnt, uint32_t* __restrict__ q1cnt) {
     __shared__ uint64_t img[kClsThreads / 64][kClsWords + 2];
     const int pb = (int)P.per_batch;
     const int lane = threadIdx.x & 63;
@@ -425,7 +568,7 @@ __global__ __launch_bounds__(kClsThreads) void k_scan_batches_probe(
         if (g.valid) ev[g.base + g.ln] = make_int2((int)(m0 ^ m1), (int)((m0 ^ m1) >> 32));
         g = gn;
     }
-    if (lane == 0) qcnt[wave] = 0;
+    if (lane == 0) qcnt[wave] = q1cnt[wave] = 0;
 }
 
 // 2./3. Exact rows, one lane per queued batch.  Lanes that finish take the next entries of
@@ -459,7 +602,8 @@ __global__ __launch_bounds__(kExThreads) void k_scan_batches_exact(
     const int64_t wq = wave * qcap;                 // this wave's queue slots
     const uint32_t n = kLevel == 0 ? qcnt[wave] : q1cnt[wave];
     const double inv_nb = 1.0 / (double)nb;
-    uint32_t head = 0, nq = 0;                      // wave-uniform
+    uint32_t head = 0;                              // wave-uniform
+    uint32_t nq = kLevel == 0 ? q1cnt[wave] : 0;    // after the classify pass's level-1 entries
     bool busy = false;
     int64_t it = 0, s = 0, j = 0, bstart = 0;
     int blen = 0, i = 0, wpos = -1;
@@ -572,66 +716,6 @@ __global__ __launch_bounds__(kExThreads) void k_scan_batches_exact(
         }
     }
     if (kLevel == 0 && lane == 0) q1cnt[wave] = nq;
-}
-
-// The fix-up list: streams with an unchanged batch (need[s]) or a carry-in that is not
-// fresh.  Every other stream's speculation is its result: the reset state (its last batch
-// changed) and nb batches with an event.  A thread looks at kListPer streams (coalesced,
-// 256 apart) and a block takes its list slots with ONE atomic.
-constexpr int kListPer = 8;
-
-__global__ __launch_bounds__(256) void k_scan_batches_list(int64_t n_streams, int64_t nb,
-                                                           ddm_state* __restrict__ state,
-                                                           const uint32_t* __restrict__ need,
-                                                           int64_t* __restrict__ nev_out, int32_t* __restrict__ list,
-                                                           uint32_t* __restrict__ ctr) {
-    __shared__ uint32_t wcount[4], wbase[4];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t below = (1ull << lane) - 1;
-    const int64_t t0 = (int64_t)blockIdx.x * 256 * kListPer + threadIdx.x;
-    uint32_t bits = 0, cnt = 0;
-#pragma unroll
-    for (int k = 0; k < kListPer; ++k) {
-        const int64_t t = t0 + (int64_t)k * 256;
-        bool fix = false;
-        if (t < n_streams) {
-            fix = need[t] != 0u || !state_fresh(state[t]);
-            if (!fix) {
-                if (nb > 0) {
-                    ddm_state st;
-                    st.miss_prob = 1.0;
-                    st.miss_std = 0.0;
-                    st.miss_prob_min = st.miss_sd_min = st.miss_prob_sd_min = __builtin_huge_val();
-                    st.sample_count = 1;
-                    st.in_concept_change = 0;
-                    st.in_warning_zone = 0;
-                    state[t] = st;
-                }
-                if (nev_out) nev_out[t] = nb;
-            }
-        }
-        bits |= (fix ? 1u : 0u) << k;
-        cnt += (uint32_t)__popcll(__ballot(fix));
-    }
-    if (lane == 0) wcount[wv] = cnt;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t total = wcount[0] + wcount[1] + wcount[2] + wcount[3];
-        uint32_t b = total ? atomicAdd(ctr, total) : 0u;
-        for (int w = 0; w < 4; ++w) {
-            wbase[w] = b;
-            b += wcount[w];
-        }
-    }
-    __syncthreads();
-    uint32_t off = wbase[wv];
-#pragma unroll
-    for (int k = 0; k < kListPer; ++k) {
-        const bool fix = (bits >> k) & 1u;
-        const uint64_t m = __ballot(fix);
-        if (fix) list[off + __popcll(m & below)] = (int32_t)(t0 + (int64_t)k * 256);
-        off += (uint32_t)__popcll(m);
-    }
 }
 
 __device__ __forceinline__ void load_det(Det& d, const ddm_state& st) {
@@ -820,48 +904,73 @@ struct FixEntry {
 constexpr int kWalkThreads = 256;
 
 __global__ __launch_bounds__(kWalkThreads) void k_scan_batches_walk(
-    int64_t L, int64_t nb, int64_t nbp, ddm_params P, ddm_state* __restrict__ state, int2* __restrict__ ev,
-    const uint8_t* __restrict__ flags, int64_t* __restrict__ nev_out, const uint8_t* __restrict__ pmap,
-    const int32_t* __restrict__ list, uint32_t* __restrict__ ctr, const double2* __restrict__ pend,
-    const int2* __restrict__ ev1, const uint8_t* __restrict__ flags1, const double2* __restrict__ pend1,
-    FixEntry* __restrict__ coop) {
+    int64_t n_streams, int64_t L, int64_t nb, int64_t nbp, ddm_params P, ddm_state* __restrict__ state,
+    int2* __restrict__ ev, const uint8_t* __restrict__ flags, int64_t* __restrict__ nev_out,
+    const uint8_t* __restrict__ pmap, const uint32_t* __restrict__ need, uint32_t* __restrict__ ctr,
+    const double2* __restrict__ pend, const int2* __restrict__ ev1, const uint8_t* __restrict__ flags1,
+    const double2* __restrict__ pend1, FixEntry* __restrict__ coop) {
     const int64_t pb = P.per_batch;
     const bool shortcuts = P.min_num_instances == 3;
     const int lane = threadIdx.x & 63;
     const uint64_t below = (1ull << lane) - 1;
-    const uint32_t n_list = __atomic_load_n(ctr, __ATOMIC_RELAXED);
-    const uint32_t stride = gridDim.x * kWalkThreads;
-    for (uint32_t k0 = blockIdx.x * kWalkThreads + (threadIdx.x & ~63u); k0 < n_list; k0 += stride) {
-        const uint32_t k = k0 + lane;
-        bool defer = false;
-        Walk W;
-        if (k < n_list) {
-            W.sid = list[k];
-            load_det(W.d, state[W.sid]);
-            W.j = W.wbase = W.nev = 0;
-            W.chg_m = nb > 0 ? change_window(flags + W.sid * nbp, 0, nb, W.st_m, W.ev_m, W.lm) : 0;
-            walk_open(W, L, nb, nbp, pb, shortcuts, ev, flags, pmap, pend, ev1, flags1, pend1);
-            if (W.j >= nb) {
-                state[W.sid] = store_det(W.d);
-                if (nev_out) nev_out[W.sid] = W.nev;
-            } else {
-                defer = true;
+    __shared__ int32_t s_list[kWalkThreads];
+    __shared__ uint32_t s_cnt;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    const int64_t t = (int64_t)blockIdx.x * kWalkThreads + threadIdx.x;
+    if (t < n_streams) {
+        const ddm_state st = state[t];
+        if (need[t] == 0u && state_fresh(st)) {
+            // a fresh carry-in and a change in every batch: the speculation is the result,
+            // the reset state and nb batches with an event
+            if (nb > 0) {
+                ddm_state f;
+                f.miss_prob = 1.0;
+                f.miss_std = 0.0;
+                f.miss_prob_min = f.miss_sd_min = f.miss_prob_sd_min = __builtin_huge_val();
+                f.sample_count = 1;
+                f.in_concept_change = 0;
+                f.in_warning_zone = 0;
+                state[t] = f;
             }
+            if (nev_out) nev_out[t] = nb;
+        } else {
+            s_list[atomicAdd(&s_cnt, 1u)] = (int32_t)(t - (int64_t)blockIdx.x * kWalkThreads);
         }
-        const uint64_t dm = __ballot(defer);
-        if (dm) {
-            uint32_t base = 0;
-            const int lead = __builtin_ctzll(dm);
-            if (lane == lead) base = atomicAdd(ctr + 2, (uint32_t)__popcll(dm));
-            base = __shfl(base, lead);
-            if (defer) {
-                FixEntry e;
-                e.d = W.d;
-                e.sid = W.sid;
-                e.j = W.j;
-                e.nev = W.nev;
-                coop[base + __popcll(dm & below)] = e;
-            }
+    }
+    __syncthreads();
+    // the block's other streams, packed onto its first lanes
+    const uint32_t cnt = s_cnt;
+    if ((threadIdx.x & ~63u) >= cnt) return;
+    bool defer = false;
+    Walk W;
+    if (threadIdx.x < cnt) {
+        const int64_t u = (int64_t)blockIdx.x * kWalkThreads + s_list[threadIdx.x];
+        W.sid = u;
+        load_det(W.d, state[u]);
+        W.j = W.wbase = W.nev = 0;
+        W.chg_m = nb > 0 ? change_window(flags + u * nbp, 0, nb, W.st_m, W.ev_m, W.lm) : 0;
+        walk_open(W, L, nb, nbp, pb, shortcuts, ev, flags, pmap, pend, ev1, flags1, pend1);
+        if (W.j >= nb) {
+            state[u] = store_det(W.d);
+            if (nev_out) nev_out[u] = W.nev;
+        } else {
+            defer = true;
+        }
+    }
+    const uint64_t dm = __ballot(defer);
+    if (dm) {
+        uint32_t base = 0;
+        const int lead = __builtin_ctzll(dm);
+        if (lane == lead) base = atomicAdd(ctr + 2, (uint32_t)__popcll(dm));
+        base = __shfl(base, lead);
+        if (defer) {
+            FixEntry e;
+            e.d = W.d;
+            e.sid = W.sid;
+            e.j = W.j;
+            e.nev = W.nev;
+            coop[base + __popcll(dm & below)] = e;
         }
     }
 }
@@ -972,9 +1081,8 @@ __global__ __launch_bounds__(kChainThreads) void k_scan_batches_chain(
 constexpr int64_t kMaxWaves = 1 << 14;
 
 struct BatchScratch {
-    uint32_t* ctr;      // [0] list length, [2] fix-up entries, [3] fix-up claim cursor
+    uint32_t* ctr;      // [2] streams handed to the chain kernel
     uint32_t* need;     // [n_streams]
-    int32_t* list;      // [n_streams]
     FixEntry* coop;     // [n_streams] streams the walker hands to the fix-up kernel
     uint8_t* flags;     // [n_streams * nbp], 64-byte aligned rows
     uint8_t* flags1;    // [n_items]
@@ -1000,7 +1108,7 @@ BatchScratch batch_scratch(void* base, int64_t n_streams, int64_t nb) {
         o += up(bytes);
         return at;
     };
-    const int64_t o_need = take(4 * n_streams), o_list = take(4 * n_streams), o_flags = take(n_streams * nbp);
+    const int64_t o_need = take(4 * n_streams), o_flags = take(n_streams * nbp);
     const int64_t o_coop = take((int64_t)sizeof(FixEntry) * n_streams);
     const int64_t o_flags1 = take(n_items), o_ev1 = take(8 * n_items), o_pend = take(48 * n_items);
     const int64_t o_pend1 = take(48 * n_items), o_q = take((int64_t)sizeof(QEntry) * nq), o_q1 = take(8 * nq);
@@ -1010,7 +1118,6 @@ BatchScratch batch_scratch(void* base, int64_t n_streams, int64_t nb) {
     BatchScratch sc;
     sc.ctr = reinterpret_cast<uint32_t*>(b);
     sc.need = reinterpret_cast<uint32_t*>(b + o_need);
-    sc.list = reinterpret_cast<int32_t*>(b + o_list);
     sc.coop = reinterpret_cast<FixEntry*>(b + o_coop);
     sc.flags = b + o_flags;
     sc.flags1 = b + o_flags1;
@@ -1075,6 +1182,8 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
     static const int ex_refill = std::max(1, std::min(64, env_int("DDM_EXACT_REFILL", 24)));
     static const int fix_blocks_max = env_int("DDM_FIX_BLOCKS", 1024);
     static const bool use_pre = env_int("DDM_SCAN_PRE", 1) != 0;
+    static const int cls_steps = std::max(0, env_int("DDM_SCAN_STEPS", 2));
+    static const int cls_pop = std::max(1, std::min(64, env_int("DDM_SCAN_POP", 16)));
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
     if (int rc = ddm::hip_status(hipMemsetAsync(scratch, 0, (size_t)(256 + ((4 * n_streams + 255) & ~255)), s),
@@ -1098,11 +1207,11 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
         static const bool probe = env_int("DDM_SCAN_PROBE", 0) != 0;
         if (probe)
             hipLaunchKernelGGL(k_scan_batches_probe<7>, dim3((unsigned)blocks), dim3(kClsThreads), 0, s, err, n_items,
-                               stream_len, nb, nbp, *prm, ev, sc.qcnt);
+                               stream_len, nb, nbp, *prm, ev, sc.qcnt, sc.q1cnt);
         else
             hipLaunchKernelGGL(cls, dim3((unsigned)blocks), dim3(kClsThreads), 0, s, err, n_items, stream_len, nb,
                                nbp, *prm, ev, sc.flags, perm_map, qcap, sc.need, pre, sc.ptab, sc.pst, sc.q,
-                               sc.qcnt);
+                               sc.qcnt, sc.q1, sc.q1cnt, sc.pend, cls_steps, cls_pop);
         if (int rc = ddm::launch_status("ddm_scan_batches/classify")) return rc;
         const auto ex0 = perm_map ? k_scan_batches_exact<0, true> : k_scan_batches_exact<0, false>;
         const auto ex1 = perm_map ? k_scan_batches_exact<1, true> : k_scan_batches_exact<1, false>;
@@ -1115,15 +1224,12 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
                            sc.pend, sc.ev1, sc.flags1, sc.pend1, ex_refill);
         if (int rc = ddm::launch_status("ddm_scan_batches/exact1")) return rc;
     }
-    hipLaunchKernelGGL(k_scan_batches_list, dim3((unsigned)ddm::ceil_div(n_streams, 256 * kListPer)), dim3(256), 0, s,
-                       n_streams, nb, state_io, sc.need, nev_out, sc.list, sc.ctr);
+    hipLaunchKernelGGL(k_scan_batches_walk, dim3((unsigned)ddm::ceil_div(n_streams, kWalkThreads)), dim3(kWalkThreads),
+                       0, s, n_streams, stream_len, nb, nbp, *prm, state_io, reinterpret_cast<int2*>(ev_out),
+                       sc.flags, nev_out, perm_map, sc.need, sc.ctr, sc.pend, sc.ev1, sc.flags1, sc.pend1, sc.coop);
+    if (int rc = ddm::launch_status("ddm_scan_batches/walk")) return rc;
     const int64_t fix_blocks =
         std::max<int64_t>(1, std::min<int64_t>(fix_blocks_max, ddm::ceil_div(n_streams, kChainThreads / 64)));
-    const int64_t walk_blocks = std::max<int64_t>(1, std::min<int64_t>(4096, ddm::ceil_div(n_streams, kWalkThreads)));
-    hipLaunchKernelGGL(k_scan_batches_walk, dim3((unsigned)walk_blocks), dim3(kWalkThreads), 0, s, stream_len, nb, nbp,
-                       *prm, state_io, reinterpret_cast<int2*>(ev_out), sc.flags, nev_out, perm_map, sc.list, sc.ctr,
-                       sc.pend, sc.ev1, sc.flags1, sc.pend1, sc.coop);
-    if (int rc = ddm::launch_status("ddm_scan_batches/walk")) return rc;
     hipLaunchKernelGGL(k_scan_batches_chain, dim3((unsigned)fix_blocks), dim3(kChainThreads), 0, s, err, stream_len,
                        nb, nbp, *prm, state_io, reinterpret_cast<int2*>(ev_out), sc.flags, nev_out, perm_map,
                        sc.coop, sc.ctr, sc.pend, sc.ev1, sc.flags1, sc.pend1);
