@@ -258,13 +258,13 @@ __device__ __forceinline__ FillGeo fill_geo(int64_t f, int64_t n_items, int64_t 
 
 // The fill's chunks, one coalesced 16-byte load per k, issued back to back (chunks past the
 // fill repeat its last one: no branch between them).
-template <int kLoads>
+template <int kLoads, bool kNt = true>
 __device__ __forceinline__ void fill_load(const uint8_t* __restrict__ err, const FillGeo& g, int lane,
                                           uint4 (&v)[kLoads]) {
 #pragma unroll
     for (int k = 0; k < kLoads; ++k) {
-        const u32x4 t = __builtin_nontemporal_load(
-            reinterpret_cast<const u32x4*>(err + g.a0 + 16 * min(k * 64 + lane, g.nch - 1)));
+        const u32x4* a = reinterpret_cast<const u32x4*>(err + g.a0 + 16 * min(k * 64 + lane, g.nch - 1));
+        const u32x4 t = kNt ? __builtin_nontemporal_load(a) : *a;
         v[k] = make_uint4(t.x, t.y, t.z, t.w);
     }
 }
@@ -536,10 +536,13 @@ __global__ __launch_bounds__(kClsThreads) void k_scan_batches_classify(
 // Timing probe (DDM_SCAN_PROBE=1, results are NOT the scan's): the classify pass's reads,
 // LDS image and bit extraction with one 8-byte store per batch and nothing else, to price
 // its decision and queue work against the pure stream.
-template <int kLoads>
+template <int kLoads, int kMode>
 __global__ __launch_bounds__(kClsThreads) void k_scan_batches_probe(
     const uint8_t* __restrict__ err, int64_t n_items, int64_t L, int64_t nb, int64_t nbp, ddm_params P,
     int2* __restrict__ ev, uint32_t* __restrict__ qcnt, uint32_t* __restrict__ q1cnt) {
+    // kMode 0: as the classify pass (non-temporal loads, one fill ahead); 1: plain loads;
+    // 2: two fills ahead
+    constexpr bool kNt = kMode != 1;
     __shared__ uint64_t img[kClsThreads / 64][kClsWords + 2];
     const int pb = (int)P.per_batch;
     const int lane = threadIdx.x & 63;
@@ -551,8 +554,12 @@ __global__ __launch_bounds__(kClsThreads) void k_scan_batches_probe(
     const double inv_nb = 1.0 / (double)nb;
     const int delta = (int)(nb * pb - L);
     FillGeo g = fill_geo(wave, n_items, L, nb, nbp, pb, delta, inv_nb, lane);
-    uint4 v[kLoads];
-    if (wave < nfill) fill_load<kLoads>(err, g, lane, v);
+    FillGeo g2 = fill_geo(min(wave + n_waves, nfill - 1), n_items, L, nb, nbp, pb, delta, inv_nb, lane);
+    uint4 v[kLoads], v2[kLoads];
+    if (wave < nfill) {
+        fill_load<kLoads, kNt>(err, g, lane, v);
+        if (kMode == 2) fill_load<kLoads, kNt>(err, g2, lane, v2);
+    }
     for (int64_t f = wave; f < nfill; f += n_waves) {
 #pragma unroll
         for (int k = 0; k < kLoads; ++k) img16[k * 64 + lane] = (uint16_t)fold16(v[k]);
@@ -562,9 +569,19 @@ __global__ __launch_bounds__(kClsThreads) void k_scan_batches_probe(
         wave_sync_lds();
         const uint64_t m0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
         const uint64_t m1 = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
-        const int64_t fn = f + n_waves;
-        const FillGeo gn = fill_geo(min(fn, nfill - 1), n_items, L, nb, nbp, pb, delta, inv_nb, lane);
-        fill_load<kLoads>(err, gn, lane, v);
+        FillGeo gn;
+        if (kMode == 2) {
+#pragma unroll
+            for (int k = 0; k < kLoads; ++k) v[k] = v2[k];
+            gn = g2;
+            const int64_t f3 = f + 2 * n_waves;
+            g2 = fill_geo(min(f3, nfill - 1), n_items, L, nb, nbp, pb, delta, inv_nb, lane);
+            fill_load<kLoads, kNt>(err, g2, lane, v2);
+        } else {
+            const int64_t fn = f + n_waves;
+            gn = fill_geo(min(fn, nfill - 1), n_items, L, nb, nbp, pb, delta, inv_nb, lane);
+            fill_load<kLoads, kNt>(err, gn, lane, v);
+        }
         if (g.valid) ev[g.base + g.ln] = make_int2((int)(m0 ^ m1), (int)((m0 ^ m1) >> 32));
         g = gn;
     }
@@ -1206,8 +1223,13 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
                                   : (small ? k_scan_batches_classify<false, 7> : k_scan_batches_classify<false, kClsLoads>);
         static const bool probe = env_int("DDM_SCAN_PROBE", 0) != 0;
         if (probe)
-            hipLaunchKernelGGL(k_scan_batches_probe<7>, dim3((unsigned)blocks), dim3(kClsThreads), 0, s, err, n_items,
-                               stream_len, nb, nbp, *prm, ev, sc.qcnt, sc.q1cnt);
+        {
+            static const int pm = env_int("DDM_SCAN_PROBE", 0);
+            const auto pk = pm == 2 ? k_scan_batches_probe<7, 1>
+                          : pm == 3 ? k_scan_batches_probe<7, 2> : k_scan_batches_probe<7, 0>;
+            hipLaunchKernelGGL(pk, dim3((unsigned)blocks), dim3(kClsThreads), 0, s, err, n_items, stream_len, nb, nbp,
+                               *prm, ev, sc.qcnt, sc.q1cnt);
+        }
         else
             hipLaunchKernelGGL(cls, dim3((unsigned)blocks), dim3(kClsThreads), 0, s, err, n_items, stream_len, nb,
                                nbp, *prm, ev, sc.flags, perm_map, qcap, sc.need, pre, sc.ptab, sc.pst, sc.q,
