@@ -292,6 +292,9 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     ref_events = {g: r.copy() for g, r in results.items()}
     runner.stats = RunStats()
     gather_s[0] = 0.0
+    # the timed steps enqueue no timing events; the kernel times come from one instrumented
+    # step after them
+    runner.set_kernel_timing(False)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -308,6 +311,18 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     for g, r in results.items():          # every step reproduces the same events
         if args.warmup and not np.array_equal(r, ref_events[g]):
             raise RuntimeError(f"partition {g}: events differ between steps")
+    st_timed = runner.stats
+    runner.stats = RunStats()
+    runner.set_kernel_timing(True)
+    log = runner.predict_log
+    runner.predict_log = None
+    step()                                # instrumented, not timed
+    st_kern = runner.stats
+    runner.stats = st_timed
+    runner.predict_log = log
+    for g, r in results.items():
+        if not np.array_equal(r, ref_events.get(g, r)):
+            raise RuntimeError(f"partition {g}: events differ in the instrumented step")
     checks = {}
     if kind == "c3":
         c3_property_check(results, n, instances, block)
@@ -321,8 +336,12 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     if all_events is not None:
         checks["events_sha1"] = events_digest(all_events)
     st = runner.stats
-    agg = {k: getattr(st, k) for k in ("epochs", "refits", "predicted_rows", "predict_ms", "predict_bytes", "scan_ms",
-                                       "shuffle_ms", "host_s", "gpu_s", "dfit_ms", "device_refits", "prep_s")}
+    agg = {k: getattr(st, k) for k in ("epochs", "refits", "predicted_rows", "predict_bytes", "host_s", "gpu_s",
+                                       "device_refits", "prep_s")}
+    # kernel times of one step (the instrumented one), scaled to the timed steps
+    for k in ("predict_ms", "scan_ms", "shuffle_ms", "dfit_ms"):
+        agg[k] = getattr(st_kern, k) * args.steps
+    agg["predict_bytes"] = st_kern.predict_bytes * args.steps
     drifts = int(sum((r[:, 1] >= 0).sum() for r in results.values()))
     warns = int(sum((r[:, 0] >= 0).sum() for r in results.values()))
     rows_rank = n * len(parts) * args.steps
@@ -362,6 +381,7 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
              "device_refit_kernels_ms_per_step": agg["dfit_ms"] / args.steps,
              "host_s_per_step": agg["host_s"] / args.steps, "gpu_wait_s_per_step": agg["gpu_s"] / args.steps,
              "stream_prep_s_per_step": agg["prep_s"] / args.steps,
+             "kernel_ms_from": "one instrumented step after the timed ones (HIP events around each launch)",
              "gather_ms_per_step": gather_s[0] / args.steps * 1e3 if world > 1 else None,
              "gather_backend": (None if world == 1 else "rccl (ctypes ncclAllGather, HBM to HBM)" if args.comm
                                 else "torch.distributed all_gather"),

@@ -883,6 +883,20 @@ class BatchRunner:
                     E.ev[2 * k], E.ev[2 * k + 1] = t.ev[0].value, t.ev[1].value
         return E
 
+    def set_kernel_timing(self, on):
+        """HIP events around the epoch's launches (the kernel-time statistics) on or off.  Off,
+        an epoch enqueues ten fewer HIP calls; the bench times its steps that way and takes
+        the kernel times from an instrumented step of its own."""
+        if not self.timing:
+            return
+        if not hasattr(self, "_timers"):
+            self._timers = (self.t_shuf, self.t_pred, self.t_scan, self.t_long, self.t_fit)
+        ts = self._timers if on else (None,) * 5
+        self.t_shuf, self.t_pred, self.t_scan, self.t_long, self.t_fit = ts
+        for k, t in enumerate(ts):
+            self._E.ev[2 * k] = t.ev[0].value if t is not None else None
+            self._E.ev[2 * k + 1] = t.ev[1].value if t is not None else None
+
     def _next_bound(self, ps):
         """The largest window the epoch after this one can give partition ps (the policy of
         _epoch_after: 9/8 of the concept just closed after a change, twice the window
@@ -1132,7 +1146,7 @@ class BatchRunner:
         """Everything after an epoch's read-back: timings, events, RNG positions, the next
         windows."""
         s, stream = self.s, self.stream
-        if self.timing:
+        if self.timing and self.t_pred is not None:
             st.predict_ms += self.t_pred.elapsed_ms()
             st.scan_ms += self.t_scan.elapsed_ms()
             if long_rows:
@@ -1286,6 +1300,10 @@ class GroupedRunner:
             for k in RunStats.__slots__:
                 setattr(agg, k, getattr(agg, k) + getattr(r.stats, k))
         return agg
+
+    def set_kernel_timing(self, on):
+        for r in self.runners:
+            r.set_kernel_timing(on)
 
     @stats.setter
     def stats(self, value):

@@ -1,0 +1,30 @@
+"""One long mode-1 stream on the GPU: segments scanned by ddm_scan_batches and the carries
+resolved (ddm_amd/longstream.py) == the C oracle's sequential scan of the whole stream."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import oracle_scan_c
+from test_longstream import long_stream
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n,seg_batches", [(2_000_000, 64), (1_234_567, 16)])
+def test_device_segments_equal_oracle(oracle_lib, n, seg_batches):
+    from ddm_amd import kernels
+    from ddm_amd.longstream import DeviceScanner, scan_long_stream
+    err = long_stream(n % 1000, n)
+    dev = torch.device("cuda", 0)
+    pad = np.zeros(((n + 15) // 16) * 16 + 16, np.uint8)
+    pad[:n] = err
+    e = torch.from_numpy(pad).to(dev)
+    ev, end, first = scan_long_stream(DeviceScanner(e, kernels.params_struct()), n, 100, seg_batches=seg_batches)
+    oev, _, ost, _ = oracle_scan_c(oracle_lib, err, np.array([0, n], dtype=np.int64), mode=1)
+    assert np.array_equal(ev, oev)
+    got = np.array([end["miss_prob"], end["miss_std"], end["miss_prob_min"], end["miss_sd_min"],
+                    end["miss_prob_sd_min"], end["sample_count"], end["in_concept_change"], end["in_warning_zone"]],
+                   dtype=np.float64)
+    np.testing.assert_array_equal(got, ost[0])
+    hit = np.nonzero(oev[:, 1] >= 0)[0]
+    assert first == (int(hit[0]) if len(hit) else -1)
