@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 12
+#define DDM_AMD_ABI_VERSION 13
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -239,12 +239,14 @@ int ddm_scan_streams(const uint8_t* err, const int64_t* stream_off, int64_t n_st
  * Replaces the per-row DDM loop of run_DDM (DDM_Process.py:135-159) for DDM-only
  * streams (SURVEY.md §8 a4/a5, configs[3]); results are those of ddm_scan_streams in
  * mode 1 with offsets s*stream_len and batch_base s*nb, nb = ceil(stream_len/per_batch).
- * Batch-parallel: every batch is scanned speculatively with a fresh detector, then one
- * lane per stream rescans the batches whose carry-in was not fresh.
- * per_batch must be 1..128.  ev_out: int32 [n_streams*nb][2] (every entry written);
- * nev_out (may be NULL): batches with an event per stream; scratch: device memory of
- * ddm_scan_batches_scratch_bytes(...) bytes, 256-byte aligned (n_streams < 2^31);
- * perm_map: as for ddm_scan_streams. */
+ * Batch-parallel (csrc/scan_batches.hip): every batch is scanned speculatively with a
+ * fresh detector, then each stream is walked over its batches' flags and the batches whose
+ * carry-in was not fresh are rescanned with the carried detector.
+ * per_batch must be 1..128, n_streams and stream_len < 2^31 (ABI 13).  ev_out: int32
+ * [n_streams*nb][2] (every entry written); nev_out (may be NULL): batches with an event per
+ * stream; scratch: device memory of ddm_scan_batches_scratch_bytes(...) bytes, 256-byte
+ * aligned (about 140 bytes per batch: speculative records, queues, end states);
+ * perm_map: as for ddm_scan_streams.  err must be 16-byte aligned. */
 int64_t ddm_scan_batches_scratch_bytes(int64_t n_streams, int64_t stream_len, int32_t per_batch);
 int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t stream_len, const ddm_params* prm,
                      ddm_state* state_io, int32_t* ev_out, int64_t* nev_out, void* scratch,
