@@ -214,6 +214,10 @@ struct QEntry {
 
 constexpr int kClsThreads = 256;
 constexpr int kLQ = 128;                        // per-wave LDS queue of batches needing exact rows
+#ifndef DDM_CLS_WAVES
+#define DDM_CLS_WAVES 4
+#endif
+constexpr int kClsWavesPerEU = DDM_CLS_WAVES;   // occupancy target of the classify pass
 constexpr int kClsLoads = 9;                    // (64 * kMaxBatch + 15) / 16 + 1 chunks <= 9 * 64
 constexpr int kClsWords = kClsLoads * 64 / 4;   // the LDS bit image in u64 words
 
@@ -270,7 +274,7 @@ __device__ __forceinline__ void fill_load(const uint8_t* __restrict__ err, const
 }
 
 template <bool kPmap, int kLoads>
-__global__ __launch_bounds__(kClsThreads) void k_scan_batches_classify(
+__global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kClsWavesPerEU))) void k_scan_batches_classify(
     const uint8_t* __restrict__ err, int64_t n_items, int64_t L, int64_t nb, int64_t nbp, ddm_params P,
     int2* __restrict__ ev, uint8_t* __restrict__ flags, const uint8_t* __restrict__ pmap, int64_t qcap,
     uint32_t* __restrict__ need, bool use_pre, const uint16_t* __restrict__ ptab, const double4* __restrict__ pst,
