@@ -21,10 +21,27 @@ __device__ __forceinline__ double shfl_d(double v, int src) {
     return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
-__device__ __forceinline__ double shfl_up_d(double v, int d) {
+// One step of the wave's inclusive arg-min scan of (value, index) through DPP: the pair
+// from the lane kCtrl names (row_shr:n, or row_bcast:15/31 into the rows of kRowMask) is
+// taken when it is valid and strictly smaller (ties keep the later row: the reference's
+// `<=` minimum).  Lanes without a source get the identity (+inf, -1).
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void argmin_step(double& v, int& idx) {
     const long long b = __double_as_longlong(v);
-    const int lo = __shfl_up((int)b, d, 64);
-    const int hi = __shfl_up((int)(b >> 32), d, 64);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, kCtrl, kRowMask, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0x7ff00000, (int)(b >> 32), kCtrl, kRowMask, 0xF, false);
+    const int oi = __builtin_amdgcn_update_dpp(-1, idx, kCtrl, kRowMask, 0xF, false);
+    const double ov = __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+    if (oi >= 0 && (idx < 0 || !(v <= ov))) {
+        v = ov;
+        idx = oi;
+    }
+}
+
+__device__ __forceinline__ double readlane_d(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, src);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
     return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
@@ -91,15 +108,13 @@ __device__ __forceinline__ TileOut wave_tile(Det& d, uint64_t m, int cnt, int mi
     const double ps = myp + s;
     double mps = gated ? ps : __builtin_huge_val();
     int midx = gated ? lane : -1;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const double ops = shfl_up_d(mps, o);
-        const int oidx = __shfl_up(midx, o, 64);
-        if (lane >= o && oidx >= 0 && (midx < 0 || !(mps <= ops))) {
-            mps = ops;
-            midx = oidx;
-        }
-    }
+    // inclusive arg-min scan: rows of 16 by row_shr 1/2/4/8, then across rows by row_bcast
+    argmin_step<0x111, 0xF>(mps, midx);
+    argmin_step<0x112, 0xF>(mps, midx);
+    argmin_step<0x114, 0xF>(mps, midx);
+    argmin_step<0x118, 0xF>(mps, midx);
+    argmin_step<0x142, 0xA>(mps, midx);
+    argmin_step<0x143, 0xC>(mps, midx);
     const bool from_lane = midx >= 0 && mps <= d.psmin;
     const int src = midx >= 0 ? midx : 0;
     const double lp = shfl_d(myp, src), ls = shfl_d(s, src);
@@ -109,12 +124,12 @@ __device__ __forceinline__ TileOut wave_tile(Det& d, uint64_t m, int cnt, int mi
     const bool wrn = gated && !chg && ps > pm + wl * sm;
     const uint64_t C = __ballot(chg), W = __ballot(wrn);
     const int kc = C ? __builtin_ctzll(C) : -1;
-    const int last = kc >= 0 ? kc : cnt - 1;
-    d.p = shfl_d(myp, last);
-    d.s = shfl_d(s, last);
-    d.pmin = shfl_d(pm, last);
-    d.smin = shfl_d(sm, last);
-    d.psmin = shfl_d(psm, last);
+    const int last = __builtin_amdgcn_readfirstlane(kc >= 0 ? kc : cnt - 1);
+    d.p = readlane_d(myp, last);
+    d.s = readlane_d(s, last);
+    d.pmin = readlane_d(pm, last);
+    d.smin = readlane_d(sm, last);
+    d.psmin = readlane_d(psm, last);
     d.n += last + 1;
     d.chg = kc >= 0;
     d.warn = (int)((W >> last) & 1ull);

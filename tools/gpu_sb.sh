@@ -5,7 +5,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_scan_batches.py tests/test_gpu_scan_long.py -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_sb.log 2>&1 || { tail -40 gpurun_out/pytest_sb.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_scan_batches.py tests/test_gpu_scan_long.py tests/test_gpu_scan.py tests/test_gpu_longstream.py -x -q -s --timeout 200 --timeout-method thread > gpurun_out/pytest_sb.log 2>&1 || { tail -40 gpurun_out/pytest_sb.log; exit 1; }
 tail -1 gpurun_out/pytest_sb.log
 for cfg in "$@"; do
   [ "$cfg" = "-" ] && cfg=DDM_X=0
