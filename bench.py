@@ -542,8 +542,8 @@ def run_c4(args, world, rank, dev, torch, dist, cpu):
                                    "note": "straightforward form ~45 fp64 VALU instructions per scanned row "
                                            "(SURVEY §8d); the batch-parallel form skips most rows"},
                 "note": "one ddm_scan_batches call: k_scan_prefix_table + k_scan_batches_classify + "
-                        "k_scan_batches_exact<0> + k_scan_batches_exact<1> + k_scan_batches_list + "
-                        "k_scan_batches_fix; HIP events around the call"}
+                        "k_scan_batches_exact<0> + k_scan_batches_exact<1> + k_scan_batches_walk + "
+                        "k_scan_batches_chain; HIP events around the call"}
     return rows, elapsed, info, extra, roofline, cpu_res, "weak"
 
 

@@ -182,15 +182,27 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
         jb.info_out[3] = d;
     }
     const int F = jb.n_features;
-    for (int e = t; e < L * F; e += kStageThreads) {
-        const int kk = e / F, f = e % F;
-        const int64_t row = d * jb.pb + jb.perm[jb.base + d * jb.pb + kk];
-        jb.x_out[e] = jb.X[(int64_t)f * jb.ld + row];
+    // the batch's shuffle offsets once through LDS, then every thread's loads issued before
+    // its stores (the pointers may alias as far as the compiler knows: a store between two
+    // loads would keep the next load from being issued early)
+    __shared__ uint8_t off_d[256];
+    for (int kk = t; kk < L; kk += kStageThreads) off_d[kk] = jb.perm[jb.base + d * jb.pb + kk];
+    __syncthreads();
+    const int64_t row0 = d * jb.pb;
+    for (int e0 = t; e0 < L * F; e0 += 4 * kStageThreads) {
+        float xv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = e0 + u * kStageThreads;
+            xv[u] = e < L * F ? jb.X[(int64_t)(e % F) * jb.ld + row0 + off_d[e / F]] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = e0 + u * kStageThreads;
+            if (e < L * F) jb.x_out[e] = xv[u];
+        }
     }
-    for (int kk = t; kk < L; kk += kStageThreads) {
-        const int64_t row = d * jb.pb + jb.perm[jb.base + d * jb.pb + kk];
-        jb.y_out[kk] = jb.y[row];
-    }
+    for (int kk = t; kk < L; kk += kStageThreads) jb.y_out[kk] = jb.y[row0 + off_d[kk]];
     if (jb.R)
         for (int w = t; w < jb.n_words; w += kStageThreads) jb.w_out[w] = jb.R[P + w];
     // ---- batch j = d + 1: its shuffle, then the refit's tree seeds
@@ -224,7 +236,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
                 const uint64_t b = __ballot(v <= (uint32_t)i);
                 if (b) {
                     const int f = __builtin_ctzll(b);
-                    const int jv = __shfl((int)v, f, 64);
+                    const int jv = __builtin_amdgcn_readlane((int)v, f);   // f is wave-uniform
                     k += f + 1;
                     if (lane == 0) js[i] = (uint8_t)jv;               // swap i <-> jv, applied below
                     break;
