@@ -1201,7 +1201,7 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
     const BatchScratch sc = batch_scratch(scratch, n_streams, nb);
     hipStream_t s = ddm::as_hip(stream);
     static const int ex_refill = std::max(1, std::min(64, env_int("DDM_EXACT_REFILL", 24)));
-    static const int fix_blocks_max = env_int("DDM_FIX_BLOCKS", 1024);
+    static const int fix_blocks_max = env_int("DDM_FIX_BLOCKS", 2048);
     static const bool use_pre = env_int("DDM_SCAN_PRE", 1) != 0;
     static const int cls_steps = std::max(0, env_int("DDM_SCAN_STEPS", 2));
     static const int cls_pop = std::max(1, std::min(64, env_int("DDM_SCAN_POP", 16)));
