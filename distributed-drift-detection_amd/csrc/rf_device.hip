@@ -5,7 +5,7 @@
 //   k_dfit_prep    one workgroup per job: gate, NaN check, classes_ (np.unique) and the
 //                  class index of every row, per-feature presorted row orders;
 //   k_dfit_trees   one wave per (job, tree):
-//                    * RandomState(seed): init_genrand on lane 0 (a serial recurrence),
+//                    * RandomState(seed): init_genrand on the scalar unit (serial),
 //                      the 624-word twist in three lane-parallel phases, tempering;
 //                    * the splitter seed = the first randint(0, 2**31-1) of that stream
 //                      (peeked) and the bootstrap = randint(0, L, L) from the same start
@@ -452,16 +452,26 @@ __device__ __forceinline__ void build_tree(const Job& jb, const Layout& lo, int 
 #ifdef DDM_DFIT_PROFILE
     const uint64_t t_a = wall_clock64();
 #endif
-    // ---- RandomState(seed): init_genrand (serial), first block
-    if (lane == 0) {
-        uint32_t v = (uint32_t)jb.seeds[tree];
-        S.mt[0] = v;
-        for (int i = 1; i < 624; ++i) {
-            v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
-            S.mt[i] = v;
+    // ---- RandomState(seed): init_genrand (serial), first block.  The recurrence runs on the
+    // scalar unit (every value is wave-uniform): one multiply, xor, shift and add per word
+    // on SGPRs, each word dropped into lane i % 64 of a VGPR, 64 words per LDS store
+    {
+        uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)jb.seeds[tree]);
+        for (int i0 = 0; i0 < 624; i0 += 64) {
+            uint32_t w = 0;
+#pragma unroll 16
+            for (int k = 0; k < 64; ++k) {
+                const int i = i0 + k;
+                if (i > 0) v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
+                w = lane == k ? v : w;
+            }
+            if (i0 + lane < 624) S.mt[i0 + lane] = w;
         }
     }
     wave_sync();
+#ifdef DDM_DFIT_PROFILE
+    const uint64_t t_a1 = wall_clock64();
+#endif
     twist(S.mt, lane);
     for (int k = lane; k < 624; k += 64) S.tw[k] = temper(S.mt[k]);
     for (int k = lane; k < L; k += 64) S.cnt[k] = 0;
@@ -621,7 +631,8 @@ __device__ __forceinline__ void build_tree(const Job& jb, const Layout& lo, int 
         meta[2] = impure;
 #ifdef DDM_DFIT_PROFILE
         if (tree == 0)   // rng init | bootstrap | build, 10-ns ticks
-            jb.result[10] = (int64_t)((t_b - t_a) | ((t_c - t_b) << 16) | ((wall_clock64() - t_c) << 32));
+            jb.result[10] = (int64_t)((t_b - t_a) | ((t_c - t_b) << 16) | (((wall_clock64() - t_c) & 0xffff) << 32) |
+                                      ((t_a1 - t_a) << 48));
 #endif
     }
 }
@@ -715,6 +726,8 @@ __device__ int64_t compile_forest(const TNode* tn, int64_t M, const int32_t* met
     __shared__ float s_thr[256];
     __shared__ int16_t s_skey[256];
     __shared__ float s_sthr[256];
+    __shared__ uint32_t s_key32[256];
+    __shared__ uint64_t s_pkey[256];
     __shared__ uint32_t s_sdel[256][4];
     __shared__ uint32_t s_rtab[kMaxTabWords];
     __shared__ int s_gnode[256], s_gleaf[256], s_gtree[256], s_nint[256], s_nlv[256];
@@ -722,6 +735,10 @@ __device__ int64_t compile_forest(const TNode* tn, int64_t M, const int32_t* met
     __shared__ uint32_t s_base[4];
     __shared__ int s_bad, s_anynl, s_U;
     __shared__ int64_t s_off[8];
+#ifdef DDM_DFIT_PROFILE
+    __shared__ uint64_t s_prof[4];
+    if (threadIdx.x == 0) s_prof[0] = wall_clock64();
+#endif
     const int t = threadIdx.x;
     if (T > 255 || K > 16) return 0;
     const int vr = K <= 4 ? 1 : K <= 8 ? 2 : 4;
@@ -771,6 +788,9 @@ __device__ int64_t compile_forest(const TNode* tn, int64_t M, const int32_t* met
     s_nint[t] = kind == 2 ? nint : 0;
     s_nlv[t] = kind == 2 ? nlv : 0;
     __syncthreads();
+#ifdef DDM_DFIT_PROFILE
+    if (threadIdx.x == 0) s_prof[1] = wall_clock64();
+#endif
     // ---- B: slots
     int used = 0;
     for (int f = t; f < F; f += kPackThreads) used += s_first[f] != 0xffffffffu;
@@ -779,6 +799,7 @@ __device__ int64_t compile_forest(const TNode* tn, int64_t M, const int32_t* met
     for (int f = t; f < F; f += kPackThreads) {
         if (s_first[f] == 0xffffffffu) continue;
         int r = 0;
+#pragma unroll 8
         for (int g = 0; g < F; ++g) r += s_first[g] < s_first[f];
         s_slot_of[f] = (int16_t)r;
         if (r < kMaxSlots) s_cols[r] = f;
@@ -808,21 +829,37 @@ __device__ int64_t compile_forest(const TNode* tn, int64_t M, const int32_t* met
         atomicAdd(&s_m[sl], 1);
     }
     __syncthreads();
-    // stump ranks: sorted by (nanleft, slot, sid); per slot by (threshold, sorted rank)
+    // stump ranks: sorted by (nanleft, slot, sid); per slot by (threshold, sorted rank).
+    // Both are counts of smaller packed keys (distinct by construction), over the keys
+    // padded to a multiple of 8 with the largest key: 8 broadcast LDS reads per round
+    const int S8 = (S + 7) & ~7;
+    if (t < S8) s_key32[t] = t < S ? ((uint32_t)s_skey[t] << 16) | (uint32_t)t : 0xffffffffu;
+    __syncthreads();
     if (t < S) {
-        const int key = s_skey[t];
+        const uint32_t key = s_key32[t];
         int r = 0;
-        for (int j = 0; j < S; ++j) r += (s_skey[j] < key || (s_skey[j] == key && j < t)) ? 1 : 0;
+#pragma unroll 8
+        for (int j = 0; j < S8; ++j) r += s_key32[j] < key ? 1 : 0;
         s_srank[t] = (int16_t)r;
+        // (slot, threshold as an order-preserving u32 (-0 as +0), sorted rank)
+        const float th = s_sthr[t];
+        const uint32_t b = th == 0.0f ? 0u : __float_as_uint(th);
+        const uint32_t ob = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+        s_pkey[t] = ((uint64_t)(s_skey[t] % kMaxSlots) << 56) | ((uint64_t)ob << 24) | (uint64_t)r;
+    } else if (t < S8) {
+        s_pkey[t] = ~0ull;
     }
     __syncthreads();
     if (t < S) {
-        const int sl = s_skey[t] % kMaxSlots;
-        const float th = s_sthr[t];
-        const int sr = s_srank[t];
+        // rank within the slot = smaller keys - keys of lower slots
+        const uint64_t key = s_pkey[t];
+        const uint64_t lo = key & ~((1ull << 56) - 1);
         int r = 0;
-        for (int j = 0; j < S; ++j)
-            r += (s_skey[j] % kMaxSlots == sl && (s_sthr[j] < th || (s_sthr[j] == th && s_srank[j] < sr))) ? 1 : 0;
+#pragma unroll 8
+        for (int j = 0; j < S8; ++j) {
+            const uint64_t kj = s_pkey[j];
+            r += (kj < key ? 1 : 0) - (kj < lo ? 1 : 0);
+        }
         s_prank[t] = (int16_t)r;
     }
     if (t == 0) {
@@ -851,12 +888,19 @@ __device__ int64_t compile_forest(const TNode* tn, int64_t M, const int32_t* met
     }
     __syncthreads();
     const int64_t total = s_off[7];
+#ifdef DDM_DFIT_PROFILE
+    if (threadIdx.x == 0) s_prof[2] = wall_clock64();
+#endif
     const int n_entries = s_U;
     if (total > cap || n_entries * vr > kMaxTabWords) return 0;
     // ---- D: write the blob
     for (int64_t k = t; k < total / 16; k += kPackThreads) reinterpret_cast<uint4*>(out)[k] = uint4{0, 0, 0, 0};
     __syncthreads();
+#ifdef DDM_DFIT_PROFILE
+    if (threadIdx.x == 0) s_prof[3] = wall_clock64();
+#endif
     ddm_cforest_head* h = reinterpret_cast<ddm_cforest_head*>(out);
+    const int n_right = __syncthreads_count(t < S && s_nl[s_sid[t]] == 0);   // stumps sending NaN right
     const int sw = vr <= 2 ? 4 : 8;
     if (t == 0) {
         h->n_slots = U;
@@ -873,8 +917,6 @@ __device__ int64_t compile_forest(const TNode* tn, int64_t M, const int32_t* met
         h->nodes_off = (int)s_off[2];
         h->leafcls_off = (int)s_off[3];
         for (int k = 0; k < 4; ++k) h->base_votes[k] = s_base[k];
-        int n_right = 0;
-        for (int j = 0; j < S; ++j) n_right += s_nl[s_sid[j]] == 0;
         h->n_stumps_right = n_right;
         h->slots_off = (int)s_off[4];
         h->xthr_off = (int)s_off[5];
@@ -967,11 +1009,49 @@ __device__ int64_t compile_forest(const TNode* tn, int64_t M, const int32_t* met
             gn[ki++] = cn;
         }
     }
+#ifdef DDM_DFIT_PROFILE
+    if (threadIdx.x == 0) {   // 8-bit fields in 80 ns: A, B-C, zero fill, D
+        const uint64_t e = wall_clock64();
+        const auto f8 = [](uint64_t dt) { return min((uint64_t)255, dt >> 3); };
+        s_prof[0] = f8(s_prof[1] - s_prof[0]) | (f8(s_prof[2] - s_prof[1]) << 8) | (f8(s_prof[3] - s_prof[2]) << 16) |
+                    (f8(e - s_prof[3]) << 24);
+        *reinterpret_cast<uint32_t*>(lrank) = (uint32_t)s_prof[0];
+    }
+#endif
     return total;
 }
 
 __device__ void pack_tree(const TNode* tn, int m, int16_t* new_id, int16_t* queue, ddm_node* out, int64_t base,
                           bool pure, const double* vals, int K, int kcap, double* leaf_value, int64_t leaf_row) {
+    if (m <= 3) {
+        // a single leaf or a stump: pre-order ids are already the BFS ids (C3's trees), so
+        // no queue; the nodes are loaded before anything is stored
+        TNode xs[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) xs[u] = tn[u < m ? u : 0];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            if (u >= m) break;
+            const TNode x = xs[u];
+            ddm_node nd;
+            if (x.left != -1) {
+                nd.threshold = x.threshold;
+                nd.feature = x.feature | (x.missing_left ? (1 << 30) : 0);
+                nd.child = (int32_t)(base + x.left);
+            } else {
+                nd.threshold = 0.0;
+                nd.feature = -1;
+                if (pure) {
+                    nd.child = x.leaf - 1;
+                } else {
+                    for (int c = 0; c < K; ++c) leaf_value[leaf_row * K + c] = vals[(int64_t)u * kcap + c];
+                    nd.child = (int32_t)leaf_row++;
+                }
+            }
+            out[base + u] = nd;
+        }
+        return;
+    }
     int head = 0, tail = 0, nxt = 1;
     queue[tail++] = 0;
     new_id[0] = 0;
@@ -1043,7 +1123,9 @@ __global__ __launch_bounds__(kPackThreads) void k_dfit_pack(const Job* __restric
     if (pure && jb.blob)
         bytes = compile_forest(tn, M, meta, T, jb.classes, K, jb.F, bfs, jb.blob, jb.blob_cap);
 #ifdef DDM_DFIT_PROFILE
-    if (t == 0) jb.result[11] = (int64_t)((t_p - t_pack0) | ((wall_clock64() - t_p) << 16));
+    if (t == 0)
+        jb.result[11] = (int64_t)((t_p - t_pack0) | ((wall_clock64() - t_p) << 16) |
+                                  (bytes ? (uint64_t)*reinterpret_cast<const uint32_t*>(bfs) << 32 : 0));
 #endif
     if (t == 0) {
         jb.result[DDM_DFIT_NODES] = n_nodes;

@@ -1,6 +1,7 @@
 """Phase times of the device refit (instrumented build: tools/build_variant.sh dprof
 rf_device.hip -DDDM_DFIT_PROFILE, then DDM_AMD_LIB=.../libddm_amd_dprof.so): a C3-like
-drift batch (100 rows x 27 features, two classes), 8 jobs of 100 trees."""
+drift batch (100 rows x 27 features, two classes), 8 jobs of 100 trees.  `stumps` as the
+argument: every feature separates the classes (C3's trees: all stumps)."""
 import sys
 import time
 
@@ -14,7 +15,7 @@ rng = np.random.default_rng(3)
 batches = []
 for k in range(8):
     y = np.where(np.arange(100) < 60, 3, 4)
-    X = rng.random((100, 27), dtype=np.float32) + (y[:, None] == 4) * 0.5
+    X = rng.random((100, 27), dtype=np.float32) + (y[:, None] == 4) * (10.0 if "stumps" in sys.argv else 0.5)
     batches.append((X.astype(np.float32), y, rng.integers(0, 2**31 - 1, 100)))
 tr = DeviceTrainer(100, 16, torch.device("cuda", 0))
 for rep in range(3):
@@ -24,5 +25,6 @@ for rep in range(3):
     r = out[0][3]
     a, p = int(r[10]), int(r[11])
     print(f"fit_many {dt*1e3:.2f} ms; tree 0: rng init {(a & 0xffff)/100:.1f} us, bootstrap {((a >> 16) & 0xffff)/100:.1f} us, "
-          f"build {(a >> 32)/100:.1f} us; pack: bfs {(p & 0xffff)/100:.1f} us, compile {((p >> 16) & 0xffff)/100:.1f} us; "
+          f"build {((a >> 32) & 0xffff)/100:.1f} us, init_genrand {(a >> 48)/100:.1f} us; pack: bfs {(p & 0xffff)/100:.1f} us, compile {((p >> 16) & 0xffff)/100:.1f} us "
+          f"(A/B-C/zero/D {', '.join(str(((p >> (32 + 8 * i)) & 255) * 0.08)[:4] for i in range(4))} us); "
           f"nodes {int(r[2])}, blob {int(r[5])}")
