@@ -679,6 +679,7 @@ __device__ __forceinline__ void inc_vote(int c, uint32_t* v) { atomicAdd(&v[c >>
 __device__ __forceinline__ uint32_t vote_word(int c, int j) { return (c >> 2) == j ? 1u << (8 * (c & 3)) : 0u; }
 
 constexpr int kPackThreads = 256;
+constexpr int kPackLdsNodes = 1024;          // forests up to this many nodes are packed in LDS
 
 // Block-wide exclusive prefix sum of one int per thread (kPackThreads threads): a wave
 // scan by shuffles, then the wave totals through LDS (two barriers).
@@ -714,8 +715,11 @@ __device__ int block_scan_excl(int v, int* tmp, int& total) {
 //     emits nodes on entry and numbers leaves left to right); the left-subtree leaf mask
 //     of node u covers the leaves with ids in [u + 1, right(u)).
 // Returns the blob size, or 0 when the forest does not compile.
+// tn_lds: when not null, this thread's tree (> 3 nodes) is at tn_lds[my_base ...] in LDS and
+// lrank_lds[my_base ...] is its scratch (k_dfit_pack copied it there)
 __device__ int64_t compile_forest(const TNode* tn, int64_t M, const int32_t* meta, int T, const int32_t* classes,
-                                  int K, int F, int16_t* lrank, uint8_t* out, int64_t cap) {
+                                  int K, int F, int16_t* lrank, uint8_t* out, int64_t cap, const TNode* tn_lds,
+                                  int16_t* lrank_lds, int my_base) {
     __shared__ int s_tmp[kPackThreads];
     __shared__ uint32_t s_first[kMaxF];
     __shared__ int16_t s_slot_of[kMaxF];
@@ -753,7 +757,7 @@ __device__ int64_t compile_forest(const TNode* tn, int64_t M, const int32_t* met
     // ---- A: classify every tree
     int kind = 3, nint = 0, nlv = 0;
     if (t < T) {
-        const TNode* nd = tn + t * M;
+        const TNode* nd = tn_lds && meta[4 * t] > 3 ? tn_lds + my_base : tn + t * M;
         const int n = meta[4 * t];
         const TNode r = nd[0];
         if (r.leaf) {
@@ -976,9 +980,9 @@ __device__ int64_t compile_forest(const TNode* tn, int64_t M, const int32_t* met
     for (int k = t; k < n_entries * vr; k += kPackThreads) rtab[k] = s_rtab[k];
     // general trees: one thread per tree
     if (t < T && kind == 2) {
-        const TNode* nd = tn + t * M;
+        const TNode* nd = tn_lds && meta[4 * t] > 3 ? tn_lds + my_base : tn + t * M;
         const int n = meta[4 * t];
-        int16_t* lr = lrank + t * M;                          // leaves before node u
+        int16_t* lr = tn_lds ? lrank_lds + my_base : lrank + t * M;   // leaves before node u
         int c = 0;
         for (int u = 0; u < n; ++u) {
             lr[u] = (int16_t)c;
@@ -1102,6 +1106,8 @@ __global__ __launch_bounds__(kPackThreads) void k_dfit_pack(const Job* __restric
     int16_t* bfs = reinterpret_cast<int16_t*>(jb.scratch + lo.bfs);
     __shared__ int s_tmp[kPackThreads];
     __shared__ int s_impure;
+    __shared__ TNode s_tn[kPackLdsNodes];
+    __shared__ int16_t s_bid[2 * kPackLdsNodes];
     if (t == 0) s_impure = 0;
     __syncthreads();
     const int nn = t < T ? meta[4 * t] : 0;
@@ -1112,8 +1118,17 @@ __global__ __launch_bounds__(kPackThreads) void k_dfit_pack(const Job* __restric
     const int lbase = block_scan_excl(nl, s_tmp, n_leaf);
     const bool pure = T <= 255 && !s_impure;
     if (t < T) {
-        pack_tree(tn + t * M, nn, bfs + 2 * t * M, bfs + 2 * t * M + M, jb.nodes, base, pure, tv + t * M * jb.k_cap, K,
-                  jb.k_cap, jb.leaf_value, lbase);
+        if (nn > 3 && n_nodes <= kPackLdsNodes) {
+            // the tree's nodes, its BFS ids and queue in LDS (each thread its own range): the
+            // queue walk and the node loop wait on LDS, not on a global round trip per node
+#pragma unroll 4
+            for (int u = 0; u < nn; ++u) s_tn[base + u] = tn[t * M + u];
+            pack_tree(s_tn + base, nn, s_bid + base, s_bid + n_nodes + base, jb.nodes, base, pure,
+                      tv + t * M * jb.k_cap, K, jb.k_cap, jb.leaf_value, lbase);
+        } else {
+            pack_tree(tn + t * M, nn, bfs + 2 * t * M, bfs + 2 * t * M + M, jb.nodes, base, pure, tv + t * M * jb.k_cap,
+                      K, jb.k_cap, jb.leaf_value, lbase);
+        }
         jb.roots[t] = base;
     }
 #ifdef DDM_DFIT_PROFILE
@@ -1121,7 +1136,8 @@ __global__ __launch_bounds__(kPackThreads) void k_dfit_pack(const Job* __restric
 #endif
     int64_t bytes = 0;
     if (pure && jb.blob)
-        bytes = compile_forest(tn, M, meta, T, jb.classes, K, jb.F, bfs, jb.blob, jb.blob_cap);
+        bytes = compile_forest(tn, M, meta, T, jb.classes, K, jb.F, bfs, jb.blob, jb.blob_cap,
+                               n_nodes <= kPackLdsNodes ? s_tn : nullptr, s_bid, base);
 #ifdef DDM_DFIT_PROFILE
     if (t == 0)
         jb.result[11] = (int64_t)((t_p - t_pack0) | ((wall_clock64() - t_p) << 16) |
