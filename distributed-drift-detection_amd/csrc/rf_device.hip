@@ -5,7 +5,7 @@
 //   k_dfit_prep    one workgroup per job: gate, NaN check, classes_ (np.unique) and the
 //                  class index of every row, per-feature presorted row orders;
 //   k_dfit_trees   one wave per (job, tree):
-//                    * RandomState(seed): init_genrand on the scalar unit (serial),
+//                    * RandomState(seed): init_genrand on lane 0 (a serial recurrence),
 //                      the 624-word twist in three lane-parallel phases, tempering;
 //                    * the splitter seed = the first randint(0, 2**31-1) of that stream
 //                      (peeked) and the bootstrap = randint(0, L, L) from the same start
@@ -452,20 +452,15 @@ __device__ __forceinline__ void build_tree(const Job& jb, const Layout& lo, int 
 #ifdef DDM_DFIT_PROFILE
     const uint64_t t_a = wall_clock64();
 #endif
-    // ---- RandomState(seed): init_genrand (serial), first block.  The recurrence runs on the
-    // scalar unit (every value is wave-uniform): one multiply, xor, shift and add per word
-    // on SGPRs, each word dropped into lane i % 64 of a VGPR, 64 words per LDS store
-    {
-        uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)jb.seeds[tree]);
-        for (int i0 = 0; i0 < 624; i0 += 64) {
-            uint32_t w = 0;
-#pragma unroll 16
-            for (int k = 0; k < 64; ++k) {
-                const int i = i0 + k;
-                if (i > 0) v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
-                w = lane == k ? v : w;
-            }
-            if (i0 + lane < 624) S.mt[i0 + lane] = w;
+    // ---- RandomState(seed): init_genrand (serial), first block, on lane 0 (on the scalar
+    // unit instead it made the trees kernel slower: 46 -> 54 us per launch with 800 waves,
+    // which share one scalar unit per CU)
+    if (lane == 0) {
+        uint32_t v = (uint32_t)jb.seeds[tree];
+        S.mt[0] = v;
+        for (int i = 1; i < 624; ++i) {
+            v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
+            S.mt[i] = v;
         }
     }
     wave_sync();

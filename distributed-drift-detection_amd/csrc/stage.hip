@@ -98,6 +98,13 @@ __device__ void plan_next(const Job& jb, int32_t stop, bool drawn, int64_t p_see
 
 __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__ jobs) {
     __shared__ int counts[kStageThreads / 64];
+#ifdef DDM_STAGE_PROFILE
+    const uint64_t t0 = wall_clock64();
+#define STAGE_MARK(k) do { if (threadIdx.x == 0) s_mark[k] = wall_clock64(); } while (0)
+    __shared__ uint64_t s_mark[6];
+#else
+#define STAGE_MARK(k) do { } while (0)
+#endif
     const Job jb = jobs[blockIdx.x];
     const int t = threadIdx.x;
     const int32_t stop = *jb.stop;
@@ -158,6 +165,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
         total += round;
         __syncthreads();
     }
+    STAGE_MARK(0);
     if (t == 0) {
         jb.info_out[1] = total;
         jb.info_out[2] = total > jb.max_events ? 1 : 0;
@@ -205,6 +213,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     for (int kk = t; kk < L; kk += kStageThreads) jb.y_out[kk] = jb.y[row0 + off_d[kk]];
     if (jb.R)
         for (int w = t; w < jb.n_words; w += kStageThreads) jb.w_out[w] = jb.R[P + w];
+    STAGE_MARK(1);
     // ---- batch j = d + 1: its shuffle, then the refit's tree seeds
     __shared__ uint32_t words[kStageWords];
     __shared__ uint8_t perm[256];
@@ -222,13 +231,35 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     const int Lj = j == jb.nb - 1 ? jb.last_len : jb.pb;
     for (int w = t; w < kStageWords; w += kStageThreads) words[w] = jb.R[P + w];
     __syncthreads();
+    STAGE_MARK(2);
     if (wv == 0) {
-        // legacy permutation(Lj), then randint(2**31 - 1) x n_trees, by the first wave: each
-        // interval's accepted draw is the first lane of a ballot over the next 64 words
+        // legacy permutation(Lj), then randint(2**31 - 1) x n_trees, by the first wave.
+        // Interval i accepts the first word w with (w & mask_i) <= i.  Speculation: lane l
+        // tries interval i - l on word k + l (every interval accepting its first word); the
+        // lanes before the first rejection are final, and the rejected interval searches
+        // the words after it by a ballot over 64 at a time.  About a quarter of the rounds
+        // of one interval per round.
         int k = 0;
         bool good = true;
-        for (int i = Lj - 1; i >= 1 && good; --i) {
+        int i = Lj - 1;
+        while (i >= 1) {
+            const int il = i - lane, wi = k + lane;
+            bool acc = false;
+            uint32_t val = 0xffffffffu;
+            if (il >= 1) {
+                const uint32_t mask = 0xffffffffu >> __builtin_clz((uint32_t)il);
+                val = wi < kStageWords ? (words[wi] & mask) : 0xffffffffu;
+                acc = val <= (uint32_t)il;
+            }
+            const uint64_t rej = __ballot(!acc);          // lane i (il = 0) always counts
+            const int r = rej ? __builtin_ctzll(rej) : 64;
+            if (lane < r) js[il] = (uint8_t)val;           // swap il <-> val, applied below
+            i -= r;
+            k += r;
+            if (i < 1 || r == 64) continue;
+            // interval i rejected word k: its first accepted word after it
             const uint32_t mask = 0xffffffffu >> __builtin_clz((uint32_t)i);
+            ++k;
             for (;;) {
                 if (k >= kStageWords) { good = false; break; }
                 const int w = k + lane;
@@ -238,13 +269,16 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
                     const int f = __builtin_ctzll(b);
                     const int jv = __builtin_amdgcn_readlane((int)v, f);   // f is wave-uniform
                     k += f + 1;
-                    if (lane == 0) js[i] = (uint8_t)jv;               // swap i <-> jv, applied below
+                    if (lane == 0) js[i] = (uint8_t)jv;
+                    --i;
                     break;
                 }
                 k += 64;
             }
+            if (!good) break;
         }
         if (lane == 0) pos[0] = P + k;
+        STAGE_MARK(3);
         int got = 0;                                                 // seeds drawn so far
         while (good && got < jb.n_trees) {
             if (k >= kStageWords) { good = false; break; }
@@ -272,6 +306,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
         }
     }
     __syncthreads();
+    STAGE_MARK(4);
     if (!ok) {
         if (t == 0) {
             jb.info_out[6] = 0;
@@ -283,6 +318,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     // transpositions i <-> js[i] for i = Lj-1 .. 1; it ends where Fisher-Yates puts it
     if (t < Lj) {
         int q = t;
+#pragma unroll 8
         for (int i = Lj - 1; i >= 1; --i) {
             const int jv = js[i];
             q = q == i ? jv : (q == jv ? i : q);
@@ -297,6 +333,13 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
         jb.info_out[6] = 1;
         if (jb.plan_out) plan_next(jb, stop, true, pos[1]);
     }
+#ifdef DDM_STAGE_PROFILE
+    __syncthreads();
+    if (t == 0 && blockIdx.x == 0)
+        printf("stage-prof compact %.2f gather %.2f words %.2f shuffle %.2f seeds %.2f swaps %.2f us\n",
+               (s_mark[0] - t0) / 100.0, (s_mark[1] - s_mark[0]) / 100.0, (s_mark[2] - s_mark[1]) / 100.0,
+               (s_mark[3] - s_mark[2]) / 100.0, (s_mark[4] - s_mark[3]) / 100.0, (wall_clock64() - s_mark[4]) / 100.0);
+#endif
 }
 
 }  // namespace
