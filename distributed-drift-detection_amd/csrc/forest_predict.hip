@@ -209,6 +209,16 @@ __device__ __forceinline__ T ldu(const T* p) {
     }
 }
 
+// Feature columns are read through pointers kept in LDS, i.e. generic (flat) pointers: a
+// flat load also counts on lgkmcnt, so the next chunk's prefetch would be waited for by the
+// first scalar load of the slot records.  As global loads they count on vmcnt only.
+__device__ __forceinline__ float ldg1(const float* p) { return *(const __attribute__((address_space(1))) float*)(p); }
+__device__ __forceinline__ float4 ldg4(const float* p) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    const f32x4 v = *(const __attribute__((address_space(1))) f32x4*)(p);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // Stumps are evaluated per feature slot through the blob's rank tables
 // (ddm_cforest_slot): r = #{k : !(x <= t_k)} over the slot's padded ascending thresholds
 // (2 VALU per threshold against uniform operands; NaN counts every entry), then one LDS
@@ -299,7 +309,7 @@ __device__ __forceinline__ void cf_segment(const Seg& sg, int64_t blk, int64_t n
 #pragma unroll
         for (int i = 0; i < kRows; ++i)
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) xc[i][k] = p[k][row[i]];
+            for (int k = 0; k < kChunk; ++k) xc[i][k] = ldg1(p[k] + row[i]);
     };
     float xa[kRows][kChunk], xb[kRows][kChunk];
 #pragma unroll
@@ -477,7 +487,7 @@ __device__ __forceinline__ void cf_segment_vec(const Seg& sg, int64_t blk, int64
     };
     auto load_chunk = [&](int c, int64_t row, float4 (&xc)[kVecChunk]) {
 #pragma unroll
-        for (int k = 0; k < kVecChunk; ++k) xc[k] = *reinterpret_cast<const float4*>(s_colp[c + k] + row);
+        for (int k = 0; k < kVecChunk; ++k) xc[k] = ldg4(s_colp[c + k] + row);
     };
     float4 xa[kVecChunk], xb[kVecChunk];
 #pragma unroll
