@@ -249,7 +249,7 @@ class BatchRunner:
             self.max_wins.append(mw)
             self.nbs.append(nb)
             pos = _round_up(pos + part.n, align) + align
-            evp += mw
+            evp += mw + (mw & 1)                # even: every partition's event rows start 16-byte aligned
         self.perm_all = torch.zeros(pos + 256, dtype=torch.uint8, device=dev)
         self.err_all = torch.zeros(pos + 32, dtype=torch.uint8, device=dev)
         self.ev_total = evp
