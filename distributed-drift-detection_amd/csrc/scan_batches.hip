@@ -922,7 +922,10 @@ struct FixEntry {
 // flight), walk_open over its flag bytes from the carried-in state.  Most streams end here;
 // a stream that needs rows with a carried detector (a chain longer than the level-1 records,
 // or a carried-in state) goes to the fix-up list with its position.
-constexpr int kWalkThreads = 256;
+#ifndef DDM_WALK_THREADS
+#define DDM_WALK_THREADS 256
+#endif
+constexpr int kWalkThreads = DDM_WALK_THREADS;
 
 __global__ __launch_bounds__(kWalkThreads) void k_scan_batches_walk(
     int64_t n_streams, int64_t L, int64_t nb, int64_t nbp, ddm_params P, ddm_state* __restrict__ state,
