@@ -4,6 +4,12 @@
 Workloads (BASELINE.json configs; rialto.csv is not shipped, so every
 rialto-shaped stream is synthetic and generated in HBM before the timed region):
 
+  c2  configs[1]: the reference's own outdoorStream (the parsed csv, tests/golden/outdoor.npz)
+      through its data prep (DDM_Process.py:42-51: concat x MULT, shuffle, stable sort by
+      target; data seed 123 as the fixtures) and row % INSTANCES (:220-226), partition d
+      seeded 1000 + d.  Default MULT=512, INSTANCES=16: the published cell (BASELINE.md §1,
+      79.6 s = 25,722 rows/s on 16 Spark instances x 2 cores) -> `vs_baseline`.  At MULT in
+      {1,2,4} every partition's events are compared with the reference-executed fixtures.
   c3  (default) configs[2]: ONE 1B-row rialto-shaped stream (27 float32 features, 10
       noise-free separable classes in class blocks of 10,000,037 global rows -> sparse
       abrupt drifts), split row % 8 (DDM_Process.py:225) into 8 partitions of 125M rows.
@@ -25,7 +31,11 @@ identical to sklearn 1.7.2).  The timed region is bracketed by a barrier and a d
 synchronisation, the time is the max over ranks, and `value` = all rows of all ranks /
 that time.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c3w|c1|c4|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c3w|c1|c4|c5]
+
+--gpus N > 1 without an external launcher starts N ranks itself (torch.distributed.run,
+before this process touches the GPU) and exits with their status; under a launcher
+WORLD_SIZE must equal N.
 """
 import argparse
 import hashlib
@@ -40,7 +50,22 @@ sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md: 8.0 TB/s; ~6.3 measured copy)
 PEAK_FP64_VALU_TFLOPS = 78.6   # MI355X FP64 vector
-BEST_PUBLISHED_ROWS_S = 25_722.0   # outdoorStream x512, 16 instances x 2 cores
+# published Final Time (s) of DDM_Process.py on outdoorStream, 8gb executors x
+# 2 cores, per (MULT_DATA, INSTANCES) (Plot Results.ipynb:325-590)
+PUBLISHED_S_2CORES = {
+    (1, 4): 12.5, (1, 8): 12.5, (1, 16): 14.7,
+    (2, 1): 19.1, (2, 2): 26.1, (2, 4): 15.3, (2, 8): 16.8, (2, 16): 18.6,
+    (4, 1): 21.5, (4, 2): 27.7, (4, 4): 32.4, (4, 8): 26.5, (4, 16): 31.3,
+    (8, 1): 26.2, (8, 2): 33.6, (8, 4): 61.1, (8, 8): 51.7, (8, 16): 50.0,
+    (16, 1): 34.2, (16, 2): 26.8, (16, 4): 64.1, (16, 8): 102.2, (16, 16): 93.9,
+    (32, 1): 48.2, (32, 2): 35.0, (32, 4): 55.7, (32, 8): 74.9, (32, 16): 158.2,
+    (64, 1): 75.7, (64, 2): 50.0, (64, 4): 47.1, (64, 8): 56.3, (64, 16): 178.1,
+    (128, 1): 131.8, (128, 2): 76.3, (128, 4): 74.1, (128, 8): 84.0, (128, 16): 115.3,
+    (256, 1): 236.1, (256, 2): 133.2, (256, 4): 125.4, (256, 8): 75.8, (256, 16): 98.4,
+    (512, 1): 456.7, (512, 2): 239.9, (512, 4): 222.5, (512, 8): 124.2, (512, 16): 79.6,
+}
+OUTDOOR_ROWS = 4000
+C2_DATA_SEED, C2_BASE_SEED = 123, 1000      # tests/golden/make_golden.py (data seed, np.random.seed(base + d))
 C3_BLOCK = 10_000_037
 C3_PARTS = 8
 SEED = 20261015
@@ -51,7 +76,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c3w", "c1", "c4", "c5"])
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c3w", "c1", "c4", "c5"])
+    ap.add_argument("--c2-mult", type=int, default=512, help="c2 MULT_DATA")
+    ap.add_argument("--c2-instances", type=int, default=16, help="c2 INSTANCES")
+    ap.add_argument("--c2-cpu-rows", type=int, default=0,
+                    help="c2 rows per CPU baseline process (0: the whole partition, i.e. the whole job over P = INSTANCES)")
+    ap.add_argument("--companion", type=int, default=1,
+                    help="c3 at N=1: also time the c2 published cell on the GPU (reported under 'companion')")
     ap.add_argument("--parts", type=int, default=8, help="partitions (INSTANCES) of the c3/c5 stream")
     ap.add_argument("--rows-per-part", type=int, default=125_000_000, help="c3/c3w rows per partition")
     ap.add_argument("--block-rows", type=int, default=C3_BLOCK, help="global class-block length (c3)")
@@ -62,9 +93,10 @@ def parse():
                     help="partition groups per GPU, each on its own epoch stream and host thread (pipelined)")
     ap.add_argument("--seed", type=int, default=SEED)
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-procs", type=int, default=8, help="CPU baseline worker processes (P)")
+    ap.add_argument("--cpu-procs", type=int, default=16,
+                    help="CPU baseline worker processes (P); P x CORES = 32 = a 256-core node's share per GPU")
     ap.add_argument("--cpu-cores", type=int, default=2, help="CPU baseline CORES = RF n_jobs per process")
-    ap.add_argument("--cpu-sample-rows", type=int, default=30_000, help="rows per CPU baseline process")
+    ap.add_argument("--cpu-sample-rows", type=int, default=90_000, help="rows per CPU baseline process")
     ap.add_argument("--oracle-check-rows", type=int, default=40_000,
                     help="rows of partition 0 re-run by the oracle after the timed region (0: off)")
     ap.add_argument("--c4-streams", type=int, default=1_000_000)
@@ -111,22 +143,68 @@ def _cpu_sample(spec):
     return X.astype(np.float64), y.astype(np.int64)
 
 
-def _cpu_worker(spec_cores):
-    """One Spark-task equivalent: the pandas/iterrows port of run_DDM_loop
-    (oracle/controller.py run_partition_frames, sklearn RF n_jobs=CORES) on one sample."""
+_C2 = {}
+
+
+def outdoor_stream(mult, instances):
+    """configs[1]: the reference's outdoorStream.csv (as pandas parsed it, tests/golden/
+    outdoor.npz) through DDM_Process.py:44-51 (seeded, stable sort, as the fixtures) and
+    :220-226.  Returns (loader.StreamTable, order, [loader.PartitionArrays]); memoised, and
+    built in the parent before the CPU baseline's workers fork, which inherit it."""
+    key = (int(mult), int(instances))
+    if key not in _C2:
+        import numpy as np
+        from ddm_amd import loader
+        d = np.load(os.path.join(ROOT, "tests", "golden", "outdoor.npz"), allow_pickle=False)
+        X, tgt = d["X"], d["target"].astype(np.int64)
+        table = loader.StreamTable(np.ascontiguousarray(X.T.astype(np.float32)), tgt,
+                                   [str(i) for i in range(X.shape[1])])
+        order = loader.prepare_order(table.n_rows, tgt, mult, np.random.RandomState(C2_DATA_SEED), "stable")
+        _C2[key] = (table, order, loader.split_partitions(table, order, instances))
+    return _C2[key]
+
+
+def c1_stream():
+    """configs[0]'s rialto-shaped table through the data prep (memoised like outdoor_stream)."""
+    if "c1" not in _C2:
+        from ddm_amd import synth
+        _C2["c1"] = synth.rialto_partitions()
+    return _C2["c1"]
+
+
+def _cpu_frame(spec):
+    """(frame, feature names, seed) of one CPU-baseline sample."""
     import numpy as np
     import pandas as pd
-    from oracle.controller import run_partition_frames
-    spec, cores = spec_cores
+    if spec[0] == "c2":
+        _, mult, inst, k, rows = spec
+        table, _, parts = outdoor_stream(mult, inst)
+        p = parts[k]
+        f = p.frame(table.features)
+        return (f.iloc[:rows] if rows else f), table.features, C2_BASE_SEED + p.device_id
+    if spec[0] == "c1":
+        _, rows, seed = spec
+        table, _, parts = c1_stream()
+        return parts[0].frame(table.features).iloc[:rows], table.features, seed
     X, y = _cpu_sample(spec)
     feats = [str(i) for i in range(X.shape[1])]
     pdf = pd.DataFrame(X, columns=feats)
     pdf["target"] = y
     pdf["full_df_row_number"] = np.arange(len(y))
-    np.random.seed(spec[1] + 1000)
+    return pdf, feats, spec[1] + 1000
+
+
+def _cpu_worker(spec_cores):
+    """One Spark-task equivalent: the pandas/iterrows port of run_DDM_loop
+    (oracle/controller.py run_partition_frames, sklearn RF n_jobs=CORES) on one sample."""
+    import numpy as np
+    from oracle.controller import run_partition_frames
+    spec, cores = spec_cores
+    pdf, feats, seed = _cpu_frame(spec)
+    np.random.seed(seed)
     t0 = time.perf_counter()
     out = run_partition_frames(pdf, feats, n_jobs=cores)
-    return len(y), int((out["change_flag_global"] >= 0).sum()), time.perf_counter() - t0
+    return len(pdf), int((out["change_flag_global"] >= 0).sum()), time.perf_counter() - t0
 
 
 class CpuBaseline:
@@ -147,20 +225,30 @@ class CpuBaseline:
         self.pool.join()
         rows = sum(r[0] for r in res)
         refits = sum(r[1] for r in res)
+        try:
+            avail = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            avail = None
         return {"value": rows / wall, "unit": "rows/s", "cores": self.procs * self.cores, "kind": "port",
-                "procs": self.procs, "CORES": self.cores, "os_cpu_count": os.cpu_count(),
+                "procs": self.procs, "CORES": self.cores, "os_cpu_count": os.cpu_count(), "cpus_available": avail,
+                "node_estimate_rows_per_s": rows / wall * 8,
+                "node_note": "P x CORES = the per-GPU share of the node's cores (256 / 8 = 32 on an 8-GPU "
+                             "MI355X node); node_estimate = 8 such shares, assuming linear scaling over them",
                 "refits_per_s": refits / wall, "sample": f"{what}; {len(specs)} samples on {self.procs} processes x "
                                                          f"n_jobs={self.cores}, {rows} rows, {refits} drifts+refits, "
-                                                         f"{wall:.1f} s wall"}
+                                                         f"{wall:.1f} s wall (from the first dispatch to the last "
+                                                         f"result, sample building included)"}
 
 
 def c3_cpu_specs(args, n_parts, block):
-    """Per partition: a window of cpu_sample_rows rows centred on the partition's first
-    class boundary (the predict, DDM, drift and refit work of the stream)."""
+    """One sample per worker process: partition k % n_parts, a window of cpu_sample_rows
+    rows centred on its (k // n_parts + 1)-th class boundary (the predict, DDM, drift and
+    refit work of the stream)."""
     half = args.cpu_sample_rows // 2
     specs = []
-    for d in range(min(n_parts, args.cpu_procs)):
-        b = (block - d + n_parts - 1) // n_parts
+    for k in range(args.cpu_procs):
+        d, m = k % n_parts, k // n_parts + 1
+        b = (m * block - d + n_parts - 1) // n_parts
         specs.append(("c3", d, n_parts, max(0, b - half), args.cpu_sample_rows, args.features, args.seed, block))
     return specs
 
@@ -230,13 +318,21 @@ def oracle_prefix_check(part, n, seed, got):
 def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     import numpy as np
     from ddm_amd import synth
-    from ddm_amd.controller import BatchRunner, GroupedRunner, RunStats
+    from ddm_amd.controller import BatchRunner, DevicePartition, GroupedRunner, RunStats
     from ddm_amd.params import DDMSettings
     from ddm_amd.rng import MTStream
     P = args.parts
     # GPUs the partitions are placed on (solo_world: rank 0's share of an N-GPU job, alone)
     gpus = args.solo_world if args.solo_world > 1 and world == 1 else world
-    if kind == "c3":
+    seed_base = args.seed
+    c2parts = None
+    if kind == "c2":
+        table, _, allp = outdoor_stream(args.c2_mult, args.c2_instances)
+        c2parts = {p.device_id: p for p in allp}
+        instances, block, n = args.c2_instances, None, None
+        mine = [d for d in sorted(c2parts) if d % gpus == rank]
+        seed_base = C2_BASE_SEED
+    elif kind == "c3":
         instances, block, n = P, args.block_rows, args.rows_per_part
         mine = [d for d in range(instances) if d % gpus == rank]
     elif kind == "c3w":
@@ -249,13 +345,18 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
         mine = [d for d in range(instances) if d % gpus == rank]
     parts = []
     for d in mine:
-        if kind == "c5":
+        if kind == "c2":
+            part = DevicePartition.from_columns(c2parts[d].X32, c2parts[d].target, dev)
+        elif kind == "c5":
             part = synth.jitter_partition(n, d, instances, args.seed, dev, flip=args.c5_flip, n_features=args.features)
         else:
             part = synth.block_partition(n, d, instances, block, args.seed, dev, n_features=args.features)
         parts.append((d, part))
     results = {}
-    n_rows = {d: (n + 99) // 100 - 1 for d in range(instances)}
+    if kind == "c2":
+        n_rows = {d: (len(p.target) + 99) // 100 - 1 for d, p in c2parts.items()}
+    else:
+        n_rows = {d: (n + 99) // 100 - 1 for d in range(instances)}
     gather_s = [0.0]
     if not parts:
         raise RuntimeError(f"rank {rank} owns no partition ({instances} partitions over {world} GPUs)")
@@ -269,7 +370,7 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     torch.cuda.synchronize()
 
     def step():
-        outs = runner.run([MTStream.from_seed(args.seed + d) for d, _ in parts])
+        outs = runner.run([MTStream.from_seed(seed_base + d) for d, _ in parts])
         for (d, _), o in zip(parts, outs):
             results[d] = o
         if getattr(runner, "trace", None) and os.environ.get("DDM_HOST_TRACE_OUT"):
@@ -324,12 +425,17 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
         if not np.array_equal(r, ref_events.get(g, r)):
             raise RuntimeError(f"partition {g}: events differ in the instrumented step")
     checks = {}
+    fixture = None
+    if kind == "c2":
+        fixture = c2_fixture_check(args.c2_mult, instances, c2parts, results)
+        if fixture:
+            checks["fixtures"] = fixture
     if kind == "c3":
         c3_property_check(results, n, instances, block)
         checks["property"] = "one drift per class boundary, in the batch holding it, no warning: ok"
-    if args.oracle_check_rows and rank == 0:
+    if args.oracle_check_rows and rank == 0 and not fixture:
         d0, p0 = parts[0]
-        k = oracle_prefix_check(p0, args.oracle_check_rows, args.seed + d0, results[d0])
+        k = oracle_prefix_check(p0, args.oracle_check_rows, seed_base + d0, results[d0])
         if k:
             checks["oracle_prefix"] = f"partition {d0}: first {k} rows == oracle/controller.py"
     all_events = getattr(step, "all", None) if world > 1 else {d: events_rows(r) for d, r in results.items()}
@@ -344,7 +450,7 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     agg["predict_bytes"] = st_kern.predict_bytes * args.steps
     drifts = int(sum((r[:, 1] >= 0).sum() for r in results.values()))
     warns = int(sum((r[:, 0] >= 0).sum() for r in results.values()))
-    rows_rank = n * len(parts) * args.steps
+    rows_rank = sum(p.n for _, p in parts) * args.steps
     launches = max(1, agg["epochs"])
     rows_per_launch = agg["predicted_rows"] / launches
     avg_ms_step = agg["predict_ms"] / launches
@@ -353,7 +459,11 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     runner.close()
     avg_ms = replay_ms if replay_n else avg_ms_step
     achieved = (agg["predict_bytes"] / launches) / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    if kind == "c5":
+    if kind == "c2":
+        wl = (f"configs[1]: outdoorStream.csv (the reference's file, 4000 x 21) x MULT={args.c2_mult} "
+              f"({OUTDOOR_ROWS * args.c2_mult} rows; concat, shuffle with data seed {C2_DATA_SEED}, stable sort by "
+              f"target), INSTANCES={instances} (row % INSTANCES), partition d seeded {C2_BASE_SEED} + d, on GPU d % N")
+    elif kind == "c5":
         wl = (f"configs[4]: {args.c5_rows} rows, {args.features} f32 features, class blocks of 150-300 partition rows "
               f"(global boundaries every 1800 +- 300 rows), label noise {args.c5_flip}, INSTANCES={instances}")
     elif kind == "c3":
@@ -362,7 +472,8 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     else:
         wl = (f"configs[2] weak-scaling variant: {P} partitions x {n} rows per GPU, INSTANCES={instances}, "
               f"class blocks of {block} global rows")
-    info = {"workload": wl, "rows_per_step": n * instances if kind != "c3w" else n * P * gpus,
+    info = {"workload": wl, "rows_per_step": (OUTDOOR_ROWS * args.c2_mult if kind == "c2" else
+                                              n * instances if kind != "c3w" else n * P * gpus),
             "partitions": instances, "partitions_this_rank": len(parts),
             "solo_share_of_gpus": gpus if gpus != world else None,
             "refit": "ddm_rf_fit_device (sklearn 1.7.2 RandomForestClassifier restated, identical trees) on the GPU",
@@ -395,16 +506,46 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
                                  "timed step's predict segment tables (2 passes)"}
     cpu_res = None
     if cpu is not None:
-        if kind == "c5":
-            specs = [("c5", d, instances, 0, args.cpu_sample_rows, args.features, args.seed,
-                      (synth.C5_PERIOD, synth.C5_JITTER, args.c5_flip)) for d in range(min(instances, cpu.procs))]
-            cpu_res = cpu.run(specs, f"first {args.cpu_sample_rows} rows of each partition of the c5 stream")
+        if kind == "c2":
+            ids = sorted(c2parts)
+            specs = [("c2", args.c2_mult, instances, k, args.c2_cpu_rows) for k in range(min(len(ids), cpu.procs))]
+            what = f"the first {args.c2_cpu_rows} rows" if args.c2_cpu_rows else "all rows"
+            cpu_res = cpu.run(specs, f"{what} of each of {len(specs)} partitions of the same stream (outdoorStream "
+                                     f"x{args.c2_mult}, INSTANCES={instances})")
+        elif kind == "c5":
+            half = args.cpu_sample_rows
+            specs = [("c5", k % instances, instances, (k // instances) * half, half, args.features, args.seed,
+                      (synth.C5_PERIOD, synth.C5_JITTER, args.c5_flip)) for k in range(cpu.procs)]
+            cpu_res = cpu.run(specs, f"{len(specs)} windows of {half} rows (partition k % {instances}, window k // "
+                                     f"{instances}) of the c5 stream")
         else:
             cpu_res = cpu.run(c3_cpu_specs(args, instances, block),
                               f"{args.cpu_sample_rows} rows around each partition's first class boundary "
                               f"(one drift + refit each) of the c3 stream")
     scaling = "weak" if kind == "c3w" else "strong"
     return rows_rank, elapsed, info, extra, roofline, cpu_res, scaling
+
+
+def c2_fixture_check(mult, instances, c2parts, results):
+    """Every partition's events (reference columns: local = partition position, global =
+    full_df_row_number) == the reference-executed fixture of this (MULT, INSTANCES), when
+    tests/golden holds one; None otherwise."""
+    import numpy as np
+    path = os.path.join(ROOT, "tests", "golden", f"outdoor_cfg_m{mult}_i{instances}.npz")
+    if not os.path.exists(path):
+        return None
+    cfg = np.load(path, allow_pickle=False)
+    for d, r in results.items():
+        rn = c2parts[d].row_number
+        ev = np.full((len(r), 4), -1, dtype=np.int64)
+        for c in range(2):
+            hit = r[:, c] >= 0
+            ev[hit, 2 * c] = r[hit, c]
+            ev[hit, 2 * c + 1] = rn[r[hit, c]]
+        want = cfg[f"events/{d}"]
+        if not np.array_equal(ev, want):
+            raise RuntimeError(f"c2 partition {d}: events differ from the reference fixture {os.path.basename(path)}")
+    return f"all {len(results)} partitions == tests/golden/{os.path.basename(path)} (reference-executed)"
 
 
 def run_c1(args, world, rank, dev, torch, dist, cpu):
@@ -414,7 +555,7 @@ def run_c1(args, world, rank, dev, torch, dist, cpu):
     from ddm_amd.controller import BatchRunner, DevicePartition, RunStats
     from ddm_amd.params import DDMSettings
     from ddm_amd.rng import MTStream
-    table, order, parts = synth.rialto_partitions()
+    table, order, parts = c1_stream()
     pa = parts[0]
     part = DevicePartition.from_columns(pa.X32, pa.target, dev)
     runner = BatchRunner([part], DDMSettings(), torch.cuda.Stream(dev, priority=-1), refit=args.refit, timing=True,
@@ -441,21 +582,17 @@ def run_c1(args, world, rank, dev, torch, dist, cpu):
     n = part.n
     checks = {"events_sha1": events_digest({0: events_rows(out[0])})}
     cpu_res = None
-    t_or = None
-    if cpu is not None or args.oracle_check_rows:
+    if args.oracle_check_rows:
         from oracle.controller import run_partition
         np.random.seed(args.seed)
-        t = time.perf_counter()
         want = run_partition(pa.X32.T.astype(np.float64), pa.target, np.arange(n), pa.row_number)
-        t_or = time.perf_counter() - t
         if not (np.array_equal(out[0][:, 0], want[:, 0]) and np.array_equal(out[0][:, 1], want[:, 2])):
             raise RuntimeError("c1: events differ from the oracle")
         checks["oracle"] = f"all {n} rows == oracle/controller.py run_partition"
-        if cpu is not None:
-            cpu_res = {"value": n / t_or, "unit": "rows/s", "cores": 1, "kind": "port", "procs": 1, "CORES": 1,
-                       "os_cpu_count": os.cpu_count(),
-                       "sample": f"the whole c1 partition ({n} rows), oracle/controller.py run_partition (numpy "
-                                 f"batches, sklearn RF n_jobs=1, DDM restated), {t_or:.1f} s"}
+    if cpu is not None:
+        rows_cpu = min(n, args.cpu_sample_rows // 2)
+        cpu_res = cpu.run([("c1", rows_cpu, args.seed)],
+                          f"the first {rows_cpu} rows of the c1 partition (configs[0]: one CPU worker)")
     st = runner.stats
     launches = max(1, st.epochs)
     info = {"workload": f"configs[0]: rialto-shaped table {synth.C1_ROWS} x {synth.C1_FEATURES} Dirichlet histograms "
@@ -513,6 +650,11 @@ def run_c4(args, world, rank, dev, torch, dist, cpu):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     changes = int((ev[:, 1] >= 0).sum().item())
+    # rows the DDM actually consumes: a batch is read up to its change (DDM_Process.py:150-152)
+    blen = torch.full((nb,), 100, dtype=torch.int64, device=dev)
+    blen[-1] = L - 100 * (nb - 1)
+    chg = ev[:, 1].view(S, nb).to(torch.int64)
+    scanned = int(torch.where(chg >= 0, chg + 1, blen.view(1, nb)).sum().item())
     rows = S * L * args.steps
     avg_ms = kms / args.steps
     alg = S * L * 1.0 + S * nb * 8
@@ -522,17 +664,25 @@ def run_c4(args, world, rank, dev, torch, dist, cpu):
         from oracle.ddm import scan_stream
         e = err[:2000 * L].cpu().numpy()
         t = time.perf_counter()
-        k = 0
+        k = cpu_scanned = 0
         while time.perf_counter() - t < 10 and k < 2000:
-            scan_stream(e[k * L:(k + 1) * L], mode="restart")
+            evk = scan_stream(e[k * L:(k + 1) * L], mode="restart")[0]
+            lens = np.minimum(100, L - 100 * np.arange(len(evk)))
+            cpu_scanned += int(np.where(evk[:, 1] >= 0, evk[:, 1] + 1, lens).sum())
             k += 1
         dt = time.perf_counter() - t
         cpu_res = {"value": k * L / dt, "unit": "rows/s", "cores": 1, "kind": "port",
-                   "sample": f"{k} streams x {L} rows, oracle/ddm.py scan_stream (pure-Python DDM, no iterrows)"}
+                   "rows_scanned_per_s": cpu_scanned / dt,
+                   "sample": f"{k} streams x {L} rows ({cpu_scanned} rows consumed by the DDM, the rest of each "
+                             f"changed batch skipped as DDM_Process.py:150-152 does), oracle/ddm.py scan_stream "
+                             f"(pure-Python DDM, no iterrows)"}
     info = {"workload": f"configs[3]: {S} independent streams x {L} rows (Bernoulli r0~U(.01,.2) stepping "
                         f"by U(.05,.3)), DDM only, fresh DDM at the batch after each change"}
     rows_s = S * L / (avg_ms * 1e-3)
-    extra = {"changes_per_step": changes, "scan_kernel_ms": avg_ms}
+    extra = {"changes_per_step": changes, "scan_kernel_ms": avg_ms, "rows_scanned_per_call": scanned,
+             "rows_scanned_per_s": scanned / (avg_ms * 1e-3),
+             "rows_note": "value counts every row of every stream (nominal); rows_scanned counts the rows the DDM "
+                          "consumes (each batch up to its change), the same way on the CPU side"}
     roofline = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_from_profile("ddm_scan_batches", S * L),
                 "kernel": "ddm_scan_batches", "alg_bytes_per_row": "1 + 8/100",
@@ -547,14 +697,69 @@ def run_c4(args, world, rank, dev, torch, dist, cpu):
     return rows, elapsed, info, extra, roofline, cpu_res, "weak"
 
 
+def launch_ranks(args):
+    """--gpus N > 1 with no launcher around this process: start N ranks of this same
+    command under torch.distributed.run (127.0.0.1, a free port) and return their exit
+    status.  Runs before anything here touches the GPU (the children initialise their own)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def published_cell(workload, args):
+    """(rows/s, basis) of the published reference number for this exact workload, or None."""
+    if workload != "c2":
+        return None
+    sec = PUBLISHED_S_2CORES.get((args.c2_mult, args.c2_instances))
+    if sec is None:
+        return None
+    rows = OUTDOOR_ROWS * args.c2_mult
+    return rows / sec, (f"BASELINE.md §1 (Plot Results.ipynb:325-590): DDM_Process.py on outdoorStream x{args.c2_mult}, "
+                        f"{args.c2_instances} Spark instances x 2 cores, 8gb: {sec} s = {rows / sec:,.0f} rows/s "
+                        f"(unspecified CPU cluster)")
+
+
+def companion_c2(args, rank, dev, torch, dist):
+    """The published cell (c2, outdoorStream x512 / 16 instances) on this GPU, after the
+    main measurement: GPU rows/s, its vs_baseline and checks, no CPU baseline."""
+    import copy
+    a = copy.copy(args)
+    a.workload, a.steps, a.warmup, a.oracle_check_rows, a.groups = "c2", 3, 1, 12_800, 1
+    rows, elapsed, info, extra, roofline, _, _ = run_partition_workload(a, 1, rank, dev, torch, dist, "c2", None)
+    value = rows / elapsed
+    pub = published_cell("c2", a)
+    return {"workload": info["workload"], "value": value, "unit": "rows/s", "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3, "vs_baseline": value / pub[0] if pub else None,
+            "vs_baseline_basis": pub[1] if pub else None, "epochs_per_step": extra["epochs_per_step"],
+            "drifts_per_step": extra["drifts_per_step"], "checks": extra["checks"],
+            "predict_roofline_frac": roofline["frac"]}
+
+
 def main():
     args = parse()
     world, rank, local_rank = dist_env()
+    if "WORLD_SIZE" in os.environ:
+        if args.gpus != world and args.solo_world == 0:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    elif args.gpus > 1:
+        sys.exit(launch_ranks(args))
     if args.solo_world > 1 and world == 1:
         args.cpu_baseline = 0
+    if args.workload == "c2" or (args.workload == "c3" and args.companion and world == 1):
+        outdoor_stream(args.c2_mult, args.c2_instances)      # host data, before the workers fork
+    if args.workload == "c1":
+        c1_stream()
     cpu = None
-    if args.cpu_baseline and rank == 0 and world == 1 and args.workload in ("c3", "c3w", "c5"):
-        cpu = CpuBaseline(args.cpu_procs, args.cpu_cores)     # forked before any HIP call
+    if args.cpu_baseline and rank == 0 and world == 1 and args.workload in ("c1", "c2", "c3", "c3w", "c5"):
+        procs = {"c1": 1, "c2": min(args.cpu_procs, args.c2_instances)}.get(args.workload, args.cpu_procs)
+        cpu = CpuBaseline(procs, args.cpu_cores)              # forked before any HIP call
     import torch
     import torch.distributed as dist
     # DDM_BENCH_BACKEND=gloo with fewer GPUs than ranks rehearses the N>1 path on one box
@@ -596,17 +801,22 @@ def main():
         rows_total = float(rows_rank)
     if rank == 0:
         value = rows_total / elapsed
+        pub = published_cell(args.workload, args)
         out = {"metric": "stream rows/sec through predict+DDM (node, 1/2/4/8 GPU) + % HBM roofline",
                "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-               "scaling": scaling, "vs_baseline": value / BEST_PUBLISHED_ROWS_S,
-               "vs_baseline_basis": "best published reference rows/s (BASELINE.md §1: outdoorStream x512, 16 Spark "
-                                    "instances x 2 cores, 25,722 rows/s; different data and hardware)",
+               "scaling": scaling, "vs_baseline": value / pub[0] if pub else None,
+               "vs_baseline_basis": pub[1] if pub else "no published reference number for this workload (the "
+                                                       "reference publishes outdoorStream only: --workload c2)",
                "dtype": "f64",
-               "data": "synthetic (rialto.csv not shipped), generated before the timed region",
+               "data": ("the reference's outdoorStream.csv (parsed, tests/golden/outdoor.npz), resident in HBM "
+                        "before the timed region" if args.workload == "c2" else
+                        "synthetic (rialto.csv not shipped), generated before the timed region"),
                "config": dict(info, parallelism=f"partitions over {world} GPU(s), partition d on GPU d % {world}, "
                                                 f"no data-path collective"),
                "roofline": roofline, "cpu_baseline": cpu_res, "breakdown": extra}
+        if args.workload == "c3" and args.companion and world == 1 and not args.solo_world:
+            out["companion"] = {"c2_published_cell": companion_c2(args, rank, dev, torch, dist)}
         print(json.dumps(out), flush=True)
     if comm is not None:
         comm.close()

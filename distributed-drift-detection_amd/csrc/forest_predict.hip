@@ -649,11 +649,15 @@ int cf_vkind(int vr) { return vr <= 1 ? 0 : vr <= 2 ? 1 : 2; }
 // rows per thread: 1 with general trees, 4 consecutive (16-byte loads) for stump forests
 // whose rows and positions are 16- / 4-byte aligned, else 2
 bool vec_env() {
+#ifdef DDM_TUNING                                   // tuning builds only (tools/build_variant.sh)
     static const bool on = [] {
         const char* e = getenv("DDM_PREDICT_VEC");
         return e ? atoi(e) != 0 : true;
     }();
     return on;
+#else
+    return true;
+#endif
 }
 int cf_rows(const Seg& g, int pb) {
     if (g.cf_leaves > 0) return 1;

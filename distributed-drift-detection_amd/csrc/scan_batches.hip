@@ -537,7 +537,8 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
     }
 }
 
-// Timing probe (DDM_SCAN_PROBE=1, results are NOT the scan's): the classify pass's reads,
+#ifdef DDM_TUNING
+// Timing probe (DDM_SCAN_PROBE=1, tuning builds only; results are NOT the scan's): the classify pass's reads,
 // LDS image and bit extraction with one 8-byte store per batch and nothing else, to price
 // its decision and queue work against the pure stream.
 template <int kLoads, int kMode>
@@ -591,6 +592,7 @@ __global__ __launch_bounds__(kClsThreads) void k_scan_batches_probe(
     }
     if (lane == 0) qcnt[wave] = q1cnt[wave] = 0;
 }
+#endif  // DDM_TUNING
 
 // 2./3. Exact rows, one lane per queued batch.  Lanes that finish take the next entries of
 // the wave's queue (one claim for all idle lanes, no atomics: the queue is the wave's own);
@@ -1158,9 +1160,16 @@ BatchScratch batch_scratch(void* base, int64_t n_streams, int64_t nb) {
     return sc;
 }
 
+// Tuning knobs read from the environment exist only in a tuning build (-DDDM_TUNING,
+// tools/build_variant.sh); the production library always runs the defaults.
 int env_int(const char* name, int dflt) {
+#ifdef DDM_TUNING
     const char* e = getenv(name);
     return e ? atoi(e) : dflt;
+#else
+    (void)name;
+    return dflt;
+#endif
 }
 
 // Waves of the classify pass: one resident round (every wave owns an equal item range and
@@ -1228,6 +1237,7 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
         const bool small = prm->per_batch <= 100;
         const auto cls = perm_map ? (small ? k_scan_batches_classify<true, 7> : k_scan_batches_classify<true, kClsLoads>)
                                   : (small ? k_scan_batches_classify<false, 7> : k_scan_batches_classify<false, kClsLoads>);
+#ifdef DDM_TUNING
         static const bool probe = env_int("DDM_SCAN_PROBE", 0) != 0;
         if (probe)
         {
@@ -1238,6 +1248,7 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
                                *prm, ev, sc.qcnt, sc.q1cnt);
         }
         else
+#endif
             hipLaunchKernelGGL(cls, dim3((unsigned)blocks), dim3(kClsThreads), 0, s, err, n_items, stream_len, nb,
                                nbp, *prm, ev, sc.flags, perm_map, qcap, sc.need, pre, sc.ptab, sc.pst, sc.q,
                                sc.qcnt, sc.q1, sc.q1cnt, sc.pend, cls_steps, cls_pop);

@@ -33,6 +33,8 @@ namespace {
 
 constexpr int kLongMaxBatch = 256;
 constexpr int kLongChunkMax = 64 * kLongMaxBatch;   // rows (= bytes) staged per chunk
+constexpr int32_t kLongFailed = DDM_STOP_FAILED;    // stop of a stream whose look-back gave up
+uint32_t g_spin_limit = 1u << 24;                  // look-back spins before giving up (~1 s)
 
 struct Carry {                 // a chunk's inclusive state (look-back record)
     double p, s, pmin, smin, psmin;
@@ -47,7 +49,7 @@ __global__ __launch_bounds__(64) void k_scan_long(
     int64_t n_streams, int64_t n_chunks, ddm_params P, ddm_state* __restrict__ state,
     const int64_t* __restrict__ batch_base, int32_t* __restrict__ ev, int32_t* __restrict__ stop_out,
     int64_t* __restrict__ nev_out, int mode, const uint8_t* __restrict__ pmap, uint32_t* __restrict__ ticket,
-    int32_t* __restrict__ flag, Carry* __restrict__ carry) {
+    int32_t* __restrict__ flag, Carry* __restrict__ carry, uint32_t spin_limit) {
     __shared__ uint4 sbytes[kLongChunkMax / 16 + 1];
     __shared__ uint64_t smask[kLongChunkMax / 64];
     __shared__ int2 sev[64];
@@ -106,16 +108,21 @@ __global__ __launch_bounds__(64) void k_scan_long(
         __shared__ Carry sin;
         if (lane == 0) {
             // bounded: the predecessor holds an earlier ticket, so it is running; a spin
-            // past ~1 s marks the call failed (ticket[1]) instead of hanging the device
+            // past ~1 s marks the call failed (ticket[1]) instead of hanging the device, and
+            // this chunk publishes a failed carry (stop = kLongFailed) rather than scanning
+            // from a state that was never published
             uint32_t spins = 0;
+            bool gave_up = false;
             while (__hip_atomic_load(cflag + c - 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 24)) {
+                if (++spins > spin_limit) {
                     atomicOr(ticket + 1, 1u);
+                    gave_up = true;
                     break;
                 }
+                __builtin_amdgcn_s_sleep(2);
             }
             sin = ccar[c - 1];
+            if (gave_up) sin.stop = kLongFailed;
         }
         __syncthreads();
         in = sin;
@@ -132,7 +139,8 @@ __global__ __launch_bounds__(64) void k_scan_long(
     d.chg = in.chg;
     d.warn = in.warn;
     int64_t stop = in.stop;
-    bool stopped = stop >= 0 && mode == 0;
+    const bool failed = stop == kLongFailed;                   // a predecessor's carry never came
+    bool stopped = failed || (stop >= 0 && mode == 0);
 
     int pos = 0;                                               // next row of the chunk
     while (!stopped && pos < rows) {
@@ -208,7 +216,7 @@ __global__ __launch_bounds__(64) void k_scan_long(
     }
     int32_t* evs = ev + 2 * (batch_base[sid] + b0);
     for (int bi = lane; bi < nbc; bi += 64) {
-        int2 e = passthrough ? make_int2(-1, -1) : sev[bi];
+        int2 e = passthrough || failed ? make_int2(-1, -1) : sev[bi];
         if (pmap) {
             const int64_t bs = c0 + (int64_t)bi * pb;
             if (e.x >= 0) e.x = pmap[bs + e.x];
@@ -228,9 +236,9 @@ __global__ __launch_bounds__(64) void k_scan_long(
         st.sample_count = outc.n;
         st.in_concept_change = outc.chg;
         st.in_warning_zone = outc.warn;
-        state[sid] = st;
-        if (stop_out) stop_out[sid] = (int32_t)outc.stop;
-        if (nev_out) nev_out[sid] = outc.nev;
+        if (!failed) state[sid] = st;
+        if (stop_out) stop_out[sid] = failed ? kLongFailed : (int32_t)outc.stop;
+        if (nev_out) nev_out[sid] = failed ? 0 : outc.nev;
     }
 }
 
@@ -282,9 +290,14 @@ extern "C" int ddm_scan_long(const uint8_t* err, const int64_t* stream_off, cons
         return rc;
     hipLaunchKernelGGL(k_scan_long, dim3((unsigned)grid), dim3(64), 0, s, err, stream_off, stream_end, n_streams,
                        n_chunks, *prm, state_io, batch_base, ev_out, stop_out, nev_out, (int)mode, perm_map,
-                       sc.ticket, sc.flag, sc.carry);
+                       sc.ticket, sc.flag, sc.carry, g_spin_limit);
     if (int rc = ddm::launch_status("ddm_scan_long")) return rc;
     if (ev_end)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
+    return 0;
+}
+
+extern "C" int ddm_scan_long_set_spin_limit(uint32_t spins) {
+    g_spin_limit = spins;
     return 0;
 }

@@ -30,7 +30,7 @@ import pandas as pd
 import torch
 
 from . import dfit, kernels
-from ._capi import DdmEpoch, check, lib
+from ._capi import DDM_STOP_FAILED, DdmEpoch, check, lib
 from .forest import upload_forests
 from .params import OUTPUT_COLUMNS, DDMSettings, infer_x_features
 from .rng import MTStream
@@ -1157,6 +1157,11 @@ class BatchRunner:
                 st.dfit_ms += self.t_fit.elapsed_ms()
         # the control block as Python ints, one conversion per array
         stops, nevs, picks = self.stop_h.tolist(), self.nev_h.tolist(), self.pick_h.tolist()
+        if long_rows:
+            bad = [ps.i for ps in live if stops[ps.i] == DDM_STOP_FAILED]
+            if bad:
+                raise RuntimeError(f"ddm_scan_long gave up waiting for a carried state (partitions {bad}): the "
+                                   "epoch's results are void")
         infos = self._info_all.tolist()
         # read-backs beyond the staging (more events than it holds): rare
         pending = False

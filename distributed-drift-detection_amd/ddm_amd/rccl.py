@@ -59,18 +59,52 @@ class RcclComm:
     torch.distributed Store shared by the ranks (e.g. the default group's); rank 0 puts
     the unique id there under `key`."""
 
-    def __init__(self, rank, world, device, store, key="ddm_amd_rccl_id"):
+    _serial = 0
+
+    def __init__(self, rank, world, device, store, key=None, agree=None):
+        """agree(ok: bool) -> bool: a collective AND over the ranks (None: no agreement
+        step).  With it every rank learns whether all ranks got the unique id before any
+        of them enters ncclCommInitRank (which blocks until all ranks join), and whether
+        all of them initialised, so that the ranks fall back together."""
         self.rank, self.world, self.device = int(rank), int(world), device
-        uid = NcclUniqueId()
-        if self.rank == 0:
-            _check(lib().ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
-            store.set(key, bytes(uid.internal))
-        else:
-            raw = store.get(key)
-            ctypes.memmove(ctypes.byref(uid), raw, NCCL_UNIQUE_ID_BYTES)
+        if key is None:             # one key per communicator: a second one never reads a stale id
+            RcclComm._serial += 1
+            key = f"ddm_amd_rccl_id/{RcclComm._serial}"
         self.comm = ctypes.c_void_p()
-        with torch.cuda.device(device):
-            _check(lib().ncclCommInitRank(ctypes.byref(self.comm), self.world, uid, self.rank), "ncclCommInitRank")
+        uid = NcclUniqueId()
+        err = None
+        if self.rank == 0:
+            try:
+                _check(lib().ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
+                store.set(key, bytes(uid.internal))
+            except Exception as e:  # noqa: BLE001  (the other ranks must not wait for the id)
+                err = e
+                store.set(key, b"")
+        else:
+            try:
+                lib()
+            except OSError as e:
+                err = e
+            raw = store.get(key)
+            if len(raw) != NCCL_UNIQUE_ID_BYTES:
+                err = err or RcclError("rank 0 could not create the RCCL unique id")
+            else:
+                ctypes.memmove(ctypes.byref(uid), raw, NCCL_UNIQUE_ID_BYTES)
+        if agree is not None and not agree(err is None):
+            raise err or RcclError("another rank could not set up RCCL")
+        if err is not None:
+            raise err
+        try:
+            with torch.cuda.device(device):
+                _check(lib().ncclCommInitRank(ctypes.byref(self.comm), self.world, uid, self.rank),
+                       "ncclCommInitRank")
+        except Exception as e:      # noqa: BLE001
+            err = e
+        if agree is not None and not agree(err is None):
+            self.close()
+            raise err or RcclError("ncclCommInitRank failed on another rank")
+        if err is not None:
+            raise err
 
     def all_gather(self, send, recv, stream=None):
         """recv[world * n] <- every rank's send[n] (device tensors, same dtype), on `stream`."""
@@ -91,4 +125,11 @@ class RcclComm:
         import torch.distributed as dist
         from torch.distributed import distributed_c10d as c10d
         store = c10d._get_default_store()
-        return cls(dist.get_rank(), dist.get_world_size(), device, store)
+        on = device if dist.get_backend() == "nccl" else torch.device("cpu")
+
+        def agree(ok):
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=on)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            return bool(t.item())
+
+        return cls(dist.get_rank(), dist.get_world_size(), device, store, agree=agree)

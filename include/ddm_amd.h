@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 13
+#define DDM_AMD_ABI_VERSION 14
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -266,12 +266,17 @@ int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t stream_len, 
  * (-1 where none), never memset as a whole; max_rows bounds every stream's length (grid
  * size); per_batch must be 1..256; scratch is ddm_scan_long_scratch_bytes(...) bytes of
  * device memory, 256-byte aligned (its second uint32 is set to 1 if a chunk ever gave up
- * waiting for its predecessor, i.e. the results are void). */
+ * waiting for its predecessor).  A stream whose look-back gave up gets stop_out =
+ * DDM_STOP_FAILED, nev_out = 0, events -1 and its state untouched: its results are void
+ * and the caller must fail (or rescan it another way), never use them. */
+#define DDM_STOP_FAILED (-2)
 int64_t ddm_scan_long_scratch_bytes(int64_t n_streams, int64_t max_rows, int32_t per_batch);
 int ddm_scan_long(const uint8_t* err, const int64_t* stream_off, const int64_t* stream_end, int64_t n_streams,
                   int64_t max_rows, const ddm_params* prm, ddm_state* state_io, const int64_t* batch_base,
                   int32_t* ev_out, int32_t* stop_out, int64_t* nev_out, int32_t mode, const uint8_t* perm_map,
                   void* scratch, ddm_stream_t stream, ddm_event_t ev_begin, ddm_event_t ev_end);
+/* Test hook: look-back spins before a chunk gives up (default 2^24, about 1 s). */
+int ddm_scan_long_set_spin_limit(uint32_t spins);
 
 /* Timing events for the ev_begin / ev_end arguments (hipEventCreate / Destroy /
  * ElapsedTime; elapsed needs both events completed, e.g. after a stream sync). */

@@ -25,11 +25,13 @@ def _port():
     return p
 
 
-def _bench(n, extra):
+def _bench(n, extra, self_launch=False):
     args = ["bench.py", "--gpus", str(n), "--steps", "1", "--warmup", "0", "--cpu-baseline", "0",
-            "--oracle-check-rows", "0"] + extra
+            "--oracle-check-rows", "0", "--companion", "0"] + extra
     env = dict(os.environ, DDM_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
-    if n == 1:
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    if n == 1 or self_launch:
         cmd = [sys.executable] + args
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
@@ -56,3 +58,28 @@ def test_events_do_not_depend_on_gpu_count(workload, extra):
     assert one["scaling"] == two["scaling"] == "strong"
     if workload == "c5":
         assert two["breakdown"]["gather_ms_per_step"] is not None
+
+
+def test_bench_launches_its_own_ranks():
+    """`bench.py --gpus 2` with no launcher starts 2 ranks itself (torch.distributed.run,
+    before touching the GPU): n_gpus 2 and the events of the N=1 run."""
+    import torch
+    assert not torch.cuda.is_initialized()
+    extra = ["--workload", "c3", "--rows-per-part", "1000000", "--block-rows", "500037"]
+    one = _bench(1, extra)
+    two = _bench(2, extra, self_launch=True)
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert two["breakdown"]["checks"]["events_sha1"] == one["breakdown"]["checks"]["events_sha1"]
+
+
+@pytest.mark.parametrize("mult,inst", [(2, 16), (2, 1), (4, 4)])
+def test_bench_c2_matches_reference_fixtures(mult, inst):
+    """configs[1] (outdoorStream) as the bench times it: every partition's events == the
+    reference-executed fixture, and vs_baseline against the matching published cell."""
+    import torch
+    assert not torch.cuda.is_initialized()
+    r = _bench(1, ["--workload", "c2", "--c2-mult", str(mult), "--c2-instances", str(inst)])
+    assert "fixtures" in r["breakdown"]["checks"]
+    assert r["config"]["rows_per_step"] == 4000 * mult
+    assert r["vs_baseline"] is not None and r["vs_baseline"] > 1
+    assert r["roofline"]["kernel"] == "ddm_forest_predict"

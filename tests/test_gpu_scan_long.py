@@ -175,3 +175,38 @@ def test_controller_routes_long_carried_windows(refit):
     after = np.random.get_state()
     assert np.array_equal(rng.key, after[1]) and rng.pos.value == after[2]
     assert runner.stats.long_scans >= 2 and n > 2 * LONG_SCAN_MIN_ROWS
+
+
+def test_look_back_give_up_is_reported_not_silent():
+    """With the look-back spin limit at 0 a chunk whose predecessor has not published gives
+    up at once: that stream must come back as DDM_STOP_FAILED (events -1, state untouched),
+    never as results scanned from a carry that was never published."""
+    from ddm_amd import _capi, kernels
+    dev = _dev()
+    n = 1_000_000
+    e = thinning_stream(n, 1.6)
+    pad = np.zeros(n + 32, np.uint8)
+    pad[:n] = e
+    err = torch.from_numpy(pad).to(dev)
+    prm = kernels.params_struct(3, 100)
+    st0 = kernels.fresh_states(1)
+    st = torch.from_numpy(st0.view(np.uint8).copy()).to(dev)
+    ev = torch.full(((n + 99) // 100, 2), -7, dtype=torch.int32, device=dev)
+    stop = torch.full((1,), -7, dtype=torch.int32, device=dev)
+    nev = torch.full((1,), -7, dtype=torch.int64, device=dev)
+    scratch = torch.empty(kernels.scan_long_scratch_size(1, n, 100), dtype=torch.uint8, device=dev)
+    off = torch.tensor([0, n], dtype=torch.int64, device=dev)
+    base = torch.zeros(1, dtype=torch.int64, device=dev)
+    _capi.lib.ddm_scan_long_set_spin_limit(0)
+    try:
+        kernels.scan_long(err, off, prm, st, base, ev, n, scratch, stop=stop, nev=nev, mode=0)
+        torch.cuda.synchronize()
+    finally:
+        _capi.lib.ddm_scan_long_set_spin_limit(1 << 24)
+    gave_up = int(scratch[4:8].view(torch.int32).item())
+    if gave_up:
+        assert int(stop.item()) == _capi.DDM_STOP_FAILED and int(nev.item()) == 0
+        assert np.array_equal(st.cpu().numpy().view(np.uint8), st0.view(np.uint8))
+    else:       # every predecessor happened to publish in time: the results must be exact
+        ref = gpu_scan_long(e, np.array([0, n]), mode=0)
+        assert np.array_equal(ev.cpu().numpy(), ref[0])
