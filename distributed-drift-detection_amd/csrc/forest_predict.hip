@@ -700,7 +700,7 @@ cf_arg_fn pick_cf_arg(int vk, int rows) {
 // LDS of the compiled path (cf_segment / cf_segment_vec): column pointers + rank tables
 // + labels + classes + err + leaf classes + row slots [kRows][slots rounded to 8][512]
 // when the forest has general trees (leaves > 0).
-size_t cf_lds_bytes(int leaves, int slots, int tab_words, int kRows) {
+__host__ __device__ size_t cf_lds_bytes(int leaves, int slots, int tab_words, int kRows) {
     const size_t slots8 = (size_t)((slots + kChunk - 1) & ~(kChunk - 1));
     return 8 * 32 + (size_t)4 * ((tab_words + 3) & ~3) + (size_t)4 * kRows * kCfThreads + 64 +
            (size_t)kRows * kCfThreads + (size_t)((leaves + 15) & ~15) +
@@ -716,6 +716,66 @@ bool cf_usable(const Seg& g, int pb) {
 }
 
 // ---------------------------------------------------------------------------------
+// The device-resident runner's predict (csrc/ctl.hip): one launch with a fixed grid; the
+// segment table and its block split were written on the device, and a segment whose
+// forest is a device refit (res[s] != NULL) takes the compiled forest's shape from the
+// refit's result words.  A forest that cannot run here (the refit reported a status, did
+// not compile, or needs more LDS than the launch has) sets stall[s]: the partition waits
+// for the host, which refits or walks it.
+constexpr size_t kDevLds = 80 * 1024;
+
+__device__ __forceinline__ int cf_rows_dev(const Seg& g, int pb) {
+    if (g.cf_leaves > 0) return 1;
+    const bool aligned = pb % 4 == 0 && g.ld % 4 == 0 && g.row_base % 4 == 0 &&
+                         ((reinterpret_cast<uintptr_t>(g.X) | reinterpret_cast<uintptr_t>(g.y)) & 15) == 0 &&
+                         ((reinterpret_cast<uintptr_t>(g.perm) | reinterpret_cast<uintptr_t>(g.err)) & 3) == 0;
+    return aligned ? kVecRows : 2;
+}
+
+__global__ __launch_bounds__(kCfThreads) void k_cforest_predict_dev(const Seg* __restrict__ segs,
+                                                                    const int64_t* const* __restrict__ res,
+                                                                    int n_segs, int pb, int32_t* __restrict__ stall) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int64_t gb = blockIdx.x;
+    int s = 0;
+    while (s < n_segs && !(ldu(&segs[s].block0) <= gb && gb < ldu(&segs[s].block0) + ldu(&segs[s].nblocks))) ++s;
+    if (s == n_segs) return;
+    Seg sg = ldu(segs + s);
+    if (sg.pos_end <= sg.pos_begin) return;
+    const int64_t* r = ldu(res + s);
+    if (r) {       // the refit's result words (written by an earlier kernel: read-only here)
+        sg.n_classes = (int32_t)ldu(r + DDM_DFIT_CLASSES);
+        sg.n_nodes = (int32_t)ldu(r + DDM_DFIT_NODES);
+        sg.pure = (int32_t)ldu(r + DDM_DFIT_PURE);
+        sg.cf_slots = (int32_t)ldu(r + DDM_DFIT_CF_SLOTS);
+        sg.cf_vote_regs = (int32_t)ldu(r + DDM_DFIT_CF_VR);
+        sg.cf_leaves = (int32_t)ldu(r + DDM_DFIT_CF_LEAVES);
+        sg.cf_tab_words = (int32_t)ldu(r + DDM_DFIT_CF_TAB);
+        if (ldu(r + DDM_DFIT_STATUS) != 0 || ldu(r + DDM_DFIT_BLOB) <= 0) sg.cforest = nullptr;
+    }
+    const int rows = cf_rows_dev(sg, pb);
+    const bool usable = sg.cforest && sg.cf_slots >= 0 && sg.cf_slots <= 32 && sg.cf_vote_regs >= 1 &&
+                        sg.cf_vote_regs <= 4 && sg.cf_tab_words >= 0 && sg.pos_begin % pb == 0 &&
+                        cf_lds_bytes(sg.cf_leaves, sg.cf_slots, sg.cf_tab_words, rows) <= kDevLds;
+    if (!usable) {
+        if (threadIdx.x == 0) stall[s] = 1;
+        return;
+    }
+    const int64_t blk = gb - sg.block0, nblk = sg.nblocks;
+    const int vk = sg.cf_vote_regs <= 1 ? 0 : sg.cf_vote_regs <= 2 ? 1 : 2;
+    switch (3 * (rows == 1 ? 0 : rows == 2 ? 1 : 2) + vk) {
+        case 0: cf_dispatch<1, 1>(sg, blk, nblk, pb, smem); break;
+        case 1: cf_dispatch<2, 1>(sg, blk, nblk, pb, smem); break;
+        case 2: cf_dispatch<4, 1>(sg, blk, nblk, pb, smem); break;
+        case 3: cf_dispatch<1, 2>(sg, blk, nblk, pb, smem); break;
+        case 4: cf_dispatch<2, 2>(sg, blk, nblk, pb, smem); break;
+        case 5: cf_dispatch<4, 2>(sg, blk, nblk, pb, smem); break;
+        case 6: cf_dispatch<1, kVecRows>(sg, blk, nblk, pb, smem); break;
+        case 7: cf_dispatch<2, kVecRows>(sg, blk, nblk, pb, smem); break;
+        default: cf_dispatch<4, kVecRows>(sg, blk, nblk, pb, smem); break;
+    }
+}
+
 using predict_fn = void (*)(Seg, int64_t);
 using predict_batch_fn = void (*)(const Seg*, int, int64_t, int64_t);
 
@@ -907,6 +967,25 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
         }
         if (int rc = ddm::launch_status("ddm_forest_predict_batch")) return rc;
     }
+    if (ev_end)
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
+    return 0;
+}
+
+extern "C" int ddm_forest_predict_dev(const ddm_predict_segment* segs_dev, const int64_t* const* res_dev,
+                                      int32_t n_segs, int32_t per_batch, int64_t grid, int32_t* stall,
+                                      ddm_stream_t stream, ddm_event_t ev_begin, ddm_event_t ev_end) {
+    if (!segs_dev || !res_dev || !stall || n_segs <= 0 || per_batch <= 0 || per_batch > 256 || grid <= 0 ||
+        grid >= ((int64_t)1 << 31)) {
+        ddm::set_error("ddm_forest_predict_dev: invalid argument");
+        return DDM_E_ARG;
+    }
+    hipStream_t s = ddm::as_hip(stream);
+    if (ev_begin)
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
+    hipLaunchKernelGGL(k_cforest_predict_dev, dim3((unsigned)grid), dim3(kCfThreads), kDevLds, s,
+                       reinterpret_cast<const Seg*>(segs_dev), res_dev, (int)n_segs, (int)per_batch, stall);
+    if (int rc = ddm::launch_status("ddm_forest_predict_dev")) return rc;
     if (ev_end)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
     return 0;

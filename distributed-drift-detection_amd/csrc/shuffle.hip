@@ -570,16 +570,39 @@ __global__ __launch_bounds__(kWalkThreads) void k_fsm_walk_batch(const Job* __re
 // first chunk) is replayed by lane 0; a chunk piece starts on a chunk boundary, so lane t
 // reads sub-chunk t's start state and batch straight from the prefix tables and every
 // lane replays its sub-chunk from HBM, 16 draws per round of loads: for each accepted draw
-// of batch b < W record J[b*L + s] = v & mask(s) and, when s == 1, E[b] = draw index.
+// of batch b < W the interval's j (v & mask(s)) is recorded and, when s == 1, E[b] = draw
+// index.  Where a j goes: the batches that begin and end inside one chunk piece (nearly all
+// of a window) are recorded in LDS and shuffled by the piece's own wave, which then writes
+// their perm bytes contiguously; the others (the batches of the window's first chunk, cut
+// into sub-chunk pieces, and the batch that straddles each chunk boundary) go to J in HBM
+// for k_fsm_perms_batch.  J[b*L] (interval 0 never draws) tells k_fsm_perms_batch which:
+// 1 = shuffled by the replay, 0 = its job.
 constexpr int kReplayBatch = 16;
 
-__device__ __forceinline__ void replay_step(uint32_t v, int64_t q, uint32_t& s, int64_t& b, uint32_t S, int L,
-                                            uint8_t* __restrict__ J, int64_t* __restrict__ E) {
+struct ReplaySink {
+    uint8_t* J;
+    int64_t* E;
+    uint8_t* Jl;          // LDS rows of batches [b_lo, b_hi)
+    int64_t b_lo, b_hi;
+    int L;
+    __device__ __forceinline__ bool local(int64_t b) const { return b >= b_lo && b < b_hi; }
+    __device__ __forceinline__ void rec(int64_t b, uint32_t s, uint8_t m) const {
+        if (local(b)) Jl[(b - b_lo) * L + s] = m;
+        else J[b * L + s] = m;
+    }
+    __device__ __forceinline__ void done(int64_t b, int64_t q) const {
+        E[b] = q;
+        if (!local(b)) J[b * L] = 0;
+    }
+};
+
+__device__ __forceinline__ void replay_step(uint32_t v, int64_t q, uint32_t& s, int64_t& b, uint32_t S,
+                                            const ReplaySink& k) {
     const uint32_t m = v & imask(s);
     if (m <= s) {
-        J[b * L + s] = (uint8_t)m;
+        k.rec(b, s, (uint8_t)m);
         if (s == 1) {
-            E[b] = q;
+            k.done(b, q);
             s = S;
             ++b;
         } else {
@@ -589,8 +612,7 @@ __device__ __forceinline__ void replay_step(uint32_t v, int64_t q, uint32_t& s, 
 }
 
 __device__ __forceinline__ void replay_range(const uint32_t* __restrict__ R, int64_t beg, int64_t fin, uint32_t s,
-                                             int64_t b, int64_t W, int L, uint8_t* __restrict__ J,
-                                             int64_t* __restrict__ E) {
+                                             int64_t b, int64_t W, int L, const ReplaySink& k) {
     const uint32_t S = (uint32_t)(L - 1);
     if (fin - beg == kSub && (beg & 3) == 0) {
         // a whole sub-chunk: 64 words at a time in flight (sixteen 16-byte loads)
@@ -598,14 +620,14 @@ __device__ __forceinline__ void replay_range(const uint32_t* __restrict__ R, int
         for (int h = 0; h < kSub / 64 && b < W; ++h) {
             uint4 v[16];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) v[k] = src[16 * h + k];
+            for (int q = 0; q < 16; ++q) v[q] = src[16 * h + q];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int64_t q = beg + 64 * h + 4 * k;
-                if (b < W) replay_step(v[k].x, q, s, b, S, L, J, E);
-                if (b < W) replay_step(v[k].y, q + 1, s, b, S, L, J, E);
-                if (b < W) replay_step(v[k].z, q + 2, s, b, S, L, J, E);
-                if (b < W) replay_step(v[k].w, q + 3, s, b, S, L, J, E);
+            for (int q = 0; q < 16; ++q) {
+                const int64_t d = beg + 64 * h + 4 * q;
+                if (b < W) replay_step(v[q].x, d, s, b, S, k);
+                if (b < W) replay_step(v[q].y, d + 1, s, b, S, k);
+                if (b < W) replay_step(v[q].z, d + 2, s, b, S, k);
+                if (b < W) replay_step(v[q].w, d + 3, s, b, S, k);
             }
         }
         return;
@@ -613,27 +635,45 @@ __device__ __forceinline__ void replay_range(const uint32_t* __restrict__ R, int
     for (int64_t q0 = beg; q0 < fin && b < W; q0 += kReplayBatch) {
         uint32_t v[kReplayBatch];
 #pragma unroll
-        for (int k = 0; k < kReplayBatch; ++k) v[k] = R[min(q0 + k, fin - 1)];
+        for (int q = 0; q < kReplayBatch; ++q) v[q] = R[min(q0 + q, fin - 1)];
 #pragma unroll
-        for (int k = 0; k < kReplayBatch; ++k)
-            if (q0 + k < fin && b < W) replay_step(v[k], q0 + k, s, b, S, L, J, E);
+        for (int q = 0; q < kReplayBatch; ++q)
+            if (q0 + q < fin && b < W) replay_step(v[q], q0 + q, s, b, S, k);
     }
 }
 
+// LDS of the fused replay: the j rows and the perms of a chunk piece's own batches (a
+// batch takes at least L-1 draws, so a chunk holds at most kChunk / (L-1) + 1 of them)
+__host__ __device__ inline int replay_local_batches(int L) { return (int)(kChunk / (L - 1)) + 2; }
+size_t replay_lds_bytes(int L) { return ((size_t)2 * replay_local_batches(L) * L + 15) & ~(size_t)15; }
+
+template <bool kFused>
 __device__ void fsm_replay(const uint32_t* __restrict__ R, const uint32_t* __restrict__ Tpre,
                            const ChunkStart* __restrict__ pieces, const int64_t* __restrict__ info, int64_t W, int L,
-                           uint8_t* __restrict__ J, int64_t* __restrict__ E, int64_t blk, int64_t nblk) {
+                           uint8_t* __restrict__ J, int64_t* __restrict__ E, uint8_t* __restrict__ perm_out,
+                           int64_t blk, int64_t nblk) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t rlds[];
     const int64_t npieces = info[0], end = info[1];
     const int S = L - 1;
     const int lane = threadIdx.x;
+    const int cap = replay_local_batches(L);
     for (int64_t pc = blk; pc < npieces; pc += nblk) {
         const ChunkStart c = pieces[pc];
         const int64_t stop = (pc + 1 < npieces) ? pieces[pc + 1].pos : end;
         if (stop <= c.pos) continue;
         if (stop - c.pos <= kSub) {
-            if (lane == 0) replay_range(R, c.pos, stop, (uint32_t)c.state, c.batch, W, L, J, E);
+            const ReplaySink k{J, E, nullptr, 0, 0, L};
+            if (lane == 0) replay_range(R, c.pos, stop, (uint32_t)c.state, c.batch, W, L, k);
             continue;
         }
+        // this piece's own batches: those that start in it and end in it
+        int64_t b_lo = 0, b_hi = 0;
+        if (kFused) {
+            b_lo = c.batch + (c.state != S ? 1 : 0);
+            b_hi = min(W, (pc + 1 < npieces) ? (int64_t)pieces[pc + 1].batch : W);
+            b_hi = max(b_lo, min(b_hi, b_lo + cap));
+        }
+        const ReplaySink k{J, E, rlds, b_lo, b_hi, L};
         const int64_t chunk = c.pos / kChunk;        // c.pos % kChunk == 0 (a chunk piece)
         const int nsub = (int)((stop - c.pos + kSub - 1) / kSub);
         for (int t = lane; t < nsub; t += 64) {
@@ -644,21 +684,51 @@ __device__ void fsm_replay(const uint32_t* __restrict__ R, const uint32_t* __res
                 s = e & 0xffu;
                 b += e >> 8;
             }
-            replay_range(R, c.pos + (int64_t)t * kSub, min(stop, c.pos + (int64_t)(t + 1) * kSub), s, b, W, L, J, E);
+            replay_range(R, c.pos + (int64_t)t * kSub, min(stop, c.pos + (int64_t)(t + 1) * kSub), s, b, W, L, k);
         }
+        if (!kFused) continue;
+        const int nloc = (int)(b_hi - b_lo);
+        uint8_t* Pl = rlds + (size_t)cap * L;
+        __syncthreads();
+        // Fisher-Yates of every own batch: lane k applies batch k's swaps i = L-1 .. 1
+        for (int q = lane; q < nloc; q += 64) {
+            uint8_t* p = Pl + (size_t)q * L;
+            const uint8_t* jr = rlds + (size_t)q * L;
+            for (int e = 0; e < L; ++e) p[e] = (uint8_t)e;
+            for (int i = L - 1; i >= 1; --i) {
+                const int jj = jr[i];
+                const uint8_t tmp = p[i];
+                p[i] = p[jj];
+                p[jj] = tmp;
+            }
+            J[(b_lo + q) * L] = 1;
+        }
+        __syncthreads();
+        // their perm bytes, contiguous in the window
+        uint8_t* dst = perm_out + b_lo * L;
+        const int nbytes = nloc * L;
+        if ((reinterpret_cast<uintptr_t>(dst) & 3) == 0) {
+            const int nw = nbytes >> 2;
+            for (int e = lane; e < nw; e += 64)
+                reinterpret_cast<uint32_t*>(dst)[e] = reinterpret_cast<const uint32_t*>(Pl)[e];
+            for (int e = 4 * nw + lane; e < nbytes; e += 64) dst[e] = Pl[e];
+        } else {
+            for (int e = lane; e < nbytes; e += 64) dst[e] = Pl[e];
+        }
+        __syncthreads();
     }
 }
 
 __global__ __launch_bounds__(64) void k_fsm_replay(Job j, int L) {
-    fsm_replay(j.R, j.Tpre, reinterpret_cast<const ChunkStart*>(j.pieces), j.info, j.W, L, j.J, j.E, blockIdx.x,
-               gridDim.x);
+    fsm_replay<false>(j.R, j.Tpre, reinterpret_cast<const ChunkStart*>(j.pieces), j.info, j.W, L, j.J, j.E, nullptr,
+                      blockIdx.x, gridDim.x);
 }
 
 __global__ __launch_bounds__(64) void k_fsm_replay_batch(const Job* __restrict__ jobs, int L) {
     const Job j = jobs[blockIdx.y];
     if (j.W <= 0) return;
-    fsm_replay(j.R, j.Tpre, reinterpret_cast<const ChunkStart*>(j.pieces), j.info, j.W, L, j.J, j.E, blockIdx.x,
-               gridDim.x);
+    fsm_replay<true>(j.R, j.Tpre, reinterpret_cast<const ChunkStart*>(j.pieces), j.info, j.W, L, j.J, j.E,
+                     j.perm_out, blockIdx.x, gridDim.x);
 }
 
 // One lane per batch: Fisher-Yates swaps i = L-1..1 with the recorded j's.
@@ -666,9 +736,10 @@ __device__ void fsm_perms(const uint8_t* __restrict__ J, int64_t W, int L, uint8
     extern __shared__ uint8_t buf[];
     const int64_t b = b0 + threadIdx.x;
     if (b >= W) return;
+    const uint8_t* j = J + b * L;
+    if (j[0]) return;                    // shuffled by the replay itself (fsm_replay<true>)
     uint8_t* p = buf + threadIdx.x * L;
     for (int k = 0; k < L; ++k) p[k] = (uint8_t)k;
-    const uint8_t* j = J + b * L;
     for (int i = L - 1; i >= 1; --i) {
         const int jj = j[i];
         const uint8_t t = p[i];
@@ -742,8 +813,8 @@ extern "C" int ddm_shuffle_window_batch(const ddm_shuffle_job* jobs_dev, int32_t
                        (int)batch_len);
     if (int rc = ddm::launch_status("ddm_shuffle_window_batch/walk")) return rc;
     const int64_t pblocks = std::max<int64_t>(1, std::min<int64_t>(max_pieces, 2048));
-    hipLaunchKernelGGL(k_fsm_replay_batch, dim3((unsigned)pblocks, (unsigned)n_jobs), dim3(64), 0, s, jobs,
-                       (int)batch_len);
+    hipLaunchKernelGGL(k_fsm_replay_batch, dim3((unsigned)pblocks, (unsigned)n_jobs), dim3(64),
+                       replay_lds_bytes(batch_len), s, jobs, (int)batch_len);
     if (int rc = ddm::launch_status("ddm_shuffle_window_batch/replay")) return rc;
     const int64_t bblocks = std::min<int64_t>(ddm::ceil_div(max_W, 256), 1024);
     hipLaunchKernelGGL(k_fsm_perms_batch, dim3((unsigned)bblocks, (unsigned)n_jobs), dim3(256),

@@ -43,6 +43,10 @@ struct Job {
     int64_t p_now, win, max_win, seg_start, n_full, min_win, next_avail, dpb_x1024;
     int64_t* plan_out;
     ddm_shuffle_job* next_job;
+    int32_t* log;
+    int64_t* log_n;
+    int64_t log_cap;
+    const int32_t* stall;
 };
 static_assert(sizeof(Job) == sizeof(ddm_stage_job), "Job must mirror ddm_stage_job");
 
@@ -107,6 +111,16 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
 #endif
     const Job jb = jobs[blockIdx.x];
     const int t = threadIdx.x;
+    if (jb.stall && *jb.stall) {            // device-resident runner: this partition waits for the host
+        if (t == 0) {
+            jb.info_out[0] = -1;
+            jb.info_out[1] = 0;
+            jb.info_out[2] = 0;
+            jb.info_out[3] = -1;
+            jb.info_out[6] = 0;
+        }
+        return;
+    }
     const int32_t stop = *jb.stop;
     const int64_t last = stop >= 0 ? jb.j + stop : jb.b_end - 1;   // last batch the scan covered
     const int64_t nrows = last - jb.j + 1;                         // window rows of ev to look at
@@ -115,6 +129,9 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     // latency per round), then a block prefix of the per-thread counts places them
     const int lane = t & 63, wv = t >> 6;
     int total = 0;
+    // device-resident runner: records go to the partition's event log (absolute batches)
+    const int64_t log0 = jb.log ? *jb.log_n : 0;
+    const int64_t cap = jb.log ? jb.log_cap - log0 : (int64_t)jb.max_events;
     for (int64_t base = 0; base < nrows; base += 8 * kStageThreads) {
         const int64_t r0 = base + 8 * (int64_t)t;
         int4 q[4];
@@ -153,13 +170,15 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
 #pragma unroll
         for (int w = 0; w < kStageThreads / 64; ++w) round += counts[w];
         int k = before + incl - c;
-        while (bits && k < jb.max_events) {
+        int32_t* out = jb.log ? jb.log + 3 * log0 : jb.ev_out;
+        const int32_t boff = jb.log ? (int32_t)jb.j : 0;
+        while (bits && k < cap) {
             const int s = __builtin_ctz(bits);
             bits &= bits - 1;
             const int4 v = q[s >> 1];
-            jb.ev_out[3 * k] = (int32_t)(r0 + s);
-            jb.ev_out[3 * k + 1] = (s & 1) ? v.z : v.x;
-            jb.ev_out[3 * k + 2] = (s & 1) ? v.w : v.y;
+            out[3 * k] = (int32_t)(r0 + s) + boff;
+            out[3 * k + 1] = (s & 1) ? v.z : v.x;
+            out[3 * k + 2] = (s & 1) ? v.w : v.y;
             ++k;
         }
         total += round;
@@ -168,7 +187,8 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     STAGE_MARK(0);
     if (t == 0) {
         jb.info_out[1] = total;
-        jb.info_out[2] = total > jb.max_events ? 1 : 0;
+        jb.info_out[2] = total > cap ? 1 : 0;
+        if (jb.log) *jb.log_n = log0 + min((int64_t)total, cap);
     }
     if (stop < 0) {
         if (t == 0) {

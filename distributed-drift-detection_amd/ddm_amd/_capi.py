@@ -12,7 +12,7 @@ import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 # DDM_AMD_LIB: an alternative build of the same library (e.g. an instrumented one)
 LIB_PATH = os.environ.get("DDM_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
@@ -61,6 +61,24 @@ class DdmEpoch(ctypes.Structure):
                 ("mid_ev", _vp), ("tail_off", _i64), ("tail_bytes", _i64)]
 _f32, _pi32 = ctypes.c_float, ctypes.POINTER(ctypes.c_int32)
 
+
+class DdmCtl(ctypes.Structure):
+    """ddm_ctl (include/ddm_amd.h): the device-resident runner's tables (device pointers)."""
+    _fields_ = [("parts", _vp), ("n", _i32), ("entry", _i32), ("jobs", _vp), ("segs", _vp), ("seg_res", _vp),
+                ("stage", _vp), ("off", _vp), ("end", _vp), ("state", _vp), ("first", _vp), ("stop", _vp),
+                ("pick", _vp), ("loff", _vp), ("lend", _vp), ("pstall", _vp), ("predict_blocks", _i64),
+                ("status", _vp)]
+
+
+class DdmCtlEpoch(ctypes.Structure):
+    """ddm_ctl_epoch: ddm_ctl_enter / ddm_ctl_epochs."""
+    _fields_ = [("stream", _vp), ("side_stream", _vp), ("fork_ev", _vp), ("join_ev", _vp), ("ctl", DdmCtl),
+                ("ctl_d", _vp), ("n", _i32), ("per_batch", _i32), ("err", _vp), ("params", _vp),
+                ("batch_base", _vp), ("n_batches_total", _i64), ("ev_out", _vp), ("nev", _vp), ("perm_map", _vp),
+                ("long_max_rows", _i64), ("long_scratch", _vp), ("dfit_jobs", _vp), ("n_dfit", _i32),
+                ("max_trees", _i32), ("max_W", _i64), ("max_pieces", _i64), ("status_h_off", _i64),
+                ("ev", _vp * 12)]
+
 # name -> (restype, argtypes); every symbol include/ddm_amd.h declares.
 SIGNATURES = {
     "ddm_abi_version": (ctypes.c_int, []),
@@ -87,6 +105,11 @@ SIGNATURES = {
     "ddm_shuffle_tables": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp]),
     "ddm_shuffle_tables_batch": (ctypes.c_int, [_vp, _i32, _i64, _i32, _vp]),
     "ddm_epoch_launch": (ctypes.c_int, [_vp]),
+    "ddm_ctl_part_bytes": (_i64, []),
+    "ddm_ctl_epoch_bytes": (_i64, []),
+    "ddm_ctl_enter": (ctypes.c_int, [_vp]),
+    "ddm_ctl_epochs": (ctypes.c_int, [_vp, _i32]),
+    "ddm_forest_predict_dev": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i64, _vp, _vp, _vp, _vp]),
     "ddm_epoch_struct_bytes": (_i64, []),
     "ddm_shuffle_window": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
                                           _vp, _vp, _vp]),
@@ -131,6 +154,8 @@ def _load():
         raise ImportError(f"libddm_amd.so ABI {lib.ddm_abi_version()} != {ABI_VERSION}")
     if lib.ddm_epoch_struct_bytes() != ctypes.sizeof(DdmEpoch):
         raise ImportError("ddm_epoch layout differs from the ctypes binding")
+    if lib.ddm_ctl_epoch_bytes() != ctypes.sizeof(DdmCtlEpoch):
+        raise ImportError("ddm_ctl_epoch layout differs from the ctypes binding")
     return lib
 
 

@@ -40,6 +40,8 @@ from .trainer import BatchForestTrainer
 # A window runs on ddm_scan_long when its carried detector is neither fresh nor trivial
 # (every row of it is exact arithmetic) and it spans at least this many rows.
 LONG_SCAN_MIN_ROWS = int(os.environ.get("DDM_LONG_SCAN_ROWS", 4 * 64 * 100))
+# Device-resident epochs (devctl.py) by default; DDM_DEVICE_CTL=0 keeps every epoch on the host path.
+DEVICE_CTL = os.environ.get("DDM_DEVICE_CTL", "0") not in ("", "0")
 
 
 def carried_exact(st):
@@ -158,11 +160,12 @@ def sklearn_refit(settings):
 class RunStats:
     __slots__ = ("epochs", "refits", "predicted_rows", "refit_s", "gpu_s", "host_s", "predict_ms", "predict_bytes",
                  "scan_ms", "scan_rows", "shuffle_ms", "sklearn_refits", "refit_fit_s", "refit_readback_s",
-                 "prep_s", "dfit_ms", "device_refits", "long_scans", "preshuffled")
+                 "prep_s", "dfit_ms", "device_refits", "long_scans", "preshuffled", "device_epochs", "device_phases")
 
     def __init__(self):
         self.epochs = self.refits = self.predicted_rows = self.predict_bytes = self.scan_rows = 0
         self.sklearn_refits = self.device_refits = self.long_scans = self.preshuffled = 0
+        self.device_epochs = self.device_phases = 0
         self.refit_s = self.gpu_s = self.host_s = self.predict_ms = self.scan_ms = self.shuffle_ms = 0.0
         self.refit_fit_s = self.refit_readback_s = self.prep_s = self.dfit_ms = 0.0
 
@@ -208,7 +211,7 @@ class BatchRunner:
     `fit_threads` host threads."""
 
     def __init__(self, parts, settings=None, stream=None, refit="device", timing=False, fit_threads=8,
-                 gen_stream=None, tab_stream=None):
+                 gen_stream=None, tab_stream=None, device_ctl=None):
         self.parts = list(parts)
         if not self.parts:
             raise ValueError("no partitions")
@@ -348,8 +351,12 @@ class BatchRunner:
         # batch, [2] drift batch's shuffle read back
         self.small_h = [[torch.empty(256, dtype=torch.uint8, pin_memory=True) for _ in range(3)] for _ in self.parts]
         self.shuffles = []
+        # stream capacity: the batch shuffles plus room for the refits' seeds (100 draws each;
+        # a refit every 2.25 batches in C5 takes the stream to ~1.3x); device epochs need
+        # every draw a window may ask for inside the buffers (they never regrow there)
+        dev_ctl = (DEVICE_CTL if device_ctl is None else device_ctl) and refit == "device"
         for part, nb, mw in zip(self.parts, self.nbs, self.max_wins):
-            cap = int(nb * expected_draws_per_batch(pb) * 1.2) + 64 * 1024
+            cap = int(nb * expected_draws_per_batch(pb) * (1.45 if dev_ctl else 1.2)) + (128 if dev_ctl else 64) * 1024
             self.shuffles.append(GpuShuffle(dev, pb, cap, mw, self.stream, self.gen_stream, self.tab_stream))
         self.stats = RunStats()
         self._gen_rest = None
@@ -358,6 +365,14 @@ class BatchRunner:
         self._pending_forests = []
         self._E = self._epoch_desc()
         self.trace = [] if _HOST_TRACE else None     # (label, seconds since run start)
+        # device-resident epochs (devctl.py): the epoch decisions on the device, epochs
+        # enqueued ahead; the host path runs the first epoch and whatever the device hands back
+        if device_ctl is None:
+            device_ctl = DEVICE_CTL
+        self.devctl = None
+        if device_ctl and refit == "device":
+            from .devctl import DeviceController
+            self.devctl = DeviceController(self, LONG_SCAN_MIN_ROWS, min(4 * LONG_SCAN_MIN_ROWS, self.long_max_rows))
 
     def _mark(self, label):
         if self.trace is not None:
@@ -696,6 +711,18 @@ class BatchRunner:
         log = self.predict_log or []
         if not log:
             return 0.0, 0
+        dev = [e for e in log if isinstance(e[0], str)]
+        if dev:                                  # device-mode launches (devctl.py)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize(self.device)
+            e0.record(self.stream)
+            for _ in range(repeats):
+                for e in dev:
+                    self.devctl.replay(e, self.stream)
+            e1.record(self.stream)
+            e1.synchronize()
+            n = repeats * len(dev)
+            return e0.elapsed_time(e1) / n, n
         cap = max(k for _, k, _ in log)
         tabs = [kernels.PinnedTable(kernels.SEG_DTYPE, cap, self.device) for _ in log]
         for t, (rec, k, _) in zip(tabs, log):
@@ -803,11 +830,20 @@ class BatchRunner:
             pool = self._pool()
             out_f = [pool.submit(np.full, (ps.nb - 1, 2), -1, np.int64) for ps in pss]
             self._mark("batch-0 shuffles")
+            host_epochs = 0
             while True:
                 live = [ps for ps in pss if not ps.done]
                 if not live:
                     break
+                if self.devctl is not None and host_epochs and self.devctl.eligible(live):
+                    # device epochs until the partitions are done or need the host again
+                    self.devctl.run_phase(live)
+                    self._forked = False
+                    host_epochs = 0
+                    self._mark("device phase")
+                    continue
                 self._epoch(live)
+                host_epochs += 1
             self._finish_pending()
             outs = []
             for ps, f in zip(pss, out_f):

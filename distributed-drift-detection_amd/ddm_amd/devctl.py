@@ -1,0 +1,374 @@
+"""Device-resident epochs for the BatchRunner (csrc/ctl.hip).
+
+The BatchRunner (controller.py) runs run_DDM_loop (DDM_Process.py:170-213) for many
+partitions in lockstep epochs.  On the host path every epoch ends in a read-back: the host
+learns where each partition's scan stopped, moves its RNG position, plans the next window
+and builds the next epoch's tables.  Here those decisions (BatchRunner._refit_prep's device
+branch, _epoch's window and _epoch_after) are taken by k_ctl on the device, so the host
+enqueues groups of epochs ahead and only polls the partitions' records between groups:
+
+    host:    enter (upload the records, plan + shuffle the first windows)
+             [K epochs][K epochs] ... poll the records of the group before the last one
+    device:  predict -> scan (+ long scan) -> pick -> staging (events into a per-partition
+             log, batch d+1's shuffle, the refit's seeds) -> k_ctl (decisions, next tables)
+             -> next windows' shuffles (side stream) | device refits -> ...
+
+A partition the device cannot carry on alone stalls (a refit that reported a status or did
+not compile, stream words that ran out) or parks (a short last batch still to shuffle);
+the phase ends, the host takes the records back into its own per-partition state and runs
+one host epoch (which handles them exactly as before), then the runner re-enters device
+mode.  The decisions are the host's, line for line, so results do not depend on the mode
+(tests/test_gpu_devctl.py).
+"""
+import ctypes
+import time
+
+import numpy as np
+import torch
+
+from . import dfit, kernels
+from ._capi import DdmCtlEpoch, check, lib
+from .shuffle import CHUNK, expected_draws_per_batch
+
+CTL = kernels.CTL_PART_DTYPE
+_OFF = {name: CTL.fields[name][1] for name in CTL.names}
+PREDICT_BLOCKS = 2048
+GROUP = 4                       # epochs per enqueued group
+
+
+class DeviceController:
+    """The device-mode state of one BatchRunner (its buffers never move)."""
+
+    def __init__(self, runner, long_min_rows, long_cap_rows):
+        r = runner
+        self.r = r
+        n, dev = len(r.parts), r.device
+        self.n = n
+        self.parts_d = torch.zeros(n * CTL.itemsize, dtype=torch.uint8, device=dev)
+        self.parts_h = torch.zeros(n * CTL.itemsize, dtype=torch.uint8, pin_memory=True)
+        self.rec = self.parts_h.numpy().view(CTL)
+        # two pinned copies of the records for the polls (one in flight, one read)
+        self.poll_h = [torch.zeros(n * CTL.itemsize, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        self.res_ptrs = torch.zeros(n, dtype=torch.int64, device=dev)
+        self.pstall = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.logs = [torch.empty(3 * max(1, nb), dtype=torch.int32, device=dev) for nb in r.nbs]
+        self.avail_h = torch.zeros(64 * n, dtype=torch.int64, pin_memory=True)   # H2D sources (a ring)
+        self._avail_k = 0
+        self.long_min_rows, self.long_cap_rows = int(long_min_rows), int(long_cap_rows)
+        self.timers = []             # per-epoch HIP event pairs when the runner times kernels
+        self.seg_log = None          # (segs, res) device copies per epoch when the runner logs predicts
+        self._E = None
+
+    # ---------------------------------------------------------------- eligibility
+    def eligible(self, live):
+        """Device epochs need device refits, compiled forests and no host-staged refit."""
+        r = self.r
+        if not r.dfit_rows:
+            return False
+        for ps in live:
+            if ps.retrain:
+                if not (ps.staged is not None and isinstance(ps.staged[0], str)):
+                    return False
+                continue
+            f = ps.forest
+            if isinstance(f, dfit.DeviceFitForest):
+                if not f.compiled:
+                    return False
+            elif f is None or not getattr(f, "compiled", False) or f.desc.cf_slots > 32:
+                return False
+        return True
+
+    # ---------------------------------------------------------------- records
+    def _epoch_struct(self):
+        if self._E is not None:
+            return self._E
+        r = self.r
+        E = DdmCtlEpoch()
+        base = r.ctrl_d.data_ptr()
+        E.stream, E.side_stream = r.stream.cuda_stream, r.side_stream.cuda_stream
+        E.fork_ev, E.join_ev = r._fork_ev.value, r._join_ev.value
+        c = E.ctl
+        c.parts, c.n, c.entry = self.parts_d.data_ptr(), self.n, 0
+        c.jobs, c.segs, c.seg_res, c.stage = r.jobs.d.data_ptr(), r.segs.d.data_ptr(), self.res_ptrs.data_ptr(), \
+            r.stage_jobs.d.data_ptr()
+        c.off, c.end, c.state, c.first = base + r.o_off, base + r.o_end, base + r.o_state, base + r.o_first
+        c.stop, c.pick, c.loff, c.lend = base + r.o_stop, base + r.o_pick, base + r.o_loff, base + r.o_lend
+        c.pstall, c.predict_blocks, c.status = self.pstall.data_ptr(), PREDICT_BLOCKS, None
+        E.n, E.per_batch = self.n, r.s.per_batch
+        E.err, E.params, E.batch_base = r.err_all.data_ptr(), ctypes.addressof(r.params), base + r.o_bbase
+        E.n_batches_total, E.ev_out, E.nev, E.perm_map = r.ev_total, r.ev_d.data_ptr(), base + r.o_nev, \
+            r.perm_all.data_ptr()
+        E.long_max_rows, E.long_scratch = self.long_cap_rows, r.long_scratch.data_ptr()
+        E.dfit_jobs, E.n_dfit, E.max_trees = r.dfit_jobs.d.data_ptr(), self.n, r.s.n_estimators
+        mw = max(r.max_wins)
+        E.max_W = mw
+        E.max_pieces = 2 + 64 + r.shuffles[0].window_draws(mw) // 8192
+        self._E = E
+        return E
+
+    def _write_records(self, live):
+        """The records of every partition (static templates + the host state of the live ones)."""
+        r = self.r
+        t = r._stream_ptrs(live)
+        t = r._templates()
+        pb, T = r.s.per_batch, r.s.n_estimators
+        rec = self.rec
+        rec[:] = np.zeros(1, CTL)
+        base_d = self.parts_d.data_ptr()
+        nlog = _OFF["n_log"]
+        lo = max(1, min(r.s.window_batches, r.s.drift_window_batches))
+        for i, part in enumerate(r.parts):
+            q = rec[i]
+            q["job"] = t["job"][i]
+            q["job"]["stop"] = t["stop"][i]
+            q["seg"] = t["seg"][i]
+            q["stage"] = t["stage"][i]
+            q["stage"]["plan_out"] = 0
+            q["stage"]["next_job"] = 0
+            q["stage"]["R"] = r.shuffles[i].ptrs[0]
+            q["stage"]["log"] = self.logs[i].data_ptr()
+            q["stage"]["log_n"] = base_d + i * CTL.itemsize + nlog
+            q["stage"]["log_cap"] = max(1, r.nbs[i])
+            q["stage"]["stall"] = self.pstall.data_ptr() + 4 * i
+            R, Tp, Tc = r.shuffles[i].ptrs
+            q["job"]["R"], q["job"]["Tpre"], q["job"]["Tchunk"] = R, Tp, Tc
+            b = r.dfit_bufs[i]
+            nodes, roots, leaf, classes, blob = b.ptrs()
+            q["res"] = r._sptr("dfit", i)
+            q["dnodes"], q["droots"], q["dleaf"], q["dclasses"], q["dblob"] = nodes, roots, leaf, classes, blob
+            q["dtrees"] = b.T
+            q["nb"], q["n_full"], q["base"] = r.nbs[i], t["stage"][i]["n_full"], r.bases[i]
+            q["max_win"], q["min_win"] = r.max_wins[i], lo
+            q["long_min_rows"], q["long_cap_rows"] = self.long_min_rows, self.long_cap_rows
+            q["dpb_x1024"] = int(np.ceil(expected_draws_per_batch(pb) * 1024))
+            q["pb"], q["last_len"], q["n_words"] = pb, part.n - (r.nbs[i] - 1) * pb, r.n_words
+            q["done"] = 1
+            q["avail"] = r.shuffles[i].waited * CHUNK
+        for ps in live:
+            q = rec[ps.i]
+            q["done"] = 0
+            q["j"], q["P"], q["win"], q["seg_start"] = ps.j, ps.P, ps.win, ps.seg_start
+            q["state"] = ps.state[0]
+            if ps.retrain:                       # a device refit staged by the last epoch
+                _, P1, P2, _ = ps.staged
+                q["retrain"], q["P1"], q["P2"] = 1, P1, P2
+                q["forest_dev"] = 1
+            else:
+                f = ps.forest
+                if isinstance(f, dfit.DeviceFitForest):
+                    q["forest_dev"] = 1
+                else:
+                    d = f.desc
+                    s = q["seg"]
+                    s["nodes"], s["roots"], s["leaf_value"], s["classes"] = d.nodes, d.roots, d.leaf_value or 0, \
+                        d.classes
+                    s["n_trees"], s["n_classes"], s["n_nodes"], s["pure"] = d.n_trees, d.n_classes, d.n_nodes, d.pure
+                    s["cforest"], s["cf_slots"], s["cf_vote_regs"] = d.cforest or 0, d.cf_slots, d.cf_vote_regs
+                    s["cf_leaves"], s["cf_tab_words"] = d.cf_leaves, d.cf_tab_words
+                    q["host_slots"] = f.features_read
+        # every partition's refit job (the slab's table is rewritten by host epochs)
+        r.dfit_jobs.rec[:self.n] = r._templates()["dfit"]
+
+    def _publish_avail(self, polled=None):
+        """Stream coverage the generator finished since the last look: the epoch stream waits
+        for it (free once done) and the records' avail fields are raised."""
+        r = self.r
+        for i, sh in enumerate(r.shuffles):
+            best = None
+            for cov, ev in sh.ready:
+                if cov > sh.waited and (best is None or cov > best[0]) and ev.query():
+                    best = (cov, ev)
+            if best is None:
+                continue
+            r.stream.wait_event(best[1])
+            sh.waited = best[0]
+            k = self._avail_k % self.avail_h.numel()
+            self._avail_k += 1
+            self.avail_h[k] = sh.waited * CHUNK
+            at = i * CTL.itemsize + _OFF["avail"]
+            with torch.cuda.stream(r.stream):
+                self.parts_d[at:at + 8].copy_(self.avail_h[k:k + 1].view(torch.uint8), non_blocking=True)
+
+    def _extend(self, rec):
+        """Enqueue generation for partitions whose position nears what is enqueued; False when
+        one would outgrow its stream buffers (the host must regrow them outside device mode)."""
+        r = self.r
+        wants = []
+        for i in range(self.n):
+            if rec["done"][i] or rec["stall"][i] or rec["park"][i]:
+                continue
+            sh = r.shuffles[i]
+            win = int(min(r.max_wins[i], max(1, int(rec["win"][i])) << (2 * GROUP)))
+            need = int(rec["P"][i]) + sh.window_draws(win) + r.n_words + 8 * CHUNK
+            need = min(need, sh.cap - 2 * CHUNK)
+            if int(rec["P"][i]) + sh.window_draws(1) + r.n_words + 4 * CHUNK > sh.cap - 2 * CHUNK:
+                return False
+            if sh.chunks_for(need) > sh.tab:
+                wants.append((i, need))
+        if wants:
+            r._ensure_all(wants, wait=False)
+        return True
+
+    # ---------------------------------------------------------------- the phase
+    def run_phase(self, live):
+        """Device epochs until every live partition is done, parked or stalled; then the
+        records back into the partitions' host state.  Returns the epochs run."""
+        r, st = self.r, self.r.stats
+        t0 = time.perf_counter()
+        stream = r.stream
+        # nothing of the host path may still be in flight: the last epoch's refits are read
+        # by the device predict itself
+        stream.synchronize()
+        r._pending_sync = False
+        r._pending_forests = []
+        while r._gen_rest is not None:       # the whole expected stream, on the side streams
+            r._enqueue_rest()
+        self._write_records(live)
+        with torch.cuda.stream(stream):
+            self.pstall.zero_()
+            self.parts_d.copy_(self.parts_h, non_blocking=True)
+            r.dfit_jobs.d[:self.n * dfit.DFIT_DTYPE.itemsize].copy_(
+                r.dfit_jobs.h[:self.n * dfit.DFIT_DTYPE.itemsize], non_blocking=True)
+        self._publish_avail()
+        E = self._epoch_struct()
+        check(lib.ddm_ctl_enter(ctypes.byref(E)), "ddm_ctl_enter")
+        timing = r.t_pred is not None
+        logging = r.predict_log is not None
+        pending, slot, epochs = None, 0, 0
+        while True:
+            if timing or logging:
+                for _ in range(GROUP):
+                    self._one_epoch_instrumented(E, timing, logging)
+            else:
+                check(lib.ddm_ctl_epochs(ctypes.byref(E), GROUP), "ddm_ctl_epochs")
+            epochs += GROUP
+            with torch.cuda.stream(stream):
+                self.poll_h[slot].copy_(self.parts_d, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            if pending is not None:
+                pev, pslot = pending
+                pev.synchronize()
+                rec = self.poll_h[pslot].numpy().view(CTL)
+                active = (rec["done"] == 0) & (rec["stall"] == 0) & (rec["park"] == 0)
+                if not active.any() or (rec["stall"] != 0).any():
+                    break
+                if not self._extend(rec):
+                    break
+                self._publish_avail()
+            pending = (ev, slot)
+            slot ^= 1
+        stream.synchronize()
+        r.side_stream.synchronize()
+        st.gpu_s += time.perf_counter() - t0
+        if timing:
+            p_ms, s_ms, f_ms, sh_ms = self.kernel_times()
+            st.predict_ms += p_ms
+            st.scan_ms += s_ms
+            st.dfit_ms += f_ms
+            st.shuffle_ms += sh_ms
+        return self._take_back(live)
+
+    def _one_epoch_instrumented(self, E, timing, logging):
+        r = self.r
+        if timing:
+            evs = [ctypes.c_void_p() for _ in range(8)]
+            for e in evs:
+                check(lib.ddm_event_create(ctypes.byref(e)), "ddm_event_create")
+            E.ev[0], E.ev[1], E.ev[2], E.ev[3] = evs[0].value, evs[1].value, evs[2].value, evs[3].value
+            E.ev[6], E.ev[7], E.ev[10], E.ev[11] = evs[4].value, evs[5].value, evs[6].value, evs[7].value
+            self.timers.append(evs)
+        if logging:
+            k = len(r.predict_log)
+            segs = torch.empty(self.n * kernels.SEG_DTYPE.itemsize, dtype=torch.uint8, device=r.device)
+            res = torch.empty(self.n, dtype=torch.int64, device=r.device)
+            with torch.cuda.stream(r.stream):
+                segs.copy_(r.segs.d[:self.n * kernels.SEG_DTYPE.itemsize], non_blocking=True)
+                res.copy_(self.res_ptrs, non_blocking=True)
+            r.predict_log.append(("dev", segs, res, k))
+        check(lib.ddm_ctl_epochs(ctypes.byref(E), 1), "ddm_ctl_epochs")
+        for k in range(12):
+            E.ev[k] = None
+
+    def kernel_times(self):
+        """(predict, scan, refit, shuffle) ms summed over the timed epochs; clears them."""
+        tot = [0.0, 0.0, 0.0, 0.0]
+        ms = ctypes.c_float()
+        for evs in self.timers:
+            for k, (a, b) in enumerate(((0, 1), (2, 3), (4, 5), (6, 7))):
+                if lib.ddm_event_elapsed_ms(evs[a], evs[b], ctypes.byref(ms)) == 0:
+                    tot[k] += ms.value
+            for e in evs:
+                lib.ddm_event_destroy(e)
+        self.timers = []
+        return tot
+
+    def replay(self, entry, stream):
+        """One logged device-mode predict launch again (the bench's roofline replays)."""
+        _, segs, res, _ = entry
+        check(lib.ddm_forest_predict_dev(segs.data_ptr(), res.data_ptr(), self.n, self.r.s.per_batch, PREDICT_BLOCKS,
+                                         self.pstall.data_ptr(), ctypes.c_void_p(stream.cuda_stream), None, None),
+              "ddm_forest_predict_dev")
+
+    def _take_back(self, live):
+        """Device records -> the partitions' host state (and their events)."""
+        r, st, pb = self.r, self.r.stats, self.r.s.per_batch
+        with torch.cuda.stream(r.stream):
+            self.parts_h.copy_(self.parts_d, non_blocking=True)
+            r.ctrl_h.copy_(r.ctrl_d, non_blocking=True)        # staging slots and refit results
+        r.stream.synchronize()
+        rec = self.rec
+        epochs = int(rec["epochs"].max()) if len(rec) else 0
+        for ps in live:
+            q = rec[ps.i]
+            n_log = int(q["n_log"])
+            if n_log:
+                lg = self.logs[ps.i][:3 * n_log].cpu().numpy().reshape(-1, 3).astype(np.int64)
+                for col in range(2):
+                    hit = lg[:, 1 + col] >= 0
+                    b = lg[hit, 0]
+                    ps.ev.append((b - 1, col, b * pb + lg[hit, 1 + col]))
+            # the last k_ctl may have applied a refit to the window it planned (P after the
+            # seeds, batch j already shuffled, a fresh DDM): the host applies it itself in
+            # _refit_prep, so it goes back as a pending refit
+            applied = bool(q["applied"]) and not q["done"]
+            if applied:
+                q["retrain"] = 1
+            st.predicted_rows += int(q["predicted_rows"])
+            st.predict_bytes += int(q["predict_bytes"])
+            st.refits += int(q["refits"]) - applied
+            st.device_refits += int(q["refits"]) - applied
+            stall = int(q["stall"])
+            if stall == kernels.CTL_STALL_SCAN:
+                raise RuntimeError(f"ddm_scan_long gave up waiting for a carried state (partition {ps.i}): the "
+                                   "epoch's results are void")
+            ps.j, ps.P, ps.win, ps.seg_start = int(q["j"]), int(q["P"]), int(q["win"]), int(q["seg_start"])
+            ps.state = np.array([q["state"]], dtype=kernels.STATE_DTYPE)
+            ps.done = bool(q["done"])
+            ps.staged = None
+            if q["retrain"]:
+                ps.retrain = True
+                if stall == kernels.CTL_STALL_WORDS:
+                    # the host path's own staging form: batch d's rows, the words after P
+                    L = ps.blen(ps.j - 1)
+                    F_i = r.parts[ps.i].X.shape[0]
+                    info = r._info_all[ps.i]
+                    ps.staged = (r._sview("x", ps.i, np.float32, L * F_i).reshape(L, -1).copy(),
+                                 r._sview("y", ps.i, np.int32, L).astype(np.int64),
+                                 r._sview("w", ps.i, np.uint32, r.n_words).copy(), None, int(info[4]), int(info[5]))
+                else:
+                    ps.staged = ("device", int(q["P1"]), int(q["P2"]), None)
+                    r._pending_sync = True         # _finish_pending reads (or redoes) the refit
+            else:
+                ps.retrain = False
+                if q["forest_dev"]:
+                    res = r._sview("dfit", ps.i, np.int64, dfit.RESULT_WORDS).copy()
+                    ps.forest = dfit.DeviceFitForest(r.dfit_bufs[ps.i], res)
+            if ps.j >= ps.nb:
+                ps.done = True
+        st.epochs += epochs
+        st.device_epochs += epochs
+        st.device_phases += 1
+        for i in range(self.n):
+            self.rec[i]["n_log"] = 0
+        return epochs

@@ -7,19 +7,28 @@ whole batches (16*k batches, so every segment starts 16-byte aligned); all segme
 scanned at once, each speculatively from a fresh detector, by ddm_scan_batches (the
 segments are its "streams").  The carries are then resolved in stream order: a segment
 whose true carry-in is fresh (the batch before it changed) keeps its speculative result;
-any other is rescanned from the carried detector, and the carry after it is the rescan's.
-On reset-heavy streams almost every carry is fresh, so the resolution is a host loop over
-the segments' end states plus a few one-segment rescans.
+a run of segments entered with a carried detector is rescanned from it in ONE
+ddm_scan_long call (the carried detector's rows are exact arithmetic, chained through
+the run), up to the first segment boundary whose carry is fresh again.  On reset-heavy
+streams almost every carry is fresh, so the resolution is a host loop over the segments'
+end states plus a few rescans.
 
 Across GPUs every rank owns a contiguous run of segments (chunk_bounds).  The ranks scan
-their segments in parallel; the carry then hops once per rank boundary (one 56-byte state,
-torch.distributed send/recv) while each rank resolves its own segments, and one
-all-reduce(MIN) gives the first change of the whole stream.  Results equal one sequential
-scan of the whole stream bit for bit, whatever the number of ranks.
+and resolve their segments in parallel as if their carry-in were fresh, then ONE
+all-gather gives every rank every chunk's carry-out under that assumption: a rank whose
+carry-in comes out fresh keeps its result without waiting for anyone.  Only a carried
+(non-fresh) detector crossing a rank boundary costs another round (that rank resolves from
+the true carry and the next all-gather publishes its carry-out).  One all-reduce(MIN) gives
+the first change of the whole stream.  The collectives run on device tensors under the
+`nccl` (RCCL) backend and on host tensors under gloo.  Results equal one sequential scan
+of the whole stream bit for bit, whatever the number of ranks.
 """
 import numpy as np
 
 from .kernels import STATE_DTYPE, fresh_states
+
+_FRESH = fresh_states(1)[0]
+_I64_MAX = np.iinfo(np.int64).max
 
 
 def state_fresh(st):
@@ -44,27 +53,83 @@ def chunk_bounds(n_rows, world, seg_rows):
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
 
 
-def resolve(carry, spec_final, n_segments, rescan):
-    """The segments' true carries in stream order.  spec_final[k]: segment k's end state from
-    a fresh carry-in; rescan(k, carry) -> (events of segment k, its end state) from `carry`.
-    Returns (the end state after the last segment, {k: events} of the rescanned segments)."""
-    redone = {}
-    for k in range(n_segments):
+class Segments:
+    """A chunk's segments: row offsets, lengths and the offsets of their batches' event rows."""
+
+    def __init__(self, n_rows, seg_len, per_batch):
+        n_full = n_rows // seg_len
+        tail = n_rows - n_full * seg_len
+        self.rows0 = [k * seg_len for k in range(n_full)] + ([n_full * seg_len] if tail else [])
+        self.lens = [seg_len] * n_full + ([tail] if tail else [])
+        nbs = [-(-L // per_batch) for L in self.lens]
+        self.ev_off = np.concatenate([[0], np.cumsum(nbs)]).astype(np.int64)
+        self.n = len(self.lens)
+
+
+def _carried(scanner, row0, n_rows, state):
+    """Mode-1 scan of rows [row0, row0 + n_rows) as one stream from `state`."""
+    if hasattr(scanner, "carried"):
+        return scanner.carried(row0, n_rows, state)
+    st = np.empty(1, STATE_DTYPE)
+    st[0] = state
+    e, f = scanner.scan(row0, 1, n_rows, st)
+    return e, f[0]
+
+
+def resolve(carry, spec_final, segs, ev, scanner, chain=4):
+    """The segments' true carries in stream order, from carry-in `carry`.  spec_final[k]:
+    segment k's end state from a fresh carry-in; ev: the speculative event rows, overwritten
+    where a segment is rescanned.  A run of segments entered with a carried detector is
+    rescanned in one carried scan of up to `chain` segments (doubling while the run goes on),
+    up to the first of them whose last batch changed (the carry after it is fresh again).
+    Returns (the end state after the last segment, segments rescanned)."""
+    k, redone = 0, 0
+    n = segs.n
+    while k < n:
         if state_fresh(carry):
             carry = spec_final[k]
+            k += 1
+            continue
+        m = min(n, k + chain)
+        rows = sum(segs.lens[k:m])
+        e, f = _carried(scanner, segs.rows0[k], rows, carry)
+        base = segs.ev_off[k]
+        j_end = None
+        for j in range(k, m - 1):                       # a change in segment j's last batch
+            if e[segs.ev_off[j + 1] - 1 - base, 1] >= 0:
+                j_end = j
+                break
+        if j_end is None:
+            ev[base:segs.ev_off[m]] = e
+            carry = f
+            redone += m - k
+            k = m
+            chain *= 2
         else:
-            redone[k], carry = rescan(k, carry)
+            ev[base:segs.ev_off[j_end + 1]] = e[:segs.ev_off[j_end + 1] - base]
+            carry = _FRESH
+            redone += j_end + 1 - k
+            k = j_end + 1
     return carry, redone
 
 
 class DeviceScanner:
-    """ddm_scan_batches over equal-length segments of a device error buffer (the product
-    path; the CPU tests inject a scanner with the same interface)."""
+    """ddm_scan_batches over equal-length segments of a device error buffer and
+    ddm_scan_long for carried runs (the product path; the CPU tests inject a scanner with
+    the same interface).  Scratch buffers are kept and reused across calls."""
 
     def __init__(self, err, params, stream=None):
         import torch
         self.err, self.params, self.stream = err, params, stream
         self.torch = torch
+        self._scratch = {}
+
+    def _buf(self, key, nbytes):
+        b = self._scratch.get(key)
+        if b is None or b.numel() < nbytes:
+            b = self.torch.empty(max(1, int(nbytes)), dtype=self.torch.uint8, device=self.err.device)
+            self._scratch[key] = b
+        return b
 
     def scan(self, row0, n_segments, seg_len, states):
         """(ev int32 [n_segments*nb, 2], end states) of segments err[row0 + k*seg_len, +seg_len)
@@ -76,67 +141,128 @@ class DeviceScanner:
         nb = -(-seg_len // pb)
         st = torch.from_numpy(np.ascontiguousarray(states).view(np.uint8).copy()).to(dev)
         ev = torch.empty((max(1, n_segments * nb), 2), dtype=torch.int32, device=dev)
-        scratch = torch.empty(kernels.scan_batches_scratch_size(n_segments, seg_len, pb), dtype=torch.uint8,
-                              device=dev)
+        scratch = self._buf("batches", kernels.scan_batches_scratch_size(n_segments, seg_len, pb))
         kernels.scan_batches(self.err[row0:], n_segments, seg_len, self.params, st, ev, scratch, stream=self.stream)
         torch.cuda.synchronize(dev)
         return ev[:n_segments * nb].cpu().numpy(), st.cpu().numpy().view(STATE_DTYPE).copy()
+
+    def carried(self, row0, n_rows, state):
+        """(ev int32 [nb, 2], end state) of rows [row0, row0 + n_rows) as ONE mode-1 stream from
+        `state` (ddm_scan_long: the carried detector's rows chained through the run)."""
+        from . import kernels
+        from ._capi import DDM_STOP_FAILED
+        torch = self.torch
+        dev = self.err.device
+        pb = self.params.per_batch
+        nb = -(-n_rows // pb)
+        st = torch.from_numpy(np.array([state], dtype=STATE_DTYPE).view(np.uint8).copy()).to(dev)
+        ev = torch.empty((max(1, nb), 2), dtype=torch.int32, device=dev)
+        stop = torch.empty(1, dtype=torch.int32, device=dev)
+        off = torch.tensor([row0], dtype=torch.int64, device=dev)
+        end = torch.tensor([row0 + n_rows], dtype=torch.int64, device=dev)
+        base = torch.zeros(1, dtype=torch.int64, device=dev)
+        scratch = self._buf("long", kernels.scan_long_scratch_size(1, n_rows, pb))
+        kernels.scan_long(self.err, off, self.params, st, base, ev, n_rows, scratch, ends=end, stop=stop, mode=1,
+                          stream=self.stream)
+        torch.cuda.synchronize(dev)
+        if int(stop.item()) == DDM_STOP_FAILED:
+            raise RuntimeError("ddm_scan_long gave up waiting for a carried state")
+        return ev[:nb].cpu().numpy(), st.cpu().numpy().view(STATE_DTYPE)[0].copy()
+
+
+def _coll_device():
+    """Where the collectives' tensors live: HBM under RCCL ("nccl"), host memory under gloo."""
+    import torch
+    import torch.distributed as dist
+    if dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def _all_gather_states(state, valid):
+    """Every rank's (valid, 56-byte state) -> [(valid, state)] in rank order (one all_gather)."""
+    import torch
+    import torch.distributed as dist
+    dev = _coll_device()
+    rec = np.zeros(64, dtype=np.uint8)
+    rec[:56] = np.array([state], dtype=STATE_DTYPE).view(np.uint8)
+    rec[56] = 1 if valid else 0
+    t = torch.from_numpy(rec).to(dev)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    res = []
+    for o in out:
+        b = o.cpu().numpy()
+        res.append((bool(b[56]), b[:56].view(STATE_DTYPE)[0].copy()))
+    return res
 
 
 def scan_long_stream(scanner, n_rows, per_batch, seg_batches=64, state_in=None, distributed=False, first_batch=0):
     """Mode-1 DDM over the rows [0, n_rows) the scanner holds, as ONE stream (the whole
     stream, or this rank's chunk of it when `distributed`: the ranks of the default
-    torch.distributed group, chunks as chunk_bounds gives them, rank order = stream order).  Returns (ev int32
-    [nb, 2] of this rank's batches, the stream's end state (on the last rank; the carry out
-    of this rank's chunk elsewhere), the first change's global batch index or -1).
-    first_batch: the global index of this chunk's first batch."""
+    torch.distributed group, chunks as chunk_bounds gives them, rank order = stream order).
+    Returns (ev int32 [nb, 2] of this rank's batches, the stream's end state (on the last
+    rank; the carry out of this rank's chunk elsewhere), the first change's global batch
+    index or -1).  first_batch: the global index of this chunk's first batch."""
     import torch
     import torch.distributed as dist
     seg_len = segment_rows(seg_batches, per_batch)
-    n_full = n_rows // seg_len
-    tail = n_rows - n_full * seg_len
+    segs = Segments(n_rows, seg_len, per_batch)
     world = dist.get_world_size() if distributed else 1
     rank = dist.get_rank() if distributed else 0
-    parts = []                                    # (row0, n_segments, length) per scan call
-    if n_full:
-        parts.append((0, n_full, seg_len))
-    if tail:
-        parts.append((n_full * seg_len, 1, tail))
-    seg_rows0 = [k * seg_len for k in range(n_full)] + ([n_full * seg_len] if tail else [])
-    seg_lens = [seg_len] * n_full + ([tail] if tail else [])
+    n_full = n_rows // seg_len
     ev_parts, finals = [], []
-    for row0, n_seg, length in parts:             # speculation: every segment from a fresh detector
+    calls = ([(0, n_full, seg_len)] if n_full else []) + ([(n_full * seg_len, 1, n_rows - n_full * seg_len)]
+                                                           if n_rows > n_full * seg_len else [])
+    for row0, n_seg, length in calls:             # speculation: every segment from a fresh detector
         e, f = scanner.scan(row0, n_seg, length, fresh_states(n_seg))
         ev_parts.append(e)
         finals.append(f)
-    ev = np.concatenate(ev_parts) if ev_parts else np.empty((0, 2), np.int32)
+    spec_ev = np.concatenate(ev_parts) if ev_parts else np.empty((0, 2), np.int32)
     spec_final = np.concatenate(finals) if finals else np.empty(0, STATE_DTYPE)
-    nbs = [-(-L // per_batch) for L in seg_lens]
-    ev_off = np.concatenate([[0], np.cumsum(nbs)]).astype(np.int64)
+    carry0 = (fresh_states(1) if state_in is None else np.asarray(state_in, STATE_DTYPE).reshape(1))[0]
 
-    def rescan(k, carry):
-        st = np.empty(1, STATE_DTYPE)
-        st[0] = carry
-        e, f = scanner.scan(seg_rows0[k], 1, seg_lens[k], st)
-        return e, f[0]
+    def resolved(carry):
+        ev = spec_ev.copy()
+        end, _ = resolve(carry, spec_final, segs, ev, scanner)
+        return ev, end
 
-    # the carry-in of this rank's chunk: the previous rank's carry-out (one hop)
-    buf = torch.zeros(56, dtype=torch.uint8)
-    carry = (fresh_states(1) if state_in is None else np.asarray(state_in, STATE_DTYPE).reshape(1))[0]
-    if world > 1 and rank > 0:
-        dist.recv(buf, src=rank - 1)
-        carry = buf.numpy().view(STATE_DTYPE)[0].copy()
-    end, redone = resolve(carry, spec_final, len(seg_lens), rescan)
-    for k, e in redone.items():
-        ev[ev_off[k]:ev_off[k + 1]] = e
-    if world > 1 and rank < world - 1:
-        out = np.array([end], dtype=STATE_DTYPE).view(np.uint8)
-        buf = torch.from_numpy(out.copy())
-        dist.send(buf, dst=rank + 1)
+    if not distributed:
+        ev, end = resolved(carry0)
+    else:
+        # every rank resolves as if its carry-in were fresh; one all-gather of the carry-outs
+        # tells each rank its true carry-in unless a carried detector crosses a rank boundary
+        ev_f, end_f = resolved(_FRESH)
+        ends_f = [s for _, s in _all_gather_states(end_f, True)]
+        carry_in = [carry0] + [None] * (world - 1)
+        true_end = {}
+        mine = None
+        while True:                       # every rank takes the same decisions (same data)
+            for q in range(1, world):
+                if carry_in[q] is None and carry_in[q - 1] is not None:
+                    if state_fresh(carry_in[q - 1]):
+                        carry_in[q] = ends_f[q - 1]
+                    elif q - 1 in true_end:
+                        carry_in[q] = true_end[q - 1]
+            if all(c is not None for c in carry_in):
+                break
+            # a carried detector crosses a rank boundary: the ranks whose carry-in is known and
+            # carried resolve from it and publish their true carry-out (at least one per round)
+            new = None
+            if carry_in[rank] is not None and not state_fresh(carry_in[rank]) and rank not in true_end:
+                mine = resolved(carry_in[rank])
+                new = mine[1]
+            for q, (ok, st) in enumerate(_all_gather_states(new if new is not None else _FRESH, new is not None)):
+                if ok:
+                    true_end[q] = st
+        if state_fresh(carry_in[rank]):
+            ev, end = ev_f, end_f
+        else:
+            ev, end = mine if mine is not None else resolved(carry_in[rank])
     hit = np.nonzero(ev[:, 1] >= 0)[0]
     first = int(first_batch + hit[0]) if len(hit) else -1
-    if world > 1:
-        t = torch.tensor([first if first >= 0 else np.iinfo(np.int64).max], dtype=torch.int64)
+    if distributed:
+        t = torch.tensor([first if first >= 0 else _I64_MAX], dtype=torch.int64, device=_coll_device())
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        first = int(t.item()) if int(t.item()) != np.iinfo(np.int64).max else -1
+        first = int(t.item()) if int(t.item()) != _I64_MAX else -1
     return ev, end, first

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 14
+#define DDM_AMD_ABI_VERSION 15
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -415,6 +415,11 @@ typedef struct ddm_stage_job {
     int64_t p_now, win, max_win, seg_start, n_full, min_win, next_avail, dpb_x1024;
     int64_t* plan_out;
     ddm_shuffle_job* next_job;
+    /* device-resident runner (ddm_ctl, log != NULL): the event rows go to log[3 * (*log_n + k)]
+     * = (batch, first warning pos, change pos) (absolute batch of the partition, at most
+     * log_cap records) instead of ev_out, and *log_n advances; stall (may be NULL): when
+     * *stall != 0 the partition is skipped (info = no change, nothing gathered or drawn). */
+    int32_t* log; int64_t* log_n; int64_t log_cap; const int32_t* stall;
 } ddm_stage_job;
 
 int ddm_epoch_stage(const ddm_stage_job* jobs_dev, int32_t n_jobs, ddm_stream_t stream);
@@ -527,6 +532,78 @@ typedef struct ddm_epoch {
 } ddm_epoch;
 int ddm_epoch_launch(const ddm_epoch* e);
 int64_t ddm_epoch_struct_bytes(void);   /* sizeof(ddm_epoch), for binding checks */
+
+/* ---- device-resident epoch controller (csrc/ctl.hip) ------------------------------
+ * The per-epoch decisions of the BatchRunner (ddm_amd/controller.py: the window after a
+ * change or after a clean window, the RNG position, the DDM state carried or dropped, the
+ * forest a refit produced, DDM_Process.py:189-210) taken on the device, so epochs are
+ * enqueued ahead and the host only collects events.  One record per partition: the static
+ * part (its buffers and the job / segment / staging templates) is written by the host when
+ * the runner enters device mode, the dynamic part mirrors the host controller's state at
+ * the start of an epoch.  Partitions that need the host (a refit that reported a status or
+ * did not compile, stream words that ran out, a look-back that gave up) get `stall`;
+ * partitions whose short last batch still needs its shuffle get `park`. */
+typedef struct ddm_ctl_part {
+    ddm_shuffle_job job;         /* window job template: R, Tpre, Tchunk, pieces, info, J, E, first, stop, pick_out */
+    ddm_predict_segment seg;     /* segment template: X, ld, y, perm, err, first_err, row_base, flags + host forest */
+    ddm_stage_job stage;         /* staging template (plan_out / next_job NULL, log / log_n / stall set) */
+    const int64_t* res;          /* the partition's device refit result words (ddm_dfit_job.result) */
+    const ddm_node* dnodes; const int32_t* droots; const double* dleaf; const int32_t* dclasses;
+    const uint8_t* dblob;        /* the device refit's forest buffers */
+    int64_t nb, n_full, base, max_win, min_win, long_min_rows, long_cap_rows, dpb_x1024;
+    int32_t pb, last_len, n_words, dtrees;
+    int32_t host_slots, pad0;    /* feature slots the host forest reads (statistics) */
+    /* dynamic: the host controller's state at the start of an epoch */
+    int64_t j, P, win, seg_start, P1, P2, avail;
+    int32_t retrain, done, stall, park, forest_dev, applied, idle, pad1;
+    int64_t g0, b_end, Wg, P_after_first, p0, p1;
+    ddm_state state;
+    int64_t n_log, predicted_rows, predict_bytes, epochs, refits;
+} ddm_ctl_part;
+
+/* Stall reasons (ddm_ctl_part.stall) */
+#define DDM_CTL_STALL_REFIT 1    /* the device refit reported a status / did not compile     */
+#define DDM_CTL_STALL_WORDS 2    /* batch d+1's shuffle or the seeds ran past the staged words */
+#define DDM_CTL_STALL_SCAN  3    /* ddm_scan_long gave up (DDM_STOP_FAILED)                   */
+
+typedef struct ddm_ctl {
+    ddm_ctl_part* parts; int32_t n, entry;       /* entry: plan the first window only     */
+    ddm_shuffle_job* jobs; ddm_predict_segment* segs; const int64_t** seg_res; ddm_stage_job* stage;
+    int64_t* off; int64_t* end; ddm_state* state; uint64_t* first; const int32_t* stop; const int64_t* pick;
+    int64_t* loff; int64_t* lend; int32_t* pstall;   /* per partition: set by the predict    */
+    int64_t predict_blocks;                        /* grid of ddm_forest_predict_dev          */
+    int64_t* status;                               /* [4]: active, stalled, parked, done       */
+} ddm_ctl;
+
+typedef struct ddm_ctl_epoch {
+    ddm_stream_t stream, side_stream; ddm_event_t fork_ev, join_ev;
+    ddm_ctl ctl;                                   /* device pointers, by value                */
+    const ddm_ctl* ctl_d;                          /* unused (reserved)                        */
+    int32_t n, per_batch;
+    const uint8_t* err; const ddm_params* params; const int64_t* batch_base; int64_t n_batches_total;
+    int32_t* ev_out; int64_t* nev; const uint8_t* perm_map;
+    int64_t long_max_rows; void* long_scratch;
+    const ddm_dfit_job* dfit_jobs; int32_t n_dfit, max_trees;
+    int64_t max_W, max_pieces;                     /* shuffle grid bounds (windows never exceed) */
+    int64_t status_h_off;                          /* unused (reserved)                        */
+    ddm_event_t ev[12];                            /* optional begin/end pairs: predict, scan, long,
+                                                      stage + ctl, refit, next shuffles        */
+} ddm_ctl_epoch;
+int64_t ddm_ctl_part_bytes(void);
+int64_t ddm_ctl_epoch_bytes(void);
+/* entry: plan every partition's first window and shuffle it (on e->stream). */
+int ddm_ctl_enter(const ddm_ctl_epoch* e);
+/* n_epochs device epochs on e->stream: predict, scan (+ long), pick, staging, decisions and
+ * the next windows' plan, then the next windows' shuffles on side_stream beside the device
+ * refits.  Epochs after every partition is done, parked or stalled do no work. */
+int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs);
+
+/* Forest predict for the device-resident runner: one launch, fixed grid, segments and block
+ * split from the device table; a segment with res[s] != NULL takes its compiled forest's shape
+ * from those refit result words (and sets stall[s] instead when the refit is unusable). */
+int ddm_forest_predict_dev(const ddm_predict_segment* segs_dev, const int64_t* const* res_dev, int32_t n_segs,
+                           int32_t per_batch, int64_t grid, int32_t* stall, ddm_stream_t stream,
+                           ddm_event_t ev_begin, ddm_event_t ev_end);
 
 /* ---- synthetic inputs (benchmark configs) ------------------------- */
 

@@ -1,0 +1,77 @@
+"""Device-resident epochs (csrc/ctl.hip, ddm_amd/devctl.py) == host-driven epochs == the
+oracle: the epoch decisions of run_DDM_loop (DDM_Process.py:189-210) taken on the device
+must give the same events and leave every partition's RNG where the reference leaves it."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _parts(sizes, F, block, seed, flip=0.0, jitter=False):
+    from ddm_amd import kernels
+    from ddm_amd.controller import DevicePartition
+    dev = torch.device("cuda", 0)
+    parts = []
+    for k, n in enumerate(sizes):
+        part = DevicePartition.allocate(n, F, dev)
+        if jitter:
+            kernels.synth_jitter_labels(part.y[:n], k, len(sizes), 1800, 300, 10, flip, seed)
+        else:
+            kernels.synth_block_labels(part.y[:n], part=k, n_parts=len(sizes), block_rows=block, n_classes=10)
+        kernels.synth_features(part.X, part.y[:n], row0=k, row_stride=len(sizes), seed=seed, noise=0.04)
+        parts.append(part)
+    torch.cuda.synchronize()
+    return parts
+
+
+def _run(parts, device_ctl, seeds, win=256, maxwin=1 << 16):
+    from ddm_amd.controller import BatchRunner
+    from ddm_amd.params import DDMSettings
+    from ddm_amd.rng import MTStream
+    runner = BatchRunner(parts, DDMSettings(window_batches=win, max_window_batches=maxwin), device_ctl=device_ctl)
+    rngs = [MTStream.from_seed(s) for s in seeds]
+    out = runner.run(rngs)
+    st = runner.stats
+    runner.close()
+    return out, [(r.key.copy(), r.pos.value) for r in rngs], st
+
+
+@pytest.mark.parametrize("case", ["blocks", "jitter", "noise", "tails"])
+def test_device_epochs_equal_host_epochs(case):
+    if case == "blocks":
+        parts = _parts((60_000,) * 4, 27, 20_011, 3)
+    elif case == "jitter":
+        parts = _parts((24_000,) * 4, 27, 0, 5, jitter=True)
+    elif case == "noise":
+        parts = _parts((30_000, 30_000), 27, 0, 7, flip=0.01, jitter=True)
+    else:       # short last batches, one partition much shorter than the others
+        parts = _parts((24_037, 17_055, 4_321, 9_999), 27, 6_007, 9)
+    seeds = [100 + k for k in range(len(parts))]
+    dev_out, dev_rng, st = _run(parts, True, seeds)
+    host_out, host_rng, st_h = _run(parts, False, seeds)
+    assert st.device_epochs > 0 and st_h.device_epochs == 0
+    for k in range(len(parts)):
+        assert np.array_equal(dev_out[k], host_out[k]), k
+        assert np.array_equal(dev_rng[k][0], host_rng[k][0]) and dev_rng[k][1] == host_rng[k][1], k
+    assert st.refits == st_h.refits
+
+
+def test_device_epochs_vs_oracle():
+    """Partitions with many refits, run with device epochs, == the oracle on each."""
+    from oracle.controller import run_partition
+    parts = _parts((12_000, 9_050, 15_100), 27, 0, 11, flip=0.005, jitter=True)
+    seeds = [7, 8, 9]
+    out, rng, st = _run(parts, True, seeds, win=7, maxwin=64)
+    assert st.device_epochs > 0
+    drifts = 0
+    for k, part in enumerate(parts):
+        X = part.X[:, :part.n].t().contiguous().cpu().numpy().astype(np.float64)
+        y = part.y[:part.n].cpu().numpy().astype(np.int64)
+        np.random.seed(seeds[k])
+        want = run_partition(X, y, np.arange(part.n), np.arange(part.n))
+        assert np.array_equal(out[k][:, 0], want[:, 0]) and np.array_equal(out[k][:, 1], want[:, 2]), k
+        after = np.random.get_state()
+        assert np.array_equal(rng[k][0], after[1]) and rng[k][1] == after[2], k
+        drifts += int((want[:, 2] >= 0).sum())
+    assert drifts >= 50
