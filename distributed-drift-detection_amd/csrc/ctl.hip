@@ -17,6 +17,8 @@
 // job.  Thread t owns partition t; thread 0 then splits the predict grid over the windows.
 // The decisions are the host controller's, line for line: results do not depend on which
 // side took them (tests/test_gpu_devctl.py runs both on the same partitions).
+#include <cstddef>
+
 #include "common.h"
 
 namespace {
@@ -110,9 +112,11 @@ __device__ void plan(const ddm_ctl& c, ddm_ctl_part& p, int i) {
         c.off[i] = c.end[i] = at;
         c.loff[i] = c.lend[i] = 0;
         c.state[i] = p.state;
+        c.log_b0[i] = p.j;
         st.j = st.b_end = p.j;
         st.g0 = p.j;
         st.log = nullptr;                          // nothing to compact
+        st.max_events = 0;
         st.p_after_first = st.p_tail_after = -1;
         return;
     }
@@ -161,6 +165,13 @@ __device__ void plan(const ddm_ctl& c, ddm_ctl_part& p, int i) {
     c.end[i] = longscan ? p.p0 : p.p1;
     c.loff[i] = longscan ? p.p0 : 0;
     c.lend[i] = longscan ? p.p1 : 0;
+    // events: the one-lane scan appends them to the log itself; a long scan writes dense
+    // rows, which the staging compacts into the log
+    c.log_b0[i] = p.j;
+    if (!longscan) {
+        st.log = nullptr;
+        st.max_events = 0;
+    }
     // staging
     st.j = p.j;
     st.g0 = g0;
@@ -280,6 +291,8 @@ int rec(ddm_event_t e, hipStream_t s) {
 
 }  // namespace
 
+static_assert(sizeof(ddm_ctl_part) % sizeof(int64_t) == 0, "ddm_ctl_part: int64 stride");
+
 extern "C" int64_t ddm_ctl_part_bytes(void) { return (int64_t)sizeof(ddm_ctl_part); }
 extern "C" int64_t ddm_ctl_epoch_bytes(void) { return (int64_t)sizeof(ddm_ctl_epoch); }
 
@@ -309,9 +322,11 @@ extern "C" int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs) {
             return rc;
         if (int rc = rec(e->ev[1], s)) return rc;
         if (int rc = rec(e->ev[2], s)) return rc;
-        if (int rc = ddm_scan_streams(e->err, c.off, c.n, e->params, c.state, c.first, e->batch_base,
-                                      e->n_batches_total, e->ev_out, const_cast<int32_t*>(c.stop), e->nev, 0, nullptr,
-                                      e->perm_map, c.end, e->stream, nullptr, nullptr))
+        if (int rc = ddm_scan_streams_log(e->err, c.off, c.n, e->params, c.state, c.first, c.logs,
+                                          reinterpret_cast<int64_t*>(reinterpret_cast<uint8_t*>(c.parts) +
+                                                                     offsetof(ddm_ctl_part, n_log)),
+                                          (int64_t)(sizeof(ddm_ctl_part) / sizeof(int64_t)), c.log_b0,
+                                          const_cast<int32_t*>(c.stop), 0, e->perm_map, c.end, e->stream))
             return rc;
         if (e->long_max_rows > 0)
             if (int rc = ddm_scan_long(e->err, c.loff, c.lend, c.n, e->long_max_rows, e->params, c.state, e->batch_base,
@@ -337,7 +352,7 @@ extern "C" int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs) {
             return rc;
         if (e->n_dfit > 0) {
             if (int rc = rec(e->ev[6], s)) return rc;
-            if (int rc = ddm_rf_fit_device(e->dfit_jobs, e->n_dfit, e->max_trees, e->stream)) return rc;
+            if (int rc = ddm_rf_fit_device_lf(e->dfit_jobs, e->n_dfit, e->max_trees, e->dfit_max_lf, e->stream)) return rc;
             if (int rc = rec(e->ev[7], s)) return rc;
         }
         if (int rc = ddm::hip_status(hipStreamWaitEvent(s, reinterpret_cast<hipEvent_t>(e->join_ev), 0), "join"))

@@ -179,11 +179,36 @@ __device__ __forceinline__ int byte_at(uint64_t lo, uint64_t hi, int k) {
 // leading zeros, a zero run, a trivial-state change, or an exact row): no nested loops,
 // so a lane that finishes a stream starts its next one at once instead of idling until
 // the slowest lane of its wave is done with the same round.
+// Event sink of k_scan_fast: the dense per-batch rows (ev), or, with a log (the device-
+// resident runner, csrc/ctl.hip), one record (b0[sid] + b, warning, change) per batch
+// with an event appended to the stream's own log (one lane owns a stream: no atomics).
+struct EvSink {
+    int32_t* ev;
+    int32_t* const* logs;
+    int64_t* log_n;
+    int64_t log_stride;          // int64 words between the streams' counters
+    const int64_t* b0;
+    __device__ __forceinline__ void put(int64_t sid, int32_t* evs, int64_t b, int w, int c, int64_t& nlog) const {
+        if (logs) {
+            int32_t* r = logs[sid] + 3 * nlog;
+            r[0] = (int32_t)(b0[sid] + b);
+            r[1] = w;
+            r[2] = c;
+            ++nlog;
+        } else {
+            evs[2 * b] = w;
+            evs[2 * b + 1] = c;
+        }
+    }
+};
+
 __global__ __launch_bounds__(kFastThreads) void k_scan_fast(
     const uint8_t* __restrict__ err, const int64_t* __restrict__ off, int64_t n_streams, ddm_params P,
     ddm_state* __restrict__ state, const uint64_t* __restrict__ first_nz, const int64_t* __restrict__ batch_base,
-    int32_t* __restrict__ ev, int32_t* __restrict__ stop_out, int64_t* __restrict__ nev_out, int mode,
+    EvSink sink, int32_t* __restrict__ stop_out, int64_t* __restrict__ nev_out, int mode,
     const uint8_t* __restrict__ pmap, const int64_t* __restrict__ stream_end) {
+    int32_t* const ev = sink.ev;
+    int64_t nlog = 0;
     __shared__ double rcp[kRcpN];
     for (int k = threadIdx.x; k < kRcpN; k += kFastThreads) rcp[k] = 1.0 / (double)(k > 0 ? k : 1);
     __syncthreads();
@@ -220,9 +245,11 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(
                 state[sid] = st;
                 if (stop_out) stop_out[sid] = stop;
                 if (nev_out) nev_out[sid] = nev;
+                if (sink.logs) sink.log_n[sid * sink.log_stride] = nlog;
             }
             sid += nthreads;
             if (sid >= n_streams) break;
+            if (sink.logs) nlog = sink.log_n[sid * sink.log_stride];
             lo = off[sid];
             hi = stream_end ? stream_end[sid] : off[sid + 1];
             const ddm_state st = state[sid];
@@ -235,7 +262,7 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(
             d.chg = st.in_concept_change;
             d.warn = st.in_warning_zone;
             hint = first_nz ? first_nz[sid] : 0ull;
-            evs = ev + 2 * batch_base[sid];
+            evs = ev ? ev + 2 * batch_base[sid] : nullptr;
             nev = 0;
             stop = -1;
             b = 0;
@@ -300,8 +327,8 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(
         }
         if (changed) {
             const int cpos = (int)(i - 1 - bstart);
-            evs[2 * b] = (pmap && wpos >= 0) ? (int)pmap[bstart + wpos] : wpos;
-            evs[2 * b + 1] = pmap ? (int)pmap[bstart + cpos] : cpos;
+            sink.put(sid, evs, b, (pmap && wpos >= 0) ? (int)pmap[bstart + wpos] : wpos,
+                     pmap ? (int)pmap[bstart + cpos] : cpos, nlog);
             ++nev;
             if (mode == 0) {
                 stop = (int32_t)b;
@@ -310,7 +337,8 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(
             }
             i = bend;                       // fresh detector from the next batch
         } else if (i >= bend && wpos >= 0) {
-            evs[2 * b] = pmap ? (int)pmap[bstart + wpos] : wpos;
+            if (sink.logs) sink.put(sid, evs, b, pmap ? (int)pmap[bstart + wpos] : wpos, -1, nlog);
+            else evs[2 * b] = pmap ? (int)pmap[bstart + wpos] : wpos;
             ++nev;
         }
         if (i >= bend && i < hi) {
@@ -354,10 +382,30 @@ extern "C" int ddm_scan_streams(const uint8_t* err, const int64_t* stream_off, i
         const int64_t fast_blocks = std::max<int64_t>(1, std::min<int64_t>(ddm::ceil_div(n_streams, kFastThreads),
                                                                            256 * 5 * 4));
         hipLaunchKernelGGL(k_scan_fast, dim3((unsigned)fast_blocks), dim3(kFastThreads), 0, s, err, stream_off,
-                           n_streams, *prm, state_io, first_nz, batch_base, ev_out, stop_out, nev_out, (int)mode,
-                           perm_map, stream_end);
+                           n_streams, *prm, state_io, first_nz, batch_base, EvSink{ev_out, nullptr, nullptr, 0, nullptr},
+                           stop_out, nev_out, (int)mode, perm_map, stream_end);
     }
     if (ev_end)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
     return ddm::launch_status("ddm_scan_streams");
+}
+
+extern "C" int ddm_scan_streams_log(const uint8_t* err, const int64_t* stream_off, int64_t n_streams,
+                                    const ddm_params* prm, ddm_state* state_io, const uint64_t* first_nz,
+                                    int32_t* const* logs, int64_t* log_n, int64_t log_n_stride, const int64_t* log_b0,
+                                    int32_t* stop_out, int32_t mode, const uint8_t* perm_map,
+                                    const int64_t* stream_end, ddm_stream_t stream) {
+    if (!err || !stream_off || !prm || !state_io || !logs || !log_n || !log_b0 || log_n_stride <= 0 || n_streams < 0 ||
+        prm->per_batch <= 0 || (mode != 0 && mode != 1)) {
+        ddm::set_error("ddm_scan_streams_log: invalid argument");
+        return DDM_E_ARG;
+    }
+    if (n_streams == 0) return 0;
+    const int64_t fast_blocks =
+        std::max<int64_t>(1, std::min<int64_t>(ddm::ceil_div(n_streams, kFastThreads), 256 * 5 * 4));
+    hipLaunchKernelGGL(k_scan_fast, dim3((unsigned)fast_blocks), dim3(kFastThreads), 0, ddm::as_hip(stream), err,
+                       stream_off, n_streams, *prm, state_io, first_nz, nullptr,
+                       EvSink{nullptr, logs, log_n, log_n_stride, log_b0}, stop_out, nullptr, (int)mode, perm_map,
+                       stream_end);
+    return ddm::launch_status("ddm_scan_streams_log");
 }

@@ -65,7 +65,7 @@ extern "C" int ddm_epoch_launch(const ddm_epoch* e) {
         if (e->ev[8])
             if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(e->ev[8]), s), "event record"))
                 return rc;
-        if (int rc = ddm_rf_fit_device(e->dfit_jobs, e->n_dfit, e->max_trees, e->stream)) return rc;
+        if (int rc = ddm_rf_fit_device_lf(e->dfit_jobs, e->n_dfit, e->max_trees, e->dfit_max_lf, e->stream)) return rc;
         if (e->ev[9])
             if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(e->ev[9]), s), "event record"))
                 return rc;

@@ -636,6 +636,85 @@ __device__ __forceinline__ void build_tree(const Job& jb, const Layout& lo, int 
 // trees when they fit (L*F <= kTreeTile); otherwise the builder reads them from HBM.
 constexpr int kTreeTile = 4096;
 
+// Small jobs (L*F <= kTreeTile, the controller's refits: 100 rows x 27 features) skip
+// k_dfit_prep: every workgroup gates, checks and presorts the batch itself in LDS (the
+// ~270k rank comparisons of a 100 x 27 batch are ~1k per thread), and workgroup 0 writes
+// the job's status, classes_ and class count for k_dfit_pack.  One launch fewer per refit.
+template <bool kFused>
+__device__ __forceinline__ bool fused_prep(const Job& jb, float* s_X, uint8_t* s_ord, uint8_t* s_yi, int& K_out) {
+    __shared__ int32_t s_y[kMaxL];
+    __shared__ uint8_t s_first[kMaxL];
+    __shared__ int s_nan, s_K, s_skip;
+    const int t = threadIdx.x;
+    constexpr int kT = 64 * kWaves;
+    const bool lead = blockIdx.x == 0;
+    if (t == 0) {
+        s_skip = (jb.gate && *jb.gate < 0) || (jb.gate2 && *jb.gate2 != 1);
+        s_nan = 0;
+        s_K = 0;
+    }
+    __syncthreads();
+    if (s_skip) {
+        if (lead && t == 0) jb.result[DDM_DFIT_STATUS] = -1;
+        return false;
+    }
+    const int L = jb.L, F = jb.F;
+    if (L < 1 || L > kMaxL || F < 1 || F > kMaxF || jb.n_trees < 1 || jb.n_trees > 256 || jb.k_cap < 1 ||
+        jb.k_cap > kMaxK || jb.max_features < 1) {
+        if (lead && t == 0) jb.result[DDM_DFIT_STATUS] = DDM_E_ARG;
+        return false;
+    }
+    const int LF = L * F;
+    for (int e = t; e < LF; e += kT) {
+        const float x = jb.X[e];
+        s_X[e] = x;
+        if (x != x) s_nan = 1;
+    }
+    if (t < L) s_y[t] = jb.y[t];
+    __syncthreads();
+    // classes_ = np.unique(y): first occurrences ranked by value
+    if (t < L) {
+        int first = 1;
+        for (int j = 0; j < t; ++j) first &= s_y[j] != s_y[t];
+        s_first[t] = (uint8_t)first;
+        if (first) atomicAdd(&s_K, 1);
+    }
+    __syncthreads();
+    const int K = s_K;
+    if (t < L) {
+        int rank = 0;
+        for (int j = 0; j < L; ++j) rank += (s_first[j] && s_y[j] < s_y[t]) ? 1 : 0;
+        s_yi[t] = (uint8_t)min(rank, 255);
+        if (lead && s_first[t] && rank < jb.k_cap) jb.classes[rank] = s_y[t];
+    }
+    if (s_nan || K > jb.k_cap) {
+        if (lead && t == 0) {
+            jb.result[DDM_DFIT_STATUS] = s_nan ? DDM_E_NAN : DDM_E_FOREST;
+            jb.result[DDM_DFIT_CLASSES] = K;
+        }
+        return false;
+    }
+    // presorted orders (stable rank of every row in every feature), straight into LDS
+    for (int e = t; e < LF; e += kT) {
+        const int k = e / L, i = e % L;
+        const float x = s_X[i * F + k];
+        int r = 0;
+        for (int j = 0; j < L; ++j) {
+            const float u = s_X[j * F + k];
+            r += (u < x || (u == x && j < i)) ? 1 : 0;
+        }
+        s_ord[k * L + r] = (uint8_t)i;
+    }
+    if (lead && t == 0) {
+        jb.result[DDM_DFIT_STATUS] = 0;
+        jb.result[DDM_DFIT_CLASSES] = K;
+    }
+    __syncthreads();
+    K_out = K;
+    return true;
+}
+
+template <bool kFused>
 __global__ __launch_bounds__(64 * kWaves) void k_dfit_trees(const Job* __restrict__ jobs) {
     __shared__ WaveLds lds[kWaves];
     __shared__ float s_X[kTreeTile];
@@ -644,6 +723,13 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfit_trees(const Job* __restric
     const Job jb = jobs[blockIdx.y];
     const int w = threadIdx.x / 64, lane = threadIdx.x & 63;
     const int tree = blockIdx.x * kWaves + w;
+    if constexpr (kFused) {
+        int K = 0;
+        if (!fused_prep<true>(jb, s_X, s_ord, s_yi, K)) return;
+        const Layout lo = layout(jb.L, jb.F, jb.n_trees, jb.k_cap);
+        if (tree < jb.n_trees) build_tree(jb, lo, tree, K, lds[w], lane, s_X, s_ord, s_yi);
+        return;
+    }
     if (jb.result[DDM_DFIT_STATUS] != 0) return;
     const int K = (int)jb.result[DDM_DFIT_CLASSES];
     const Layout lo = layout(jb.L, jb.F, jb.n_trees, jb.k_cap);
@@ -1160,7 +1246,8 @@ extern "C" int64_t ddm_rf_device_scratch_bytes(int32_t L, int32_t F, int32_t n_t
     return layout(L, F, n_trees, k_cap).total;
 }
 
-extern "C" int ddm_rf_fit_device(const ddm_dfit_job* jobs_dev, int32_t n_jobs, int32_t max_trees, ddm_stream_t stream) {
+extern "C" int ddm_rf_fit_device_lf(const ddm_dfit_job* jobs_dev, int32_t n_jobs, int32_t max_trees, int64_t max_lf,
+                                    ddm_stream_t stream) {
     if (!jobs_dev || n_jobs < 0 || max_trees < 1 || max_trees > 256) {
         ddm::set_error("ddm_rf_fit_device: invalid argument");
         return DDM_E_ARG;
@@ -1168,11 +1255,19 @@ extern "C" int ddm_rf_fit_device(const ddm_dfit_job* jobs_dev, int32_t n_jobs, i
     if (n_jobs == 0) return 0;
     hipStream_t s = ddm::as_hip(stream);
     const Job* jobs = reinterpret_cast<const Job*>(jobs_dev);
-    hipLaunchKernelGGL(k_dfit_prep, dim3((unsigned)n_jobs), dim3(kPrepThreads), 0, s, jobs);
-    if (int rc = ddm::launch_status("ddm_rf_fit_device/prep")) return rc;
-    hipLaunchKernelGGL(k_dfit_trees, dim3((unsigned)ddm::ceil_div(max_trees, kWaves), (unsigned)n_jobs),
-                       dim3(64 * kWaves), 0, s, jobs);
+    const bool fused = max_lf > 0 && max_lf <= kTreeTile;
+    if (!fused) {
+        hipLaunchKernelGGL(k_dfit_prep, dim3((unsigned)n_jobs), dim3(kPrepThreads), 0, s, jobs);
+        if (int rc = ddm::launch_status("ddm_rf_fit_device/prep")) return rc;
+    }
+    hipLaunchKernelGGL(fused ? k_dfit_trees<true> : k_dfit_trees<false>,
+                       dim3((unsigned)ddm::ceil_div(max_trees, kWaves), (unsigned)n_jobs), dim3(64 * kWaves), 0, s,
+                       jobs);
     if (int rc = ddm::launch_status("ddm_rf_fit_device/trees")) return rc;
     hipLaunchKernelGGL(k_dfit_pack, dim3((unsigned)n_jobs), dim3(kPackThreads), 0, s, jobs);
     return ddm::launch_status("ddm_rf_fit_device/pack");
+}
+
+extern "C" int ddm_rf_fit_device(const ddm_dfit_job* jobs_dev, int32_t n_jobs, int32_t max_trees, ddm_stream_t stream) {
+    return ddm_rf_fit_device_lf(jobs_dev, n_jobs, max_trees, -1, stream);
 }

@@ -132,7 +132,9 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     // device-resident runner: records go to the partition's event log (absolute batches)
     const int64_t log0 = jb.log ? *jb.log_n : 0;
     const int64_t cap = jb.log ? jb.log_cap - log0 : (int64_t)jb.max_events;
-    for (int64_t base = 0; base < nrows; base += 8 * kStageThreads) {
+    // no log and no staging room: the scan logged the events itself (device-resident runner)
+    const int64_t nscan = (jb.log || jb.max_events > 0) ? nrows : 0;
+    for (int64_t base = 0; base < nscan; base += 8 * kStageThreads) {
         const int64_t r0 = base + 8 * (int64_t)t;
         int4 q[4];
         const bool vec = r0 + 8 <= nrows && ((reinterpret_cast<uintptr_t>(jb.ev + 2 * r0) & 15) == 0);

@@ -58,7 +58,7 @@ class DdmEpoch(ctypes.Structure):
                 ("dfit_jobs", _vp), ("n_dfit", _i32), ("max_trees", _i32), ("ev", _vp * 10),
                 ("pick_jobs", _vp), ("n_pick", _i32), ("n_next", _i32), ("next_jobs", _vp), ("next_max_W", _i64),
                 ("next_max_pieces", _i64), ("side_stream", _vp), ("fork_ev", _vp), ("join_ev", _vp),
-                ("mid_ev", _vp), ("tail_off", _i64), ("tail_bytes", _i64)]
+                ("mid_ev", _vp), ("tail_off", _i64), ("tail_bytes", _i64), ("dfit_max_lf", _i64)]
 _f32, _pi32 = ctypes.c_float, ctypes.POINTER(ctypes.c_int32)
 
 
@@ -67,7 +67,7 @@ class DdmCtl(ctypes.Structure):
     _fields_ = [("parts", _vp), ("n", _i32), ("entry", _i32), ("jobs", _vp), ("segs", _vp), ("seg_res", _vp),
                 ("stage", _vp), ("off", _vp), ("end", _vp), ("state", _vp), ("first", _vp), ("stop", _vp),
                 ("pick", _vp), ("loff", _vp), ("lend", _vp), ("pstall", _vp), ("predict_blocks", _i64),
-                ("status", _vp)]
+                ("status", _vp), ("logs", _vp), ("log_b0", _vp)]
 
 
 class DdmCtlEpoch(ctypes.Structure):
@@ -76,7 +76,7 @@ class DdmCtlEpoch(ctypes.Structure):
                 ("ctl_d", _vp), ("n", _i32), ("per_batch", _i32), ("err", _vp), ("params", _vp),
                 ("batch_base", _vp), ("n_batches_total", _i64), ("ev_out", _vp), ("nev", _vp), ("perm_map", _vp),
                 ("long_max_rows", _i64), ("long_scratch", _vp), ("dfit_jobs", _vp), ("n_dfit", _i32),
-                ("max_trees", _i32), ("max_W", _i64), ("max_pieces", _i64), ("status_h_off", _i64),
+                ("max_trees", _i32), ("max_W", _i64), ("max_pieces", _i64), ("dfit_max_lf", _i64),
                 ("ev", _vp * 12)]
 
 # name -> (restype, argtypes); every symbol include/ddm_amd.h declares.
@@ -93,6 +93,8 @@ SIGNATURES = {
     "ddm_scan_long": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, ctypes.POINTER(DdmParams), _vp, _vp, _vp, _vp, _vp,
                                      _i32, _vp, _vp, _vp, _vp, _vp]),
     "ddm_scan_long_scratch_bytes": (_i64, [_i64, _i64, _i32]),
+    "ddm_scan_streams_log": (ctypes.c_int, [_vp, _vp, _i64, ctypes.POINTER(DdmParams), _vp, _vp, _vp, _vp, _i64, _vp,
+                                            _vp, _i32, _vp, _vp, _vp]),
     "ddm_scan_long_set_spin_limit": (ctypes.c_int, [ctypes.c_uint32]),
     "ddm_forest_predict_batch": (ctypes.c_int, [_vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "ddm_shuffle_generate_batch": (ctypes.c_int, [_vp, _i32, _vp]),
@@ -128,6 +130,7 @@ SIGNATURES = {
     "ddm_epoch_stage": (ctypes.c_int, [_vp, _i32, _vp]),
     "ddm_rf_device_scratch_bytes": (_i64, [_i32, _i32, _i32, _i32]),
     "ddm_rf_fit_device": (ctypes.c_int, [_vp, _i32, _i32, _vp]),
+    "ddm_rf_fit_device_lf": (ctypes.c_int, [_vp, _i32, _i32, _i64, _vp]),
     "ddm_words_perm_seeds": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _vp]),
     "ddm_rf_fit": (ctypes.c_int, [_vp, _i32, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp]),
     "ddm_synth_block_labels": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i32, _vp]),

@@ -41,7 +41,7 @@ from .trainer import BatchForestTrainer
 # (every row of it is exact arithmetic) and it spans at least this many rows.
 LONG_SCAN_MIN_ROWS = int(os.environ.get("DDM_LONG_SCAN_ROWS", 4 * 64 * 100))
 # Device-resident epochs (devctl.py) by default; DDM_DEVICE_CTL=0 keeps every epoch on the host path.
-DEVICE_CTL = os.environ.get("DDM_DEVICE_CTL", "0") not in ("", "0")
+DEVICE_CTL = os.environ.get("DDM_DEVICE_CTL", "1") not in ("", "0")
 
 
 def carried_exact(st):
@@ -911,6 +911,7 @@ class BatchRunner:
             self._mid_ev = ctypes.c_void_p()
             check(lib.ddm_event_create(ctypes.byref(self._mid_ev)), "ddm_event_create")
             E.mid_ev = self._mid_ev.value
+            E.dfit_max_lf = self.s.per_batch * max(p.X.shape[0] for p in self.parts)
             E.tail_off = self.stage_off["dfit"]
             E.tail_bytes = self.stage_stride["dfit"] * len(self.parts)
         if self.timing:
@@ -1138,7 +1139,7 @@ class BatchRunner:
             # the refits of the partitions that changed, on the rows the staging gathered
             if self.t_fit is not None:
                 check(lib.ddm_event_record(self.t_fit.ev[0], ctypes.c_void_p(stream.cuda_stream)), "event record")
-            dfit.fit_device(self.dfit_jobs.d, len(live), self.s.n_estimators, stream)
+            dfit.fit_device(self.dfit_jobs.d, len(live), self.s.n_estimators, stream, self._E.dfit_max_lf)
             if self.t_fit is not None:
                 check(lib.ddm_event_record(self.t_fit.ev[1], ctypes.c_void_p(stream.cuda_stream)), "event record")
         with torch.cuda.stream(stream):

@@ -52,6 +52,8 @@ class DeviceController:
         self.res_ptrs = torch.zeros(n, dtype=torch.int64, device=dev)
         self.pstall = torch.zeros(n, dtype=torch.int32, device=dev)
         self.logs = [torch.empty(3 * max(1, nb), dtype=torch.int32, device=dev) for nb in r.nbs]
+        self.log_ptrs = torch.tensor([lg.data_ptr() for lg in self.logs], dtype=torch.int64, device=dev)
+        self.log_b0 = torch.zeros(n, dtype=torch.int64, device=dev)
         self.avail_h = torch.zeros(64 * n, dtype=torch.int64, pin_memory=True)   # H2D sources (a ring)
         self._avail_k = 0
         self.long_min_rows, self.long_cap_rows = int(long_min_rows), int(long_cap_rows)
@@ -94,6 +96,7 @@ class DeviceController:
         c.off, c.end, c.state, c.first = base + r.o_off, base + r.o_end, base + r.o_state, base + r.o_first
         c.stop, c.pick, c.loff, c.lend = base + r.o_stop, base + r.o_pick, base + r.o_loff, base + r.o_lend
         c.pstall, c.predict_blocks, c.status = self.pstall.data_ptr(), PREDICT_BLOCKS, None
+        c.logs, c.log_b0 = self.log_ptrs.data_ptr(), self.log_b0.data_ptr()
         E.n, E.per_batch = self.n, r.s.per_batch
         E.err, E.params, E.batch_base = r.err_all.data_ptr(), ctypes.addressof(r.params), base + r.o_bbase
         E.n_batches_total, E.ev_out, E.nev, E.perm_map = r.ev_total, r.ev_d.data_ptr(), base + r.o_nev, \
@@ -102,6 +105,7 @@ class DeviceController:
         E.dfit_jobs, E.n_dfit, E.max_trees = r.dfit_jobs.d.data_ptr(), self.n, r.s.n_estimators
         mw = max(r.max_wins)
         E.max_W = mw
+        E.dfit_max_lf = r.s.per_batch * max(p.X.shape[0] for p in r.parts)
         E.max_pieces = 2 + 64 + r.shuffles[0].window_draws(mw) // 8192
         self._E = E
         return E

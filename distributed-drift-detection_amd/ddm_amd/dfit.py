@@ -105,18 +105,19 @@ class DeviceFitForest:
         return int(self.res[CF_SLOTS]) if self.compiled else self.bufs.F
 
 
-def fit_device(table_d, n_jobs, max_trees, stream):
-    """ddm_rf_fit_device over a device table of DFIT_DTYPE records."""
-    check(lib.ddm_rf_fit_device(table_d.data_ptr(), int(n_jobs), int(max_trees), ctypes.c_void_p(stream.cuda_stream)),
-          "ddm_rf_fit_device")
+def fit_device(table_d, n_jobs, max_trees, stream, max_lf=-1):
+    """ddm_rf_fit_device over a device table of DFIT_DTYPE records (max_lf >= every job's
+    L*F: small batches are prepared inside the tree kernel)."""
+    check(lib.ddm_rf_fit_device_lf(table_d.data_ptr(), int(n_jobs), int(max_trees), int(max_lf),
+                                   ctypes.c_void_p(stream.cuda_stream)), "ddm_rf_fit_device")
 
 
 class DeviceTrainer:
     """Stand-alone device refits of host batches (tests, tools): uploads the rows, runs the
     fit and reads back packed forests and blobs in the BatchForestTrainer.fit_many format."""
 
-    def __init__(self, n_estimators=100, k_cap=16, device=None):
-        self.T, self.k_cap = int(n_estimators), int(k_cap)
+    def __init__(self, n_estimators=100, k_cap=16, device=None, fused=True):
+        self.T, self.k_cap, self.fused = int(n_estimators), int(k_cap), bool(fused)
         self.device = device or torch.device("cuda", torch.cuda.current_device())
 
     def fit_many(self, batches, stream=None):
@@ -135,7 +136,8 @@ class DeviceTrainer:
             recs.append(b.record(xd.data_ptr(), yd.data_ptr(), sd.data_ptr(), res_d[k].data_ptr()))
         table = torch.from_numpy(np.array(recs, dtype=DFIT_DTYPE).view(np.uint8)).to(dev)
         torch.cuda.synchronize(dev)
-        fit_device(table, len(batches), self.T, stream)
+        max_lf = max(np.asarray(X32).size for X32, _, _ in batches) if self.fused else -1
+        fit_device(table, len(batches), self.T, stream, max_lf)
         stream.synchronize()
         res = res_d.cpu().numpy()
         out = []

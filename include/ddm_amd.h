@@ -253,6 +253,15 @@ int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t stream_len, 
                      const uint8_t* perm_map, ddm_stream_t stream, ddm_event_t ev_begin,
                      ddm_event_t ev_end);
 
+/* ddm_scan_streams (mode, state, stop, perm_map and first_nz as there) with the events
+ * appended to per-stream logs instead of dense rows: for every batch b of stream s with an
+ * event, logs[s][3 * k] = (log_b0[s] + b, first warning pos, change pos) at
+ * k = log_n[s * log_n_stride]++ (the device-resident runner's event logs, csrc/ctl.hip). */
+int ddm_scan_streams_log(const uint8_t* err, const int64_t* stream_off, int64_t n_streams, const ddm_params* prm,
+                         ddm_state* state_io, const uint64_t* first_nz, int32_t* const* logs, int64_t* log_n,
+                         int64_t log_n_stride, const int64_t* log_b0, int32_t* stop_out, int32_t mode,
+                         const uint8_t* perm_map, const int64_t* stream_end, ddm_stream_t stream);
+
 /* run_DDM over LONG carried segments (DDM_Process.py:135-159 with the DDM carried across
  * batches, :144-152, :202): the results of ddm_scan_streams (same stream_off / stream_end /
  * batch_base / ev_out / stop_out / nev_out / mode / perm_map meaning) for streams whose
@@ -499,6 +508,10 @@ int64_t ddm_rf_device_scratch_bytes(int32_t L, int32_t F, int32_t n_trees, int32
 /* Fits every job (device table of n_jobs records) on `stream`; max_trees bounds the
  * jobs' n_trees (grid size).  Asynchronous: results land in each job's result[]. */
 int ddm_rf_fit_device(const ddm_dfit_job* jobs_dev, int32_t n_jobs, int32_t max_trees, ddm_stream_t stream);
+/* The same with max_lf >= every job's L*F: batches of at most 4096 values are gated, checked
+ * and presorted inside the tree kernel (one launch fewer); max_lf <= 0: unknown. */
+int ddm_rf_fit_device_lf(const ddm_dfit_job* jobs_dev, int32_t n_jobs, int32_t max_trees, int64_t max_lf,
+                         ddm_stream_t stream);
 
 /* ---- epoch executor (csrc/epoch.hip) -------------------------------------------- */
 /* One call enqueues a BatchRunner epoch on `stream`: ctrl_d[0, upload_bytes) <- ctrl_h
@@ -529,6 +542,7 @@ typedef struct ddm_epoch {
     /* split read-back (mid_ev != NULL): the slab right after the staging, then mid_ev,
      * and after the refits only ctrl[tail_off, tail_off + tail_bytes) (their results) */
     ddm_event_t mid_ev; int64_t tail_off, tail_bytes;
+    int64_t dfit_max_lf;     /* ddm_rf_fit_device_lf's max_lf (<= 0: unknown)              */
 } ddm_epoch;
 int ddm_epoch_launch(const ddm_epoch* e);
 int64_t ddm_epoch_struct_bytes(void);   /* sizeof(ddm_epoch), for binding checks */
@@ -573,6 +587,8 @@ typedef struct ddm_ctl {
     int64_t* loff; int64_t* lend; int32_t* pstall;   /* per partition: set by the predict    */
     int64_t predict_blocks;                        /* grid of ddm_forest_predict_dev          */
     int64_t* status;                               /* [4]: active, stalled, parked, done       */
+    int32_t* const* logs;                          /* per partition: its event log             */
+    int64_t* log_b0;                               /* per partition: the window's first batch  */
 } ddm_ctl;
 
 typedef struct ddm_ctl_epoch {
@@ -585,7 +601,7 @@ typedef struct ddm_ctl_epoch {
     int64_t long_max_rows; void* long_scratch;
     const ddm_dfit_job* dfit_jobs; int32_t n_dfit, max_trees;
     int64_t max_W, max_pieces;                     /* shuffle grid bounds (windows never exceed) */
-    int64_t status_h_off;                          /* unused (reserved)                        */
+    int64_t dfit_max_lf;                           /* ddm_rf_fit_device_lf's max_lf             */
     ddm_event_t ev[12];                            /* optional begin/end pairs: predict, scan, long,
                                                       stage + ctl, refit, next shuffles        */
 } ddm_ctl_epoch;

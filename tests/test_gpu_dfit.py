@@ -12,9 +12,9 @@ def _host(batches):
     return BatchForestTrainer(100, n_threads=4).fit_many(batches)
 
 
-def _device(batches, k_cap=16):
+def _device(batches, k_cap=16, fused=True):
     from ddm_amd.dfit import DeviceTrainer
-    return DeviceTrainer(100, k_cap=k_cap).fit_many(batches)
+    return DeviceTrainer(100, k_cap=k_cap, fused=fused).fit_many(batches)
 
 
 def _same(h, d):
@@ -59,11 +59,13 @@ def _batch(rs, L, F, K, kind):
 @pytest.mark.parametrize("L,F,K,kind", [(100, 27, 2, "separable"), (100, 21, 10, "noisy"), (100, 12, 3, "ties"),
                                         (100, 9, 4, "impure"), (256, 5, 5, "noisy"), (7, 3, 2, "noisy"),
                                         (2, 4, 2, "noisy"), (150, 40, 16, "noisy"), (64, 6, 30, "noisy")])
-def test_device_refit_matches_host(L, F, K, kind):
+@pytest.mark.parametrize("fused", [True, False])
+def test_device_refit_matches_host(L, F, K, kind, fused):
+    """fused: batches of <= 4096 values prepared inside the tree kernel; else k_dfit_prep."""
     rs = np.random.RandomState(L * 1000 + F * 10 + K)
     batches = [_batch(rs, L, F, K, kind) for _ in range(3)]
     host = _host(batches)
-    dev = _device(batches, k_cap=64 if K > 16 else 16)
+    dev = _device(batches, k_cap=64 if K > 16 else 16, fused=fused)
     for h, d in zip(host, dev):
         _same(h, d)
 
@@ -82,6 +84,7 @@ def test_device_refit_reports_nan_and_class_overflow():
     Xn = X.copy()
     Xn[3, 2] = np.nan
     yk = np.arange(50) % 20
-    out = _device([(Xn, y, seeds), (X, yk, seeds)], k_cap=16)
-    assert out[0][3][0] == DDM_E_NAN
-    assert out[1][3][0] == DDM_E_FOREST and out[1][3][1] == 20
+    for fused in (True, False):
+        out = _device([(Xn, y, seeds), (X, yk, seeds)], k_cap=16, fused=fused)
+        assert out[0][3][0] == DDM_E_NAN
+        assert out[1][3][0] == DDM_E_FOREST and out[1][3][1] == 20
