@@ -17,6 +17,7 @@
 // job.  Thread t owns partition t; thread 0 then splits the predict grid over the windows.
 // The decisions are the host controller's, line for line: results do not depend on which
 // side took them (tests/test_gpu_devctl.py runs both on the same partitions).
+#include <algorithm>
 #include <cstddef>
 
 #include "common.h"
@@ -61,6 +62,7 @@ __device__ __forceinline__ int64_t blen(const ddm_ctl_part& p, int64_t b) { retu
 // tables) when it is done, parked, stalled, or its stream words are not tabulated yet.
 __device__ void plan(const ddm_ctl& c, ddm_ctl_part& p, int i) {
     const int64_t pb = p.pb;
+    p.log_mark = p.n_log;                           // this epoch's scans append after it
     bool active = !(p.done || p.stall || p.park);
     const bool apply = active && p.retrain;
     const int64_t P_eff = apply ? p.P2 : p.P;
@@ -191,6 +193,9 @@ __device__ void plan(const ddm_ctl& c, ddm_ctl_part& p, int i) {
 __device__ void commit(const ddm_ctl& c, ddm_ctl_part& p, int i) {
     if (p.idle || p.done || p.park) return;
     if (c.pstall[i]) {                              // the predict found the refit unusable
+        // the predict wrote no errors for this window, so the scans read stale bytes: their
+        // events are void (the host redoes the epoch)
+        p.n_log = p.log_mark;
         p.stall = DDM_CTL_STALL_REFIT;
         if (p.applied) {                            // the host redoes the refit (_finish_pending)
             p.retrain = 1;
@@ -201,6 +206,7 @@ __device__ void commit(const ddm_ctl& c, ddm_ctl_part& p, int i) {
     }
     const int32_t stop = c.stop[i];
     p.epochs += 1;
+    if (c.lend[i] > c.loff[i]) p.long_scans += 1;   // this epoch's window ran on ddm_scan_long
     const int64_t rows = p.p1 - p.p0;
     p.predicted_rows += rows;
     int64_t slots = p.host_slots;
@@ -285,6 +291,12 @@ int launch_ctl(const ddm_ctl& c, int entry, hipStream_t s) {
     return ddm::launch_status("ddm_ctl");
 }
 
+// The window shuffles' grids: the replay and perms kernels stride over pieces and batches,
+// so a device-planned window of any size is covered by a fixed grid; sizing it by the
+// largest window the runner allows (65,536 batches) launched ~13k mostly idle blocks per
+// epoch (C5: 64 us of every epoch).
+constexpr int64_t kShufW = 64 * 256, kShufPieces = 256;
+
 int rec(ddm_event_t e, hipStream_t s) {
     return e ? ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(e), s), "event record") : 0;
 }
@@ -303,7 +315,8 @@ extern "C" int ddm_ctl_enter(const ddm_ctl_epoch* e) {
     }
     hipStream_t s = ddm::as_hip(e->stream);
     if (int rc = launch_ctl(e->ctl, 1, s)) return rc;
-    return ddm_shuffle_window_batch(e->ctl.jobs, e->ctl.n, e->max_W, e->max_pieces, e->per_batch, e->stream,
+    return ddm_shuffle_window_batch(e->ctl.jobs, e->ctl.n, std::min(e->max_W, kShufW),
+                                    std::min(e->max_pieces, kShufPieces), e->per_batch, e->stream,
                                     nullptr, nullptr);
 }
 
@@ -344,7 +357,8 @@ extern "C" int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs) {
         if (int rc = ddm::hip_status(hipStreamWaitEvent(side, reinterpret_cast<hipEvent_t>(e->fork_ev), 0), "fork"))
             return rc;
         if (int rc = rec(e->ev[10], side)) return rc;
-        if (int rc = ddm_shuffle_window_batch(c.jobs, c.n, e->max_W, e->max_pieces, e->per_batch, e->side_stream,
+        if (int rc = ddm_shuffle_window_batch(c.jobs, c.n, std::min(e->max_W, kShufW),
+                                              std::min(e->max_pieces, kShufPieces), e->per_batch, e->side_stream,
                                               nullptr, nullptr))
             return rc;
         if (int rc = rec(e->ev[11], side)) return rc;

@@ -58,6 +58,14 @@ struct Job {
 };
 static_assert(sizeof(Job) == sizeof(ddm_dfit_job), "Job must mirror ddm_dfit_job");
 
+// A job whose gate says "no refit this epoch" (no change: *gate < 0; or batch d+1's shuffle
+// and the seeds were not staged: *gate2 != 1).  Every kernel of the refit checks it, and
+// nothing is written: the result words keep the partition's last refit, whose forest the
+// device-resident runner's predict is still using.
+__device__ __forceinline__ bool gated_off(const Job& jb) {
+    return (jb.gate && *jb.gate < 0) || (jb.gate2 && *jb.gate2 != 1);
+}
+
 // Tree node in creation (_add_node) order, which is pre-order (depth first, left child
 // first): a node's left subtree is the id range [id + 1, right).
 struct TNode {
@@ -198,15 +206,12 @@ __global__ __launch_bounds__(kPrepThreads) void k_dfit_prep(const Job* __restric
     __shared__ uint8_t s_first[kMaxL];
     __shared__ int s_nan, s_K, s_skip;
     if (t == 0) {
-        s_skip = (jb.gate && *jb.gate < 0) || (jb.gate2 && *jb.gate2 != 1);
+        s_skip = gated_off(jb);
         s_nan = 0;
         s_K = 0;
     }
     __syncthreads();
-    if (s_skip) {
-        if (t == 0) jb.result[DDM_DFIT_STATUS] = -1;
-        return;
-    }
+    if (s_skip) return;                          // the result words keep the last refit's
     const int L = jb.L, F = jb.F;
     if (L < 1 || L > kMaxL || F < 1 || F > kMaxF || jb.n_trees < 1 || jb.n_trees > 256 || jb.k_cap < 1 ||
         jb.k_cap > kMaxK ||
@@ -649,15 +654,12 @@ __device__ __forceinline__ bool fused_prep(const Job& jb, float* s_X, uint8_t* s
     constexpr int kT = 64 * kWaves;
     const bool lead = blockIdx.x == 0;
     if (t == 0) {
-        s_skip = (jb.gate && *jb.gate < 0) || (jb.gate2 && *jb.gate2 != 1);
+        s_skip = gated_off(jb);
         s_nan = 0;
         s_K = 0;
     }
     __syncthreads();
-    if (s_skip) {
-        if (lead && t == 0) jb.result[DDM_DFIT_STATUS] = -1;
-        return false;
-    }
+    if (s_skip) return false;                    // the result words keep the last refit's
     const int L = jb.L, F = jb.F;
     if (L < 1 || L > kMaxL || F < 1 || F > kMaxF || jb.n_trees < 1 || jb.n_trees > 256 || jb.k_cap < 1 ||
         jb.k_cap > kMaxK || jb.max_features < 1) {
@@ -730,7 +732,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfit_trees(const Job* __restric
         if (tree < jb.n_trees) build_tree(jb, lo, tree, K, lds[w], lane, s_X, s_ord, s_yi);
         return;
     }
-    if (jb.result[DDM_DFIT_STATUS] != 0) return;
+    if (gated_off(jb) || jb.result[DDM_DFIT_STATUS] != 0) return;
     const int K = (int)jb.result[DDM_DFIT_CLASSES];
     const Layout lo = layout(jb.L, jb.F, jb.n_trees, jb.k_cap);
     const int LF = jb.L * jb.F;
@@ -1176,7 +1178,7 @@ __global__ __launch_bounds__(kPackThreads) void k_dfit_pack(const Job* __restric
 #ifdef DDM_DFIT_PROFILE
     const uint64_t t_pack0 = wall_clock64();
 #endif
-    if (jb.result[DDM_DFIT_STATUS] != 0) return;
+    if (gated_off(jb) || jb.result[DDM_DFIT_STATUS] != 0) return;
     const int t = threadIdx.x;
     const int T = jb.n_trees, K = (int)jb.result[DDM_DFIT_CLASSES];
     const Layout lo = layout(jb.L, jb.F, T, jb.k_cap);

@@ -12,7 +12,7 @@ import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 # DDM_AMD_LIB: an alternative build of the same library (e.g. an instrumented one)
 LIB_PATH = os.environ.get("DDM_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
@@ -90,6 +90,9 @@ SIGNATURES = {
     "ddm_scan_batches": (ctypes.c_int, [_vp, _i64, _i64, ctypes.POINTER(DdmParams), _vp, _vp, _vp, _vp, _vp, _vp,
                                         _vp, _vp]),
     "ddm_scan_batches_scratch_bytes": (_i64, [_i64, _i64, _i32]),
+    "ddm_scan_batches_v1": (ctypes.c_int, [_vp, _i64, _i64, ctypes.POINTER(DdmParams), _vp, _vp, _vp, _vp, _vp, _vp,
+                                           _vp, _vp]),
+    "ddm_scan_batches_v1_scratch_bytes": (_i64, [_i64, _i64, _i32]),
     "ddm_scan_long": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, ctypes.POINTER(DdmParams), _vp, _vp, _vp, _vp, _vp,
                                      _i32, _vp, _vp, _vp, _vp, _vp]),
     "ddm_scan_long_scratch_bytes": (_i64, [_i64, _i64, _i32]),

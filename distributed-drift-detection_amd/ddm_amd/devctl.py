@@ -339,6 +339,7 @@ class DeviceController:
             if applied:
                 q["retrain"] = 1
             st.predicted_rows += int(q["predicted_rows"])
+            st.long_scans += int(q["long_scans"])
             st.predict_bytes += int(q["predict_bytes"])
             st.refits += int(q["refits"]) - applied
             st.device_refits += int(q["refits"]) - applied

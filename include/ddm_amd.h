@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 15
+#define DDM_AMD_ABI_VERSION 16
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -252,6 +252,13 @@ int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t stream_len, 
                      ddm_state* state_io, int32_t* ev_out, int64_t* nev_out, void* scratch,
                      const uint8_t* perm_map, ddm_stream_t stream, ddm_event_t ev_begin,
                      ddm_event_t ev_end);
+/* The round-2 form of ddm_scan_batches (speculative classify pass + exact / walk / chain
+ * kernels), kept for A/B measurement; same arguments, its own scratch size. */
+int64_t ddm_scan_batches_v1_scratch_bytes(int64_t n_streams, int64_t stream_len, int32_t per_batch);
+int ddm_scan_batches_v1(const uint8_t* err, int64_t n_streams, int64_t stream_len, const ddm_params* prm,
+                        ddm_state* state_io, int32_t* ev_out, int64_t* nev_out, void* scratch,
+                        const uint8_t* perm_map, ddm_stream_t stream, ddm_event_t ev_begin,
+                        ddm_event_t ev_end);
 
 /* ddm_scan_streams (mode, state, stop, perm_map and first_nz as there) with the events
  * appended to per-stream logs instead of dense rows: for every batch b of stream s with an
@@ -492,7 +499,7 @@ typedef struct ddm_dfit_job {
     int64_t* result;         /* device int64[12]: DDM_DFIT_* indices                        */
 } ddm_dfit_job;
 
-#define DDM_DFIT_STATUS    0   /* -1 not run (gate), 0 ok, DDM_E_NAN / DDM_E_FOREST / DDM_E_ARG */
+#define DDM_DFIT_STATUS    0   /* 0 ok, DDM_E_NAN / DDM_E_FOREST / DDM_E_ARG; a gated-off job writes nothing */
 #define DDM_DFIT_CLASSES   1
 #define DDM_DFIT_NODES     2
 #define DDM_DFIT_PURE      3
@@ -573,6 +580,8 @@ typedef struct ddm_ctl_part {
     int64_t g0, b_end, Wg, P_after_first, p0, p1;
     ddm_state state;
     int64_t n_log, predicted_rows, predict_bytes, epochs, refits;
+    int64_t log_mark;            /* n_log before this epoch's scans: restored when the epoch stalls */
+    int64_t long_scans;          /* windows that ran on ddm_scan_long (statistics) */
 } ddm_ctl_part;
 
 /* Stall reasons (ddm_ctl_part.stall) */

@@ -7,6 +7,8 @@
 #              + bench NAME [bench.py args]   -> gpurun_out/bench_NAME.json (+ .err)
 #              + prof NAME [bench.py args]    -> gpurun_out/prof_NAME/ (rocprofv3 --kernel-trace --stats)
 #              + pmc NAME REGEX [bench args]  -> gpurun_out/pmc_NAME_{FETCH_SIZE,WRITE_SIZE}/ (one pass each)
+#              + pmcx NAME REGEX 'CTR ...' [bench args] -> gpurun_out/pmcx_NAME/ (one pass of those counters)
+#              + run NAME script.py [args]    -> gpurun_out/run_NAME.log
 #              + htrace NAME [bench.py args]  -> gpurun_out/htrace_NAME.json (host phase marks, DDM_HOST_TRACE)
 #
 # e.g. tools/gpu.sh tests + bench c3 + bench c2 --workload c2 + prof c3 --cpu-baseline 0
@@ -58,6 +60,20 @@ PY
                 || { tail -10 gpurun_out/pmc_${name}_$c.err; fail pmc $name $c; }
         done
         echo "pmc $name done" ;;
+    pmcx)
+        # one pass of the given counters (quoted, space separated; within one pass's slots)
+        local name=$1 rx=$2 ctrs=$3; shift 3
+        rm -rf gpurun_out/pmcx_${name}
+        timeout -s KILL 300 rocprofv3 --pmc $ctrs --kernel-include-regex "$rx" --output-format csv \
+            -d gpurun_out/pmcx_${name} -o p -- python3 bench.py "$@" \
+            > gpurun_out/pmcx_${name}.json 2> gpurun_out/pmcx_${name}.err \
+            || { tail -10 gpurun_out/pmcx_${name}.err; fail pmcx $name; }
+        echo "pmcx $name done" ;;
+    run)
+        # any python script of the repo: run NAME script.py [args] -> gpurun_out/run_NAME.log
+        local name=$1; shift
+        timeout -k 10 600 python -u "$@" > gpurun_out/run_$name.log 2>&1 || { tail -30 gpurun_out/run_$name.log; fail run $name; }
+        tail -5 gpurun_out/run_$name.log ;;
     htrace)
         local name=$1; shift
         DDM_HOST_TRACE=1 DDM_HOST_TRACE_OUT=gpurun_out/htrace_$name.json timeout -k 10 300 python -u bench.py "$@" \
