@@ -244,19 +244,42 @@ __device__ void commit(const ddm_ctl& c, ddm_ctl_part& p, int i) {
     if (p.j >= p.nb) p.done = 1;
 }
 
+// A wave per partition record: the 1 KB record comes into LDS by one coalesced load of the
+// wave, lane 0 takes the decisions on the LDS copy, and the wave writes it back (holding
+// the record in one thread's registers cost 208 VGPRs and 616 B of scratch: 31 us per call).
+constexpr int kCtlWaves = kCtlThreads / 64;
+constexpr int kPartVec = (int)(sizeof(ddm_ctl_part) / 16);
+static_assert(sizeof(ddm_ctl_part) % 16 == 0, "ddm_ctl_part: 16-byte multiple");
+
 __global__ __launch_bounds__(kCtlThreads) void k_ctl(const ddm_ctl c) {
-    __shared__ int64_t s_rows[kCtlThreads];
+    __shared__ ddm_ctl_part s_part[kCtlWaves];
     __shared__ int s_count[4];
     const int t = threadIdx.x;
+    const int lane = t & 63, w = t >> 6;
     if (t < 4) s_count[t] = 0;
     __syncthreads();
-    for (int i = t; i < c.n; i += kCtlThreads) {
-        ddm_ctl_part p = c.parts[i];
-        if (!c.entry) commit(c, p, i);
-        plan(c, p, i);
-        c.parts[i] = p;
-        atomicAdd(&s_count[p.done ? 3 : p.stall ? 1 : p.park ? 2 : 0], 1);
+    for (int i = w; i < c.n; i += kCtlWaves) {
+        const uint4* src = reinterpret_cast<const uint4*>(c.parts + i);
+        uint4* lds = reinterpret_cast<uint4*>(&s_part[w]);
+        for (int k = lane; k < kPartVec; k += 64) lds[k] = src[k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane == 0) {
+            ddm_ctl_part& p = s_part[w];
+            if (!c.entry) commit(c, p, i);
+            plan(c, p, i);
+            atomicAdd(&s_count[p.done ? 3 : p.stall ? 1 : p.park ? 2 : 0], 1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint4* dst = reinterpret_cast<uint4*>(c.parts + i);
+        for (int k = lane; k < kPartVec; k += 64) dst[k] = lds[k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
+    __threadfence();
     __syncthreads();
     // the predict grid, split over the windows in proportion to their rows (at least one
     // block per non-empty window)
@@ -281,7 +304,6 @@ __global__ __launch_bounds__(kCtlThreads) void k_ctl(const ddm_ctl c) {
             for (int k = 0; k < 4; ++k) c.status[k] = s_count[k];
         }
     }
-    (void)s_rows;
 }
 
 int launch_ctl(const ddm_ctl& c, int entry, hipStream_t s) {
@@ -296,6 +318,15 @@ int launch_ctl(const ddm_ctl& c, int entry, hipStream_t s) {
 // largest window the runner allows (65,536 batches) launched ~13k mostly idle blocks per
 // epoch (C5: 64 us of every epoch).
 constexpr int64_t kShufW = 64 * 256, kShufPieces = 256;
+
+}  // namespace
+
+extern "C" int ddm_scan_long_reuse(const uint8_t* err, const int64_t* stream_off, const int64_t* stream_end,
+                                   int64_t n_streams, int64_t max_rows, const ddm_params* prm, ddm_state* state_io,
+                                   const int64_t* batch_base, int32_t* ev_out, int32_t* stop_out, int64_t* nev_out,
+                                   int32_t mode, const uint8_t* perm_map, void* scratch, ddm_stream_t stream);
+
+namespace {
 
 int rec(ddm_event_t e, hipStream_t s) {
     return e ? ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(e), s), "event record") : 0;
@@ -314,6 +345,12 @@ extern "C" int ddm_ctl_enter(const ddm_ctl_epoch* e) {
         return DDM_E_ARG;
     }
     hipStream_t s = ddm::as_hip(e->stream);
+    if (e->long_max_rows > 0) {                     // zeroed once; every epoch's call leaves it zeroed
+        const int64_t lb = ddm_scan_long_scratch_bytes(e->ctl.n, e->long_max_rows, e->per_batch);
+        if (lb > 0)
+            if (int rc = ddm::hip_status(hipMemsetAsync(e->long_scratch, 0, (size_t)lb, s), "ddm_ctl_enter: memset"))
+                return rc;
+    }
     if (int rc = launch_ctl(e->ctl, 1, s)) return rc;
     return ddm_shuffle_window_batch(e->ctl.jobs, e->ctl.n, std::min(e->max_W, kShufW),
                                     std::min(e->max_pieces, kShufPieces), e->per_batch, e->stream,
@@ -342,9 +379,9 @@ extern "C" int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs) {
                                           const_cast<int32_t*>(c.stop), 0, e->perm_map, c.end, e->stream))
             return rc;
         if (e->long_max_rows > 0)
-            if (int rc = ddm_scan_long(e->err, c.loff, c.lend, c.n, e->long_max_rows, e->params, c.state, e->batch_base,
-                                       e->ev_out, const_cast<int32_t*>(c.stop), e->nev, 0, e->perm_map, e->long_scratch,
-                                       e->stream, nullptr, nullptr))
+            if (int rc = ddm_scan_long_reuse(e->err, c.loff, c.lend, c.n, e->long_max_rows, e->params, c.state,
+                                             e->batch_base, e->ev_out, const_cast<int32_t*>(c.stop), e->nev, 0,
+                                             e->perm_map, e->long_scratch, e->stream))
                 return rc;
         if (int rc = ddm_shuffle_pick_batch(c.jobs, c.n, e->stream)) return rc;
         if (int rc = rec(e->ev[3], s)) return rc;

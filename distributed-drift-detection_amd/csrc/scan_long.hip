@@ -44,6 +44,27 @@ struct Carry {                 // a chunk's inclusive state (look-back record)
     int64_t stop;              // batch of the (mode 0) change or -1
 };
 
+// Every block ends here: the last one to finish re-zeroes the dispatch ticket and the
+// look-back flags, so the scratch is ready for the next call without a memset (the
+// device-resident runner launches ddm_scan_long every epoch, mostly on empty windows).
+__device__ __forceinline__ void long_block_done(uint32_t* ticket, int32_t* flag, int64_t n_flags, uint32_t grid) {
+    __shared__ int s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        s_last = atomicAdd(ticket + 2, 1u) == grid - 1;
+    }
+    __syncthreads();
+    if (s_last) {
+        __threadfence();
+        for (int64_t q = threadIdx.x; q < n_flags; q += blockDim.x) flag[q] = 0;
+        if (threadIdx.x == 0) {
+            ticket[0] = 0;
+            ticket[2] = 0;
+        }
+    }
+}
+
 __global__ __launch_bounds__(64) void k_scan_long(
     const uint8_t* __restrict__ err, const int64_t* __restrict__ off, const int64_t* __restrict__ stream_end,
     int64_t n_streams, int64_t n_chunks, ddm_params P, ddm_state* __restrict__ state,
@@ -60,12 +81,19 @@ __global__ __launch_bounds__(64) void k_scan_long(
     __syncthreads();
     const int64_t t = stk;
     const int64_t c = t / n_streams, sid = t % n_streams;     // chunk-major: chunk c-1 holds an earlier ticket
-    if (c >= n_chunks) return;
+    const uint32_t grid = gridDim.x;
+    if (c >= n_chunks) {
+        long_block_done(ticket, flag, n_streams * n_chunks, grid);
+        return;
+    }
     const int64_t lo = off[sid], hi = stream_end ? stream_end[sid] : off[sid + 1];
     const int pb = P.per_batch;
     const int64_t C = 64 * (int64_t)pb;
     const int64_t c0 = lo + c * C;
-    if (c0 >= hi) return;                                      // no such chunk (empty streams: untouched)
+    if (c0 >= hi) {                                            // no such chunk (empty streams: untouched)
+        long_block_done(ticket, flag, n_streams * n_chunks, grid);
+        return;
+    }
     const int64_t c1 = min(c0 + C, hi);
     const int64_t last_chunk = (hi - lo - 1) / C;
     const int min_inst = P.min_num_instances;
@@ -240,6 +268,7 @@ __global__ __launch_bounds__(64) void k_scan_long(
         if (stop_out) stop_out[sid] = failed ? kLongFailed : (int32_t)outc.stop;
         if (nev_out) nev_out[sid] = failed ? 0 : outc.nev;
     }
+    long_block_done(ticket, flag, n_streams * n_chunks, grid);
 }
 
 struct LongScratch {
@@ -265,11 +294,11 @@ extern "C" int64_t ddm_scan_long_scratch_bytes(int64_t n_streams, int64_t max_ro
         .bytes;
 }
 
-extern "C" int ddm_scan_long(const uint8_t* err, const int64_t* stream_off, const int64_t* stream_end,
-                             int64_t n_streams, int64_t max_rows, const ddm_params* prm, ddm_state* state_io,
-                             const int64_t* batch_base, int32_t* ev_out, int32_t* stop_out, int64_t* nev_out,
-                             int32_t mode, const uint8_t* perm_map, void* scratch, ddm_stream_t stream,
-                             ddm_event_t ev_begin, ddm_event_t ev_end) {
+static int scan_long_launch(const uint8_t* err, const int64_t* stream_off, const int64_t* stream_end,
+                            int64_t n_streams, int64_t max_rows, const ddm_params* prm, ddm_state* state_io,
+                            const int64_t* batch_base, int32_t* ev_out, int32_t* stop_out, int64_t* nev_out,
+                            int32_t mode, const uint8_t* perm_map, void* scratch, ddm_stream_t stream,
+                            ddm_event_t ev_begin, ddm_event_t ev_end, bool zero) {
     if (!err || !stream_off || !prm || !state_io || !batch_base || !ev_out || !scratch || n_streams < 0 ||
         max_rows < 0 || prm->per_batch <= 0 || prm->per_batch > kLongMaxBatch || (mode != 0 && mode != 1)) {
         ddm::set_error("ddm_scan_long: invalid argument (per_batch must be 1..%d)", kLongMaxBatch);
@@ -286,8 +315,9 @@ extern "C" int ddm_scan_long(const uint8_t* err, const int64_t* stream_off, cons
     hipStream_t s = ddm::as_hip(stream);
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
-    if (int rc = ddm::hip_status(hipMemsetAsync(scratch, 0, (size_t)sc.flag_bytes, s), "ddm_scan_long: memset"))
-        return rc;
+    if (zero)
+        if (int rc = ddm::hip_status(hipMemsetAsync(scratch, 0, (size_t)sc.flag_bytes, s), "ddm_scan_long: memset"))
+            return rc;
     hipLaunchKernelGGL(k_scan_long, dim3((unsigned)grid), dim3(64), 0, s, err, stream_off, stream_end, n_streams,
                        n_chunks, *prm, state_io, batch_base, ev_out, stop_out, nev_out, (int)mode, perm_map,
                        sc.ticket, sc.flag, sc.carry, g_spin_limit);
@@ -295,6 +325,25 @@ extern "C" int ddm_scan_long(const uint8_t* err, const int64_t* stream_off, cons
     if (ev_end)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
     return 0;
+}
+
+extern "C" int ddm_scan_long(const uint8_t* err, const int64_t* stream_off, const int64_t* stream_end,
+                             int64_t n_streams, int64_t max_rows, const ddm_params* prm, ddm_state* state_io,
+                             const int64_t* batch_base, int32_t* ev_out, int32_t* stop_out, int64_t* nev_out,
+                             int32_t mode, const uint8_t* perm_map, void* scratch, ddm_stream_t stream,
+                             ddm_event_t ev_begin, ddm_event_t ev_end) {
+    return scan_long_launch(err, stream_off, stream_end, n_streams, max_rows, prm, state_io, batch_base, ev_out,
+                            stop_out, nev_out, mode, perm_map, scratch, stream, ev_begin, ev_end, true);
+}
+
+// The device-resident runner's form (csrc/ctl.hip): the scratch was zeroed once when the
+// runner entered device mode and every call leaves it zeroed (long_block_done).
+extern "C" int ddm_scan_long_reuse(const uint8_t* err, const int64_t* stream_off, const int64_t* stream_end,
+                                   int64_t n_streams, int64_t max_rows, const ddm_params* prm, ddm_state* state_io,
+                                   const int64_t* batch_base, int32_t* ev_out, int32_t* stop_out, int64_t* nev_out,
+                                   int32_t mode, const uint8_t* perm_map, void* scratch, ddm_stream_t stream) {
+    return scan_long_launch(err, stream_off, stream_end, n_streams, max_rows, prm, state_io, batch_base, ev_out,
+                            stop_out, nev_out, mode, perm_map, scratch, stream, nullptr, nullptr, false);
 }
 
 extern "C" int ddm_scan_long_set_spin_limit(uint32_t spins) {

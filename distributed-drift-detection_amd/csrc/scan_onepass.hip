@@ -42,9 +42,9 @@ constexpr int kChunkBatches = 64;               // batches per image (lane b own
 constexpr int kPre = 16;
 constexpr int kPreN = 1 << kPre;
 constexpr int64_t kNoCert = (int64_t)1 << 24;  // fp32 holds k and n exactly below this
-// scratch counters: [0] replays that hit a change (never: the rows were certified), [1]
-// batches evaluated by certified rows, [2] of them not certified (exact path), [3] exact
-// end-state replays
+// scratch counters: [0] replays that hit a change (never: the rows were certified); in a
+// -DDDM_OP_COUNT build also [1] batches evaluated by certified rows, [2] of them not
+// certified (exact path), [3] exact end-state replays
 constexpr int kWalkCount = 4;
 
 // ---------------------------------------------------------------- bit helpers
@@ -80,6 +80,12 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ float readlane_f(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -93,8 +99,10 @@ __device__ __forceinline__ void wave_sync_lds() {
 // ---------------------------------------------------------------- the prefix table
 // A fresh detector's first kPre rows depend only on their kPre error bits.  Entry m (bit t
 // = row t is an error): (first warning row + 1) | (change row + 1) << 5 inside the prefix
-// (0 = none), stepped by det_add_fast (the production recurrence, bit for bit).
-__global__ __launch_bounds__(256) void k_prefix_table(ddm_params P, uint16_t* __restrict__ ptab) {
+// (0 = none), and pst[m] the detector after row kPre - 1 when there is no change (n = kPre
+// + 1), stepped by det_add_fast (the production recurrence, bit for bit).
+__global__ __launch_bounds__(256) void k_prefix_table(ddm_params P, uint16_t* __restrict__ ptab,
+                                                      double4* __restrict__ pst) {
     __shared__ double rcp[kPre + 2];
     if (threadIdx.x < kPre + 2) rcp[threadIdx.x] = 1.0 / (double)(threadIdx.x > 0 ? threadIdx.x : 1);
     __syncthreads();
@@ -112,6 +120,7 @@ __global__ __launch_bounds__(256) void k_prefix_table(ddm_params P, uint16_t* __
         }
     }
     ptab[m] = (uint16_t)((wpos + 1) | ((cpos + 1) << 5));
+    pst[m] = make_double4(d.p, d.pmin, d.smin, d.psmin);      // the detector after row kPre - 1
 }
 
 // ---------------------------------------------------------------- certified rows
@@ -244,6 +253,10 @@ struct BatchRes {
 __device__ __forceinline__ BatchRes cert_batch(CDet& D, uint64_t m0, uint64_t m1, int blen, int min_inst, float wl,
                                                float cl) {
     BatchRes r{-1, -1, 0};
+#ifdef DDM_OP_NOCERT      // timing variant (tools/build_variant.sh): results are NOT the scan's
+    r.c = 0;
+    return r;
+#endif
     TileRes t = cert_tile(D, m0, min(blen, 64), min_inst, wl, cl);
     if (t.bad) {
         r.bad = 1;
@@ -355,8 +368,11 @@ __device__ __forceinline__ void chunk_load(const uint8_t* __restrict__ err, cons
 
 enum : int { kFresh = 0, kTriv = 1, kCarr = 2 };
 
+#ifndef DDM_OP_WAVES
+#define DDM_OP_WAVES 4
+#endif
 template <bool kPmap, int kLoads>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_scan_onepass(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(DDM_OP_WAVES))) void k_scan_onepass(
     const uint8_t* __restrict__ err, int64_t n_streams, int64_t L, int64_t nb, ddm_params P,
     ddm_state* __restrict__ state, int2* __restrict__ ev, int64_t* __restrict__ nev_out,
     const uint8_t* __restrict__ pmap, const uint16_t* __restrict__ ptab, int use_pre, uint32_t* __restrict__ cnt_out) {
@@ -536,7 +552,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
                 if (cd.cc + bj_len < kNoCert) {
                     const uint64_t a0 = readlane64(m0, j), a1 = readlane64(m1, j);
                     const BatchRes r = cert_batch(cd, a0, a1, bj_len, min_inst, wlf, clf);
+#ifdef DDM_OP_COUNT
                     if (lane == 0) atomicAdd(cnt_out + 1 + r.bad, 1u);
+#endif
                     if (!r.bad) {
                         if (lane == j) {
                             rw = r.w;
@@ -551,7 +569,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
                 job = 1;
             } else if (last_chunk && kind == kCarr && !xact) {
                 job = 2;
+#ifdef DDM_OP_COUNT
                 if (lane == 0) atomicAdd(cnt_out + 3, 1u);
+#endif
             } else {
                 break;
             }
@@ -657,6 +677,407 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
 }
 
+// ---------------------------------------------------------------- streams of <= 64 batches
+// The same walk with exact rows only.  A wave classifies a GROUP of streams (at most kSlots,
+// their open batches at most 64), then runs the open batches -- fresh detectors whose
+// change the speculation did not find -- one per lane with the exact recurrence (all 64
+// lanes busy: a batch costs ~1/64 of a wave per row, against a whole wave-wide tile), then
+// walks the group's streams.  A batch with a carried detector (after an unchanged one, rare
+// in a reset-heavy stream) runs wave-wide (xtile) from the exact detector the walk holds.
+// Every detector the walk holds is exact, so the handed-back state is too.
+constexpr int kSlots = 20;
+constexpr int kBatchRcp = 2 * kMaxBatch + 2;
+
+// 128-bit nonzero mask of the rows [bstart, bstart + blen), blen in 1..128, by nine 16-byte
+// loads of this lane (the rare carried batches read their bytes again)
+__device__ __forceinline__ void batch_mask(const uint8_t* __restrict__ err, int64_t bstart, int blen, uint64_t& m0,
+                                           uint64_t& m1) {
+    const int64_t c0 = bstart & ~(int64_t)15;
+    const int64_t clast = (bstart + blen - 1) & ~(int64_t)15;
+    uint32_t c[9];
+    const int off = (int)(bstart & 15);
+    const int nch = (off + blen + 15) >> 4;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        uint4 v = *reinterpret_cast<const uint4*>(err + min(c0 + 16 * k, clast));
+        v.x = nzbytes(v.x);
+        v.y = nzbytes(v.y);
+        v.z = nzbytes(v.z);
+        v.w = nzbytes(v.w);
+        c[k] = k < nch ? fold16(v) : 0u;
+    }
+    const uint64_t a0 = (uint64_t)c[0] | ((uint64_t)c[1] << 16) | ((uint64_t)c[2] << 32) | ((uint64_t)c[3] << 48);
+    const uint64_t a1 = (uint64_t)c[4] | ((uint64_t)c[5] << 16) | ((uint64_t)c[6] << 32) | ((uint64_t)c[7] << 48);
+    const uint64_t a2 = c[8];
+    m0 = off ? (a0 >> off) | (a1 << (64 - off)) : a0;
+    m1 = off ? (a1 >> off) | (a2 << (64 - off)) : a1;
+    if (blen < 64) {
+        m0 &= (1ull << blen) - 1;
+        m1 = 0;
+    } else if (blen < 128) {
+        m1 &= (1ull << (blen - 64)) - 1;
+    }
+}
+
+
+// One exact row of a lane's detector whose p and s are already computed (det_add_fast's
+// tests): 2 = change, 1 = warning.
+__device__ __forceinline__ int lane_test(Det& d, double p, double s, int min_inst, double wl, double cl) {
+    d.p = p;
+    d.s = s;
+    d.n += 1;
+    d.warn = 0;
+    if (d.n < min_inst) return 0;
+    const double ps = p + s;
+    if (ps <= d.psmin) {
+        d.pmin = p;
+        d.smin = s;
+        d.psmin = ps;
+    }
+    if (ps > d.pmin + cl * d.smin) return 2;
+    d.warn = ps > d.pmin + wl * d.smin ? 1 : 0;
+    return d.warn;
+}
+
+__device__ __forceinline__ void write_ev(int2* __restrict__ ev, const uint8_t* __restrict__ pmap, int64_t item,
+                                        int64_t brow, int w, int c) {
+    if (pmap) {
+        if (w >= 0) w = pmap[brow + w];
+        if (c >= 0) c = pmap[brow + c];
+    }
+    ev[item] = make_int2(w, c);
+}
+
+template <bool kPmap, int kLoads>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(DDM_OP_WAVES))) void k_scan_group(
+    const uint8_t* __restrict__ err, int64_t n_streams, int64_t L, int64_t nb, ddm_params P,
+    ddm_state* __restrict__ state, int2* __restrict__ ev, int64_t* __restrict__ nev_out,
+    const uint8_t* __restrict__ pmap, const uint16_t* __restrict__ ptab, const double4* __restrict__ pst, int use_pre,
+    uint32_t* __restrict__ cnt_out) {
+    __shared__ uint64_t img_all[kWaves][kLoads * 16 + 2];
+    __shared__ uint64_t s_msk[kWaves][kSlots][4];     // per slot: C (speculation changes), N, X (open), Z
+    __shared__ int64_t s_sid[kWaves][kSlots];
+    __shared__ int32_t s_jb[kWaves][kSlots];          // the slot's first job
+    __shared__ uint8_t s_fe[kWaves][kSlots][64];      // first error row of each batch
+    __shared__ uint64_t j_m0[kWaves][64], j_m1[kWaves][64];
+    __shared__ int32_t j_hdr[kWaves][64];             // batch | rows done by the prefix << 8 | (warning + 1) << 16
+    __shared__ double rcp[kBatchRcp];
+    for (int k = threadIdx.x; k < kBatchRcp; k += kThreads) rcp[k] = 1.0 / (double)(k > 0 ? k : 1);
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint64_t* const img = img_all[wv];
+    uint16_t* const img16 = reinterpret_cast<uint16_t*>(img);
+    const int pb = (int)P.per_batch;
+    const int min_inst = P.min_num_instances;
+    const double wl = P.warning_level, cl = P.out_control_level;
+    const bool shortcuts = min_inst == 3;
+    const int64_t wave = (int64_t)blockIdx.x * kWaves + wv;
+    const int64_t n_waves = (int64_t)gridDim.x * kWaves;
+    const int nbi = (int)nb;                          // <= 64 here
+    const uint64_t below = (1ull << lane) - 1;
+
+    int64_t s = wave;
+    if (s >= n_streams) return;
+    ChunkGeo g = chunk_geo(s, 0, L, pb);
+    uint4 v[kLoads];
+    chunk_load<kLoads>(err, g, lane, v);
+
+    // the classified stream not yet in a group (per lane: batch `lane`)
+    bool pending = false;
+    int64_t psid = 0;
+    uint64_t pm0 = 0, pm1 = 0, pC = 0, pN = 0, pX = 0, pZ = 0;
+    int pfe = 128, prw = -1, prc = -1, phdr = 0;
+
+    for (;;) {
+        // ---- 1. a group: classify streams until kSlots or 64 open batches
+        int nslots = 0, njobs = 0;
+        for (;;) {
+            if (!pending) {
+                if (s >= n_streams) break;
+                uint32_t odd = 0;
+#pragma unroll
+                for (int k = 0; k < kLoads; ++k) odd |= v[k].x | v[k].y | v[k].z | v[k].w;
+                if (__ballot((odd & 0xfefefefeu) != 0u)) {
+#pragma unroll
+                    for (int k = 0; k < kLoads; ++k) {
+                        v[k].x = nzbytes(v[k].x);
+                        v[k].y = nzbytes(v[k].y);
+                        v[k].z = nzbytes(v[k].z);
+                        v[k].w = nzbytes(v[k].w);
+                    }
+                }
+                wave_sync_lds();
+#pragma unroll
+                for (int k = 0; k < kLoads; ++k) img16[k * 64 + lane] = (uint16_t)fold16(v[k]);
+                wave_sync_lds();
+                const ChunkGeo cg = g;
+                const int64_t ns = s + n_waves;
+                g = chunk_geo(ns < n_streams ? ns : s, 0, L, pb);
+                chunk_load<kLoads>(err, g, lane, v);
+                // lane b: batch b's bits and its speculation from a fresh detector
+                const bool valid = lane < nbi;
+                const int bl = valid ? lane : 0;
+                const int blen = min(pb, cg.rows - bl * pb);
+                const int o = cg.off + bl * pb;
+                const int wo = o >> 6, sh = o & 63;
+                const uint64_t x0 = img[wo], x1 = img[wo + 1], x2 = img[wo + 2];
+                uint64_t m0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
+                uint64_t m1 = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
+                if (blen < 64) {
+                    m0 &= (1ull << blen) - 1;
+                    m1 = 0;
+                } else if (blen < 128) {
+                    m1 &= (1ull << (blen - 64)) - 1;
+                }
+                const bool triv = shortcuts && blen >= 2 && (m0 & 3ull) == 0;
+                const int t2 = mask_next(m0, m1, 2);
+                const uint32_t inf = ptab[(uint32_t)(m0 & (uint64_t)(kPreN - 1))];
+                const bool pre_ok = !triv && use_pre && blen >= kPre;
+                const bool pre = pre_ok && (inf >> 5) != 0u;
+                int rw = -1, rc = -1;
+                bool dec = false;
+                if (triv && t2 < blen) {
+                    rc = t2;
+                    dec = true;
+                } else if (pre) {
+                    rc = (int)(inf >> 5) - 1;
+                    rw = (int)(inf & 31u) - 1;
+                    dec = true;
+                }
+                const bool open = valid && !dec && !(triv && t2 >= blen);
+                pC = __ballot(valid && dec);
+                pN = __ballot(valid && triv && t2 >= blen);
+                pX = __ballot(open);
+                pZ = __ballot(valid && (m0 | m1) == 0ull);
+                pm0 = m0;
+                pm1 = m1;
+                pfe = mask_next(m0, m1, 0);
+                prw = rw;
+                prc = rc;
+                // an open batch longer than the prefix starts after it (no change there)
+                const bool from_pre = pre_ok && blen > kPre;
+                phdr = lane | ((from_pre ? kPre : 0) << 8) | ((from_pre ? (int)(inf & 31u) : 0) << 16);
+                psid = s;
+                s = ns;
+                pending = true;
+            }
+            const int xc = __popcll(pX);
+            if (nslots == kSlots || njobs + xc > 64) break;
+            // commit the pending stream into slot nslots
+            if (lane == 0) {
+                s_msk[wv][nslots][0] = pC;
+                s_msk[wv][nslots][1] = pN;
+                s_msk[wv][nslots][2] = pX;
+                s_msk[wv][nslots][3] = pZ;
+                s_sid[wv][nslots] = psid;
+                s_jb[wv][nslots] = njobs;
+            }
+            s_fe[wv][nslots][lane] = (uint8_t)pfe;
+            if ((pX >> lane) & 1ull) {
+                const int jx = njobs + __popcll(pX & below);
+                j_m0[wv][jx] = pm0;
+                j_m1[wv][jx] = pm1;
+                j_hdr[wv][jx] = phdr | (nslots << 24);
+            }
+            if (lane < nbi) write_ev(ev, kPmap ? pmap : nullptr, psid * nb + lane, psid * L + (int64_t)lane * pb, prw, prc);
+            njobs += xc;
+            ++nslots;
+            pending = false;
+        }
+        if (nslots == 0) break;
+        wave_sync_lds();
+
+        // ---- 2. the open batches, one per lane, exact rows from a fresh detector (or the
+        // detector after the prefix rows)
+        Det d;
+        det_reset(d);
+        int jw = -1, jc = -1;
+        bool busy = lane < njobs;
+        uint64_t m0 = 0, m1 = 0;
+        int i = 0, blen = 0;
+        if (busy) {
+            m0 = j_m0[wv][lane];
+            m1 = j_m1[wv][lane];
+            const int hdr = j_hdr[wv][lane];
+            const int b = hdr & 255, slot = (hdr >> 24) & 255;
+            blen = (int)min((int64_t)pb, L - (int64_t)b * pb);
+            i = (hdr >> 8) & 255;
+            jw = ((hdr >> 16) & 255) - 1;
+            (void)slot;
+            if (i) {
+                const double4 t = pst[(uint32_t)(m0 & (uint64_t)(kPreN - 1))];
+                d.p = t.x;
+                d.pmin = t.y;
+                d.smin = t.z;
+                d.psmin = t.w;
+                d.n = i + 1;
+            }
+        }
+        // the batch's bits from row i on, consumed two at a time
+        uint64_t q0 = i == 0 ? m0 : (m0 >> i) | (m1 << (64 - i)), q1 = i == 0 ? m1 : m1 >> i;   // i in {0, 16}
+#ifdef DDM_OP_NOSTEP      // timing variant: results are NOT the scan's
+        busy = false;
+#endif
+        while (__ballot(busy)) {
+            if (busy) {
+                const bool two = i + 1 < blen;
+                const int n0 = (int)d.n;
+                const double nd0 = (double)n0, r0 = rcp[n0], nd1 = (double)(n0 + 1), r1 = rcp[n0 + 1];
+                const double x0 = (double)(int)(q0 & 1ull), x1 = two ? (double)(int)((q0 >> 1) & 1ull) : 0.0;
+                q0 = (q0 >> 2) | (q1 << 62);
+                q1 >>= 2;
+                const double p0 = d.p + div_rn(x0 - d.p, nd0, r0);
+                const double p1 = p0 + div_rn(x1 - p0, nd1, r1);
+                const double s0 = sqrt_q(div_rn(p0 * (1.0 - p0), nd0, r0));
+                const double s1 = sqrt_q(div_rn(p1 * (1.0 - p1), nd1, r1));
+                int r = lane_test(d, p0, s0, min_inst, wl, cl);
+                if (r == 1 && jw < 0) jw = i;
+                ++i;
+                if (r != 2 && two) {
+                    r = lane_test(d, p1, s1, min_inst, wl, cl);
+                    if (r == 1 && jw < 0) jw = i;
+                    ++i;
+                }
+                if (r == 2) {
+                    jc = i - 1;
+                    busy = false;
+                } else if (i >= blen) {
+                    busy = false;
+                }
+            }
+        }
+
+        // ---- 3. the walks
+#ifdef DDM_OP_NOWALK      // timing variant: results are NOT the scan's
+        nslots = 0;
+#endif
+        for (int k = 0; k < nslots; ++k) {
+            // wave-uniform values into scalar registers: the walk is scalar code
+            const uint64_t C = uni64(s_msk[wv][k][0]), N = uni64(s_msk[wv][k][1]), X = uni64(s_msk[wv][k][2]),
+                           Z = uni64(s_msk[wv][k][3]);
+            const int64_t sid = (int64_t)uni64((uint64_t)s_sid[wv][k]);
+            const int jb = __builtin_amdgcn_readfirstlane(s_jb[wv][k]);
+            const int64_t srow = sid * L;
+            const ddm_state st = state[sid];
+            Det c;
+            c.p = st.miss_prob;
+            c.s = st.miss_std;
+            c.pmin = st.miss_prob_min;
+            c.smin = st.miss_sd_min;
+            c.psmin = st.miss_prob_sd_min;
+            c.n = st.sample_count;
+            c.chg = st.in_concept_change;
+            c.warn = st.in_warning_zone;
+            int kind = kCarr;
+            if (det_fresh(c)) kind = kFresh;
+            else if (shortcuts && det_trivial(c)) kind = kTriv;
+            uint64_t E = C;                              // batches with an event
+            int j = 0;
+            while (j < nbi) {
+                const int bj_len = (int)min((int64_t)pb, L - (int64_t)j * pb);
+                const int64_t brow = srow + (int64_t)j * pb;
+                if (kind == kFresh) {
+                    const uint64_t R = C >> j;
+                    const int run = min(nbi - j, R == ~0ull ? 64 : __builtin_ctzll(~R));
+                    if (run > 0) {
+                        j += run;
+                        continue;
+                    }
+                    if ((N >> j) & 1ull) {
+                        det_reset(c);
+                        c.p = c.s = c.pmin = c.smin = c.psmin = 0.0;
+                        c.n = 1 + bj_len;
+                        kind = kTriv;
+                        ++j;
+                        continue;
+                    }
+                    // open: the lane that ran it holds the result and the detector after it
+                    const int jl = jb + __popcll(X & ((1ull << j) - 1));
+                    const int w = __builtin_amdgcn_readlane(jw, jl), cp = __builtin_amdgcn_readlane(jc, jl);
+                    if (lane == 0) write_ev(ev, kPmap ? pmap : nullptr, sid * nb + j, brow, w, cp);
+                    if (w >= 0 || cp >= 0) E |= 1ull << j;
+                    if (cp < 0) {
+                        c.p = readlane_d(d.p, jl);
+                        c.s = readlane_d(d.s, jl);
+                        c.pmin = readlane_d(d.pmin, jl);
+                        c.smin = readlane_d(d.smin, jl);
+                        c.psmin = readlane_d(d.psmin, jl);
+                        c.n = __builtin_amdgcn_readlane((int)d.n, jl);
+                        c.warn = __builtin_amdgcn_readlane(d.warn, jl);
+                        c.chg = 0;
+                        kind = kCarr;
+                    }
+                    ++j;
+                    continue;
+                }
+                if (kind == kTriv) {
+                    const uint64_t R = Z >> j;
+                    const int run = min(nbi - j, R == ~0ull ? 64 : __builtin_ctzll(~R));
+                    if (run > 0) {
+                        // no error: n moves (the stream's last batch may be short); no event
+                        for (int u = 0; u < run; ++u) c.n += min((int64_t)pb, L - (int64_t)(j + u) * pb);
+                        const uint64_t rm = run >= 64 ? ~0ull : ((1ull << run) - 1);
+                        E &= ~(rm << j);                // (their rows were written as no event)
+                        j += run;
+                        continue;
+                    }
+                    const int e = __builtin_amdgcn_readfirstlane((int)s_fe[wv][k][j]);   // the change: the first error row
+                    if (lane == 0) write_ev(ev, kPmap ? pmap : nullptr, sid * nb + j, brow, -1, e);
+                    E |= 1ull << j;
+                    kind = kFresh;
+                    ++j;
+                    continue;
+                }
+                // kCarr: batch j wave-wide from the exact detector
+                uint64_t a0, a1;
+                if ((X >> j) & 1ull) {
+                    const int jl = jb + __popcll(X & ((1ull << j) - 1));
+                    a0 = j_m0[wv][jl];
+                    a1 = j_m1[wv][jl];
+                } else {
+                    uint64_t b0_, b1_;
+                    batch_mask(err, brow, bj_len, b0_, b1_);
+                    a0 = readlane64(b0_, 0);
+                    a1 = readlane64(b1_, 0);
+                }
+                int w = -1, cp = -1;
+                for (int ci = 0; ci < bj_len; ci += 64) {
+                    const int cnt = min(64, bj_len - ci);
+                    const TileOut to = xtile(c, ci == 0 ? a0 : a1, cnt, min_inst, wl, cl);
+                    const uint64_t upto = to.last >= 63 ? ~0ull : ((1ull << (to.last + 1)) - 1);
+                    const uint64_t wb = to.warn & upto;
+                    if (w < 0 && wb) w = ci + __builtin_ctzll(wb);
+                    if (to.kc >= 0) {
+                        cp = ci + to.kc;
+                        break;
+                    }
+                }
+                if (lane == 0) write_ev(ev, kPmap ? pmap : nullptr, sid * nb + j, brow, w, cp);
+                if (w >= 0 || cp >= 0) E |= 1ull << j;
+                else E &= ~(1ull << j);
+                if (cp >= 0) kind = kFresh;
+                ++j;
+            }
+            if (kind == kFresh) det_reset(c);
+            if (lane == 0) {
+                ddm_state o;
+                o.miss_prob = c.p;
+                o.miss_std = c.s;
+                o.miss_prob_min = c.pmin;
+                o.miss_sd_min = c.smin;
+                o.miss_prob_sd_min = c.psmin;
+                o.sample_count = c.n;
+                o.in_concept_change = 0;
+                o.in_warning_zone = kind == kCarr ? c.warn : 0;
+                state[sid] = o;
+                if (nev_out) nev_out[sid] = __popcll(E);
+            }
+        }
+        (void)cnt_out;
+    }
+}
+
 int64_t onepass_waves() {
     static const int64_t w = [] {
         int dev = 0, cus = 256, per_cu = 4;
@@ -674,7 +1095,7 @@ int64_t onepass_waves() {
 
 extern "C" int64_t ddm_scan_batches_scratch_bytes(int64_t n_streams, int64_t stream_len, int32_t per_batch) {
     if (n_streams < 0 || stream_len < 0 || per_batch <= 0) return -1;
-    return 256 + 2 * (int64_t)kPreN;
+    return 256 + 2 * (int64_t)kPreN + 32 * (int64_t)kPreN;
 }
 
 extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t stream_len, const ddm_params* prm,
@@ -695,8 +1116,9 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
         uint8_t* b = static_cast<uint8_t*>(scratch);
         uint32_t* cnt = reinterpret_cast<uint32_t*>(b);
         uint16_t* ptab = reinterpret_cast<uint16_t*>(b + 256);
+        double4* pst = reinterpret_cast<double4*>(b + 256 + 2 * (int64_t)kPreN);
         if (int rc = ddm::hip_status(hipMemsetAsync(cnt, 0, 4 * kWalkCount, s), "ddm_scan_batches: memset")) return rc;
-        hipLaunchKernelGGL(k_prefix_table, dim3(kPreN / 256), dim3(256), 0, s, *prm, ptab);
+        hipLaunchKernelGGL(k_prefix_table, dim3(kPreN / 256), dim3(256), 0, s, *prm, ptab, pst);
         if (int rc = ddm::launch_status("ddm_scan_batches/prefix")) return rc;
         // 16-byte pieces of a chunk: (64 * pb + 15) / 16 + 1, per 64 lanes
         const int64_t rows = std::min<int64_t>(stream_len, (int64_t)kChunkBatches * prm->per_batch);
@@ -709,8 +1131,19 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
         const int64_t waves = std::min<int64_t>(onepass_waves(), n_streams);
         const int64_t blocks = ddm::ceil_div(waves, kWaves);
         const bool use_pre = prm->per_batch >= kPre;
-        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kThreads), 0, s, err, n_streams, stream_len, nb, *prm,
-                           state_io, reinterpret_cast<int2*>(ev_out), nev_out, perm_map, ptab, (int)use_pre, cnt);
+        if (nb <= kChunkBatches) {
+            const auto gk = loads <= 3 ? (pm ? k_scan_group<true, 3> : k_scan_group<false, 3>)
+                          : loads <= 5 ? (pm ? k_scan_group<true, 5> : k_scan_group<false, 5>)
+                          : loads <= 7 ? (pm ? k_scan_group<true, 7> : k_scan_group<false, 7>)
+                                       : (pm ? k_scan_group<true, 9> : k_scan_group<false, 9>);
+            hipLaunchKernelGGL(gk, dim3((unsigned)blocks), dim3(kThreads), 0, s, err, n_streams, stream_len, nb, *prm,
+                               state_io, reinterpret_cast<int2*>(ev_out), nev_out, perm_map, ptab, pst, (int)use_pre,
+                               cnt);
+        } else {
+            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kThreads), 0, s, err, n_streams, stream_len, nb,
+                               *prm, state_io, reinterpret_cast<int2*>(ev_out), nev_out, perm_map, ptab, (int)use_pre,
+                               cnt);
+        }
         if (int rc = ddm::launch_status("ddm_scan_batches/onepass")) return rc;
     }
     if (ev_end)

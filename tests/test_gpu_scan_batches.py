@@ -1,6 +1,7 @@
-"""ddm_scan_batches (batch-parallel mode-1 scan for equal-length streams, configs[3]) vs
-ddm_scan_streams in mode 1 and the C oracle: events, event counts and the carried state,
-bit for bit."""
+"""ddm_scan_batches (mode-1 scan for equal-length streams, configs[3]: the grouped kernel
+for streams of <= 64 batches, the chunked one-pass kernel with certified rows for longer
+ones) vs ddm_scan_streams in mode 1 and the C oracle: events, event counts and the carried
+state, bit for bit."""
 import numpy as np
 import pytest
 import torch
@@ -60,7 +61,7 @@ def mixed_streams(rs, n, L):
 
 @pytest.mark.parametrize("per_batch,L", [(100, 4096), (100, 1000), (1, 37), (3, 301), (64, 640), (127, 1000),
                                          (128, 1031), (100, 1), (100, 100), (100, 199), (15, 300), (16, 400),
-                                         (16, 1000), (17, 340)])
+                                         (16, 1000), (17, 340), (50, 10000), (1, 100)])
 @pytest.mark.parametrize("min_inst", [3, 5])
 def test_scan_batches_equals_scan_streams(oracle_lib, per_batch, L, min_inst):
     rs = np.random.RandomState(per_batch * 7919 + L + min_inst)

@@ -2,12 +2,14 @@
 round-2 kernels on the same device-generated streams, events compared, and the one-pass
 kernel's path counters (scratch words: replay anomalies, certified batches, uncertified
 batches, end-state replays)."""
+import os
 import sys
-import time
 
 import numpy as np
 import torch
 
+if len(sys.argv) > 2:                       # a variant library (tools/build_variant.sh)
+    os.environ["DDM_AMD_LIB"] = os.path.abspath(sys.argv[2])
 sys.path.insert(0, "distributed-drift-detection_amd")
 from ddm_amd import kernels  # noqa: E402
 
@@ -20,7 +22,7 @@ nb = (L + 99) // 100
 prm = kernels.params_struct()
 st0 = torch.from_numpy(kernels.fresh_states(S).view(np.uint8)).to(dev)
 out = {}
-for v1 in (False, True):
+for v1 in ((False, True) if len(sys.argv) <= 3 else (False,)):
     ev = torch.empty((S * nb, 2), dtype=torch.int32, device=dev)
     st = st0.clone()
     sc = torch.zeros(kernels.scan_batches_scratch_size(S, L, v1=v1), dtype=torch.uint8, device=dev)
@@ -36,4 +38,6 @@ for v1 in (False, True):
     out[v1] = (ev.cpu().numpy(), st.cpu().numpy())
     cnt = sc[:16].cpu().numpy().view(np.uint32) if not v1 else None
     print(f"{'v1' if v1 else 'onepass'}: ms per call {['%.3f' % t for t in times]}; counters {cnt}")
-print("events equal:", np.array_equal(out[False][0], out[True][0]), "states equal:", np.array_equal(out[False][1], out[True][1]))
+if len(out) > 1:
+    print("events equal:", np.array_equal(out[False][0], out[True][0]),
+          "states equal:", np.array_equal(out[False][1], out[True][1]))
