@@ -101,8 +101,6 @@ def parse():
                     help="rows of partition 0 re-run by the oracle after the timed region (0: off)")
     ap.add_argument("--c4-streams", type=int, default=1_000_000)
     ap.add_argument("--c4-len", type=int, default=4096)
-    ap.add_argument("--c4-impl", default="onepass", choices=["onepass", "v1"],
-                    help="ddm_scan_batches (one pass) or the round-2 kernels (ddm_scan_batches_v1), for A/B")
     ap.add_argument("--c5-rows", type=int, default=64_000_000, help="c5 rows (all partitions)")
     ap.add_argument("--c5-flip", type=float, default=0.0, help="c5 label-noise rate")
     ap.add_argument("--solo-world", type=int, default=0,
@@ -624,8 +622,7 @@ def run_c4(args, world, rank, dev, torch, dist, cpu):
     kernels.synth_bernoulli_streams(err, S, L, args.seed + rank)
     nb = (L + 99) // 100
     ev = torch.empty((S * nb, 2), dtype=torch.int32, device=dev)
-    v1 = args.c4_impl == "v1"
-    flags = torch.empty(kernels.scan_batches_scratch_size(S, L, v1=v1), dtype=torch.uint8, device=dev)
+    flags = torch.empty(kernels.scan_batches_scratch_size(S, L), dtype=torch.uint8, device=dev)
     state0 = torch.from_numpy(kernels.fresh_states(S).view(np.uint8)).to(dev)
     state = torch.empty_like(state0)
     prm = kernels.params_struct()
@@ -636,7 +633,7 @@ def run_c4(args, world, rank, dev, torch, dist, cpu):
         state.copy_(state0)
         if timed:
             e0.record(stream)
-        kernels.scan_batches(err, S, L, prm, state, ev, flags, stream=stream, v1=v1)
+        kernels.scan_batches(err, S, L, prm, state, ev, flags, stream=stream)
         if timed:
             e1.record(stream)
 
@@ -689,18 +686,16 @@ def run_c4(args, world, rank, dev, torch, dist, cpu):
              "rows_note": "value counts every row of every stream (nominal); rows_scanned counts the rows the DDM "
                           "consumes (each batch up to its change), the same way on the CPU side"}
     roofline = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_from_profile("ddm_scan_batches_v1" if v1 else "ddm_scan_batches", S * L),
+                "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_from_profile("ddm_scan_batches", S * L),
                 "kernel": "ddm_scan_batches", "alg_bytes_per_row": "1 + 8/100",
                 "avg_launch_ms": avg_ms,
                 "fp64_valu_roof": {"rows_per_s_at_roof": PEAK_FP64_VALU_TFLOPS * 1e12 / 2 / 45,
                                    "achieved_rows_per_s": rows_s,
                                    "note": "straightforward form ~45 fp64 VALU instructions per scanned row "
                                            "(SURVEY §8d); the batch-parallel form skips most rows"},
-                "note": ("one ddm_scan_batches call: k_prefix_table + k_scan_onepass (a wave per stream, "
-                         "certified rows); HIP events around the call" if not v1 else
-                         "one ddm_scan_batches_v1 call: k_scan_prefix_table + k_scan_batches_classify + "
-                         "k_scan_batches_exact<0> + k_scan_batches_exact<1> + k_scan_batches_walk + "
-                         "k_scan_batches_chain; HIP events around the call")}
+                "note": "one ddm_scan_batches call: k_scan_prefix_table + k_scan_batches_classify + "
+                        "k_scan_batches_exact<0> + k_scan_batches_exact<1> + k_scan_batches_walk + "
+                        "k_scan_batches_chain; HIP events around the call"}
     return rows, elapsed, info, extra, roofline, cpu_res, "weak"
 
 

@@ -1191,12 +1191,12 @@ int64_t classify_waves() {
 
 }  // namespace
 
-extern "C" int64_t ddm_scan_batches_v1_scratch_bytes(int64_t n_streams, int64_t stream_len, int32_t per_batch) {
+extern "C" int64_t ddm_scan_batches_scratch_bytes(int64_t n_streams, int64_t stream_len, int32_t per_batch) {
     if (n_streams < 0 || stream_len < 0 || per_batch <= 0) return -1;
     return batch_scratch(nullptr, n_streams, ddm::ceil_div(stream_len, per_batch)).bytes;
 }
 
-extern "C" int ddm_scan_batches_v1(const uint8_t* err, int64_t n_streams, int64_t stream_len, const ddm_params* prm,
+extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t stream_len, const ddm_params* prm,
                                 ddm_state* state_io, int32_t* ev_out, int64_t* nev_out, void* scratch,
                                 const uint8_t* perm_map, ddm_stream_t stream, ddm_event_t ev_begin,
                                 ddm_event_t ev_end) {

@@ -90,9 +90,6 @@ SIGNATURES = {
     "ddm_scan_batches": (ctypes.c_int, [_vp, _i64, _i64, ctypes.POINTER(DdmParams), _vp, _vp, _vp, _vp, _vp, _vp,
                                         _vp, _vp]),
     "ddm_scan_batches_scratch_bytes": (_i64, [_i64, _i64, _i32]),
-    "ddm_scan_batches_v1": (ctypes.c_int, [_vp, _i64, _i64, ctypes.POINTER(DdmParams), _vp, _vp, _vp, _vp, _vp, _vp,
-                                           _vp, _vp]),
-    "ddm_scan_batches_v1_scratch_bytes": (_i64, [_i64, _i64, _i32]),
     "ddm_scan_long": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, ctypes.POINTER(DdmParams), _vp, _vp, _vp, _vp, _vp,
                                      _i32, _vp, _vp, _vp, _vp, _vp]),
     "ddm_scan_long_scratch_bytes": (_i64, [_i64, _i64, _i32]),

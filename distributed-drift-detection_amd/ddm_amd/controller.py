@@ -900,7 +900,7 @@ class BatchRunner:
         E.stage_jobs, E.dfit_jobs = self.stage_jobs.d.data_ptr(), self.dfit_jobs.d.data_ptr()
         E.max_trees = self.s.n_estimators
         E.next_jobs = self.njobs.d.data_ptr()
-        self.side_stream = torch.cuda.Stream(self.device, priority=0)    # below the refits (epoch stream)
+        self.side_stream = torch.cuda.Stream(self.device, priority=-1)   # the next windows' shuffles: as long as the refits
         E.side_stream = self.side_stream.cuda_stream
         self._fork_ev, self._join_ev = ctypes.c_void_p(), ctypes.c_void_p()
         check(lib.ddm_event_create(ctypes.byref(self._fork_ev)), "ddm_event_create")
@@ -911,7 +911,7 @@ class BatchRunner:
             self._mid_ev = ctypes.c_void_p()
             check(lib.ddm_event_create(ctypes.byref(self._mid_ev)), "ddm_event_create")
             E.mid_ev = self._mid_ev.value
-            E.dfit_max_lf = self.s.per_batch * max(p.X.shape[0] for p in self.parts)
+            E.dfit_max_lf = dfit.max_lf(self.s.per_batch, max(p.X.shape[0] for p in self.parts))
             E.tail_off = self.stage_off["dfit"]
             E.tail_bytes = self.stage_stride["dfit"] * len(self.parts)
         if self.timing:

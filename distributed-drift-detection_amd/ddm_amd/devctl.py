@@ -105,7 +105,7 @@ class DeviceController:
         E.dfit_jobs, E.n_dfit, E.max_trees = r.dfit_jobs.d.data_ptr(), self.n, r.s.n_estimators
         mw = max(r.max_wins)
         E.max_W = mw
-        E.dfit_max_lf = r.s.per_batch * max(p.X.shape[0] for p in r.parts)
+        E.dfit_max_lf = dfit.max_lf(r.s.per_batch, max(p.X.shape[0] for p in r.parts))
         E.max_pieces = 2 + 64 + r.shuffles[0].window_draws(mw) // 8192
         self._E = E
         return E
@@ -225,8 +225,10 @@ class DeviceController:
         stream.synchronize()
         r._pending_sync = False
         r._pending_forests = []
-        while r._gen_rest is not None:       # the whole expected stream, on the side streams
-            r._enqueue_rest()
+        # the rest of the streams in growing pieces, two more at every poll (all of it up
+        # front kept the side streams busy past the last epoch: the run waited ~14 ms for
+        # generation no epoch needed, C3)
+        r._enqueue_rest()
         self._write_records(live)
         with torch.cuda.stream(stream):
             self.pstall.zero_()
@@ -236,6 +238,7 @@ class DeviceController:
         self._publish_avail()
         E = self._epoch_struct()
         check(lib.ddm_ctl_enter(ctypes.byref(E)), "ddm_ctl_enter")
+        r._mark("device phase entered")
         timing = r.t_pred is not None
         logging = r.predict_log is not None
         pending, slot, epochs = None, 0, 0
@@ -256,14 +259,19 @@ class DeviceController:
                 rec = self.poll_h[pslot].numpy().view(CTL)
                 active = (rec["done"] == 0) & (rec["stall"] == 0) & (rec["park"] == 0)
                 if not active.any() or (rec["stall"] != 0).any():
+                    r._mark(f"poll: {int(active.sum())} active, {int((rec['stall'] != 0).sum())} stalled")
                     break
                 if not self._extend(rec):
+                    r._mark("poll: stream buffers would overflow")
                     break
+                r._enqueue_rest()
                 self._publish_avail()
             pending = (ev, slot)
             slot ^= 1
+        r._mark(f"device loop done ({epochs} epochs enqueued)")
         stream.synchronize()
         r.side_stream.synchronize()
+        r._mark("device epochs drained")
         st.gpu_s += time.perf_counter() - t0
         if timing:
             p_ms, s_ms, f_ms, sh_ms = self.kernel_times()
@@ -271,7 +279,9 @@ class DeviceController:
             st.scan_ms += s_ms
             st.dfit_ms += f_ms
             st.shuffle_ms += sh_ms
-        return self._take_back(live)
+        out = self._take_back(live)
+        r._mark("records taken back")
+        return out
 
     def _one_epoch_instrumented(self, E, timing, logging):
         r = self.r

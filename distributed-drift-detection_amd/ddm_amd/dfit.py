@@ -105,6 +105,18 @@ class DeviceFitForest:
         return int(self.res[CF_SLOTS]) if self.compiled else self.bufs.F
 
 
+# Small batches can be gated, checked and presorted inside the tree kernel (every workgroup
+# again) instead of by k_dfit_prep.  Measured on MI355X (tools/bench_refit.py, 8 refits of
+# 100 x 27 batches): separable batches (C3's refits) 87 us with the prep kernel, 123 us
+# fused; noisy batches 1.61 ms either way.  So the prep kernel stays.
+FUSED_PREP = False
+
+
+def max_lf(per_batch, n_features):
+    """ddm_rf_fit_device_lf's max_lf for the controller's refits."""
+    return int(per_batch) * int(n_features) if FUSED_PREP else -1
+
+
 def fit_device(table_d, n_jobs, max_trees, stream, max_lf=-1):
     """ddm_rf_fit_device over a device table of DFIT_DTYPE records (max_lf >= every job's
     L*F: small batches are prepared inside the tree kernel)."""

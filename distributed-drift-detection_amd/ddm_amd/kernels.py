@@ -218,26 +218,24 @@ def scan_streams(err, offsets, params, state, batch_base, n_batches_total, ev, f
                                _stream(err, stream), *_evs(timer)), "ddm_scan_streams")
 
 
-def scan_batches_scratch_size(n_streams, stream_len, per_batch=100, v1=False):
-    """Bytes of device scratch ddm_scan_batches (v1: the round-2 form) needs."""
-    f = lib.ddm_scan_batches_v1_scratch_bytes if v1 else lib.ddm_scan_batches_scratch_bytes
-    return int(f(int(n_streams), int(stream_len), int(per_batch)))
+def scan_batches_scratch_size(n_streams, stream_len, per_batch=100):
+    """Bytes of device scratch ddm_scan_batches needs."""
+    return int(lib.ddm_scan_batches_scratch_bytes(int(n_streams), int(stream_len), int(per_batch)))
 
 
 def scan_batches(err, n_streams, stream_len, params, state, ev, scratch, nev=None, perm_map=None, stream=None,
-                 timer=None, v1=False):
-    """Mode-1 DDM over n_streams back-to-back streams of stream_len rows (one pass, a wave
-    per stream; v1: the round-2 batch-parallel kernels).  ev int32 [n_streams*nb, 2];
-    scratch uint8 [scan_batches_scratch_size(...)]; state n_streams ddm_state records
-    (updated in place)."""
+                 timer=None):
+    """Mode-1 DDM over n_streams back-to-back streams of stream_len rows (batch-parallel kernels).
+    ev int32 [n_streams*nb, 2]; scratch uint8 [scan_batches_scratch_size(...)]; state n_streams
+    ddm_state records (updated in place)."""
     nb = -(-stream_len // params.per_batch)
     assert err.dtype == torch.uint8 and err.numel() >= ((n_streams * stream_len + 15) // 16) * 16
     assert ev.dtype == torch.int32 and ev.numel() >= 2 * n_streams * nb
-    assert scratch.numel() >= scan_batches_scratch_size(n_streams, stream_len, params.per_batch, v1)
+    assert scratch.numel() >= scan_batches_scratch_size(n_streams, stream_len, params.per_batch)
     assert state.numel() >= 56 * n_streams
-    f = lib.ddm_scan_batches_v1 if v1 else lib.ddm_scan_batches
-    check(f(err.data_ptr(), int(n_streams), int(stream_len), ctypes.byref(params), _ptr(state), _ptr(ev), _ptr(nev),
-            _ptr(scratch), _ptr(perm_map), _stream(err, stream), *_evs(timer)), "ddm_scan_batches")
+    check(lib.ddm_scan_batches(err.data_ptr(), int(n_streams), int(stream_len), ctypes.byref(params), _ptr(state),
+                               _ptr(ev), _ptr(nev), _ptr(scratch), _ptr(perm_map), _stream(err, stream),
+                               *_evs(timer)), "ddm_scan_batches")
 
 
 def scan_long_scratch_size(n_streams, max_rows, per_batch=100):

@@ -252,13 +252,6 @@ int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t stream_len, 
                      ddm_state* state_io, int32_t* ev_out, int64_t* nev_out, void* scratch,
                      const uint8_t* perm_map, ddm_stream_t stream, ddm_event_t ev_begin,
                      ddm_event_t ev_end);
-/* The round-2 form of ddm_scan_batches (speculative classify pass + exact / walk / chain
- * kernels), kept for A/B measurement; same arguments, its own scratch size. */
-int64_t ddm_scan_batches_v1_scratch_bytes(int64_t n_streams, int64_t stream_len, int32_t per_batch);
-int ddm_scan_batches_v1(const uint8_t* err, int64_t n_streams, int64_t stream_len, const ddm_params* prm,
-                        ddm_state* state_io, int32_t* ev_out, int64_t* nev_out, void* scratch,
-                        const uint8_t* perm_map, ddm_stream_t stream, ddm_event_t ev_begin,
-                        ddm_event_t ev_end);
 
 /* ddm_scan_streams (mode, state, stop, perm_map and first_nz as there) with the events
  * appended to per-stream logs instead of dense rows: for every batch b of stream s with an

@@ -1,7 +1,6 @@
-"""ddm_scan_batches (mode-1 scan for equal-length streams, configs[3]: the grouped kernel
-for streams of <= 64 batches, the chunked one-pass kernel with certified rows for longer
-ones) vs ddm_scan_streams in mode 1 and the C oracle: events, event counts and the carried
-state, bit for bit."""
+"""ddm_scan_batches (batch-parallel mode-1 scan for equal-length streams, configs[3]) vs
+ddm_scan_streams in mode 1 and the C oracle: events, event counts and the carried state,
+bit for bit."""
 import numpy as np
 import pytest
 import torch

@@ -48,16 +48,17 @@ def main():
             recs.append(b.record(xd.data_ptr(), yd.data_ptr(), sd.data_ptr(), res[k].data_ptr()))
         table = torch.from_numpy(np.array(recs, dtype=DFIT_DTYPE).view(np.uint8)).to(dev)
         torch.cuda.synchronize()
-        fit_device(table, 8, 100, stream)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(10):
-            fit_device(table, 8, 100, stream)
-        e1.record()
-        torch.cuda.synchronize()
-        print(f"{kind:10s} host fit_many {host_ms:.3f} ms   device {e0.elapsed_time(e1) / 10:.3f} ms   "
-              f"status {res[:, 0].tolist()} blob {res[:, 5].tolist()}", flush=True)
+        for max_lf, label in ((-1, "prep+trees+pack"), (100 * 27, "fused prep")):
+            fit_device(table, 8, 100, stream, max_lf)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                fit_device(table, 8, 100, stream, max_lf)
+            e1.record()
+            torch.cuda.synchronize()
+            print(f"{kind:10s} host fit_many {host_ms:.3f} ms   device ({label}) {e0.elapsed_time(e1) / 10:.3f} ms   "
+                  f"status {res[:, 0].tolist()} blob {res[:, 5].tolist()}", flush=True)
 
 
 if __name__ == "__main__":
