@@ -684,14 +684,20 @@ __device__ void fsm_replay(const uint32_t* __restrict__ R, const uint32_t* __res
                 s = e & 0xffu;
                 b += e >> 8;
             }
+#ifndef DDM_SHUF_NOREPLAY     // timing variant (tools/build_variant.sh): results are NOT the shuffle's
             replay_range(R, c.pos + (int64_t)t * kSub, min(stop, c.pos + (int64_t)(t + 1) * kSub), s, b, W, L, k);
+#endif
         }
         if (!kFused) continue;
         const int nloc = (int)(b_hi - b_lo);
         uint8_t* Pl = rlds + (size_t)cap * L;
         __syncthreads();
         // Fisher-Yates of every own batch: lane k applies batch k's swaps i = L-1 .. 1
+#ifdef DDM_SHUF_NOFY          // timing variant: results are NOT the shuffle's
+        for (int q = lane; q < 0; q += 64) {
+#else
         for (int q = lane; q < nloc; q += 64) {
+#endif
             uint8_t* p = Pl + (size_t)q * L;
             const uint8_t* jr = rlds + (size_t)q * L;
             for (int e = 0; e < L; ++e) p[e] = (uint8_t)e;

@@ -52,6 +52,8 @@ class DeviceController:
         self.res_ptrs = torch.zeros(n, dtype=torch.int64, device=dev)
         self.pstall = torch.zeros(n, dtype=torch.int32, device=dev)
         self.logs = [torch.empty(3 * max(1, nb), dtype=torch.int32, device=dev) for nb in r.nbs]
+        self.log_off = np.concatenate([[0], np.cumsum([3 * max(1, nb) for nb in r.nbs])]).astype(np.int64)
+        self.logs_h = torch.empty(int(self.log_off[-1]), dtype=torch.int32, pin_memory=True)   # read-back of all
         self.log_ptrs = torch.tensor([lg.data_ptr() for lg in self.logs], dtype=torch.int64, device=dev)
         self.log_b0 = torch.zeros(n, dtype=torch.int64, device=dev)
         self.avail_h = torch.zeros(64 * n, dtype=torch.int64, pin_memory=True)   # H2D sources (a ring)
@@ -333,11 +335,21 @@ class DeviceController:
         r.stream.synchronize()
         rec = self.rec
         epochs = int(rec["epochs"].max()) if len(rec) else 0
+        # every partition's event log in one read-back
+        with torch.cuda.stream(r.stream):
+            for ps in live:
+                n_log = int(rec[ps.i]["n_log"])
+                if n_log:
+                    o = int(self.log_off[ps.i])
+                    self.logs_h[o:o + 3 * n_log].copy_(self.logs[ps.i][:3 * n_log], non_blocking=True)
+        r.stream.synchronize()
+        logs_np = self.logs_h.numpy()
         for ps in live:
             q = rec[ps.i]
             n_log = int(q["n_log"])
             if n_log:
-                lg = self.logs[ps.i][:3 * n_log].cpu().numpy().reshape(-1, 3).astype(np.int64)
+                o = int(self.log_off[ps.i])
+                lg = logs_np[o:o + 3 * n_log].reshape(-1, 3).astype(np.int64)
                 for col in range(2):
                     hit = lg[:, 1 + col] >= 0
                     b = lg[hit, 0]
