@@ -1,0 +1,793 @@
+// Certified long carried DDM segments: run_DDM (DDM_Process.py:135-159) over streams whose
+// detector carries across very many rows (:144-152, :202), evaluated row-parallel.
+//
+// The reference's p is a rounded running mean, p += (x - p) / n, so the exact value of row
+// i needs every row before it (ddm_scan_long runs that chain: ~50 ns per row).  But the
+// DECISIONS only need p to the precision that separates them.  In exact arithmetic the
+// recurrence is the running mean: from a detector holding p0 over c0 samples, row i (the
+// c_i = c0 + i'th sample, K_i errors in the window so far) has
+//     pa_i = (c0 * p0 + K_i) / c_i.
+// Each reference step adds a rounding error rho_k (|rho_k| <= u (p_k + 2 / c_k), u = 2^-53:
+// the subtraction, the division and the addition), and the step contracts older errors by
+// (c_k - 1) / c_k, so c_i e_i = c_m e_m + sum_{m<k<=i} c_k rho_k for the error e = p_ref - pa.
+// Hence (the sums are closed forms of prefix counts, computed exactly in integers):
+//   * |e_i| <= B_i = (c0 B0 + u S_i) / c_i,   S_i = sum_{k<=i} (c0 p0 + K_k + 2 + c_k 2^-30);
+//   * and, what makes it work, for two rows m < i of the window
+//     |e_i - e_m| <= B_m (c_i - c_m) / c_i + u (S_i - S_m) / c_i,
+//     i.e. comparing a row with a recent one (the running arg-min) cancels the long
+//     history's error and leaves only the rounding of the rows in between.
+// Every decision the reference takes compares row i with its arg-min row m: the min update
+// ps_i <= ps_min and the tests ps_i > p_min + k s_min (k = out_control / warning level).
+// With s' = ds/dp the margin's error is at most
+//   D (1 + 2|s'_i|) + 2 |s'_i - k s'_m| B_m + (evaluation rounding, 2^-50 of the operands);
+// a decision whose margin exceeds that bound is the reference's decision.  Rows in the
+// exact regime (p stays exactly 0 or 1 from an exact start) compare exactly.  A stream with
+// any uncertified decision up to its stop (or the end) is rescanned by the exact kernel
+// (ddm_scan_long), so decisions and events are always the reference's; the state handed
+// back is pa's (|p - p_ref| <= B, in practice ~1e-13 relative; north_star allows p/s within
+// 1e-12 relative) together with its bound (bound_io), which a following call continues from.
+//
+// Kernels per round (a stream is cut into chunks of 4096 rows, 16 per thread):
+//   count   per chunk: errors, sum of in-chunk prefix counts, first 0 / first 1; event rows
+//           of the chunk's batches preset
+//   scan1   per stream: chunk prefix counts; the incoming detector (c0, p0, its minimum,
+//           the exact regime)
+//   eval    per chunk: every row's pa, s, p+s and bound; the chunk's arg-min
+//   scan2   per stream: the arg-min before each chunk (the incoming minimum first)
+//   decide  per chunk: every row's decisions against its arg-min, certified; first change,
+//           first uncertified row, first warning of each batch
+//   final   per stream: stop, state, bound, or the exact fallback
+//   fix     per chunk: the event rows up to the stop (perm_map labels), event counts
+// Mode 1 (a change drops the detector, a fresh one takes the next batch) repeats the round
+// from the batch after the change, up to kCertRounds rounds; what is left runs exact.
+#include <cstddef>
+
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kRowsPerThread = 16;
+constexpr int kChunk = kThreads * kRowsPerThread;   // rows per chunk
+constexpr int kMaxBatch = 256;                      // ddm_scan_long's limit (the fallback)
+constexpr int kSlots = kChunk + 2;                  // batches a chunk can touch (per_batch 1)
+constexpr int kCertRounds = 4;                      // mode 1: certified rounds before the exact kernel
+constexpr double kU = 0x1p-53;
+constexpr double kG = 0x1p-30;                      // guard: |p_ref - pa| <= 2^-30 (checked)
+constexpr unsigned long long kNone = ~0ull;
+
+struct MinEl {                 // the arg-min element: a row of the window or the incoming minimum
+    double ps, p, s, B;        // p + s, p, s, error bound of p
+    int64_t c;                 // sample count c of the row (in-window)
+    int64_t sk;                // prefix sum of the window's prefix error counts at the row
+    int32_t kind;              // 0 none, 1 the incoming minimum, 2 a window row
+    int32_t pad;
+};
+
+struct Rec {                   // the detector after a row (state handed back)
+    double p, s, B;
+    MinEl m;
+    int64_t n;
+    int32_t chg, warn;
+};
+
+struct Hdr {                   // per stream
+    int64_t lo0;               // the stream's first row (batch numbering)
+    int64_t lo, hi;            // this round's rows
+    int64_t next_lo;           // mode 1: the next round's first row
+    int64_t c0;                // samples in the incoming p (0: fresh)
+    double p0, A, B0, Bmin;    // incoming p, c0 * p0, bound of p0, bound of the incoming minimum
+    MinEl inmin;
+    int64_t rstar;             // window rows before rstar are exact (p stays 0 or 1)
+    int64_t skr;               // prefix-count sum over the exact rows
+    unsigned long long fc, fu; // first change / first uncertified row of the window (kNone)
+    int64_t nev;               // batches with an event so far (certified rounds)
+    int32_t regime;            // -1 none, 0 / 1 the exact regime's p
+    int32_t touched;           // non-empty stream: results are written
+    int32_t active;            // this round scans the stream
+    int32_t cont;              // mode 1: another round from next_lo
+    int32_t fb;                // exact fallback from lo
+    int32_t status;            // 0 certified, 1 uncertified decision, 2 rounds exhausted
+};
+
+__device__ __forceinline__ MinEl mcomb(const MinEl& L, const MinEl& R) {
+    if (R.kind == 0) return L;
+    if (L.kind == 0) return R;
+    return R.ps <= L.ps ? R : L;                    // the reference's `<=`: the later row on ties
+}
+
+__device__ __forceinline__ double sd_of(double p, double s) {   // ds/dp at (p, s = sqrt(p(1-p)/c))
+    return (s > 0.0 && p > 0.0 && p < 1.0) ? (1.0 - 2.0 * p) * s / (2.0 * p * (1.0 - p)) : 0.0;
+}
+
+struct RowV {
+    double pa, sa, ps, sd, B;
+    int64_t c;
+};
+
+// sum_{k=lo..w} (A + 2 + K_k + 2^-30 c_k) for window rows lo..w, sum K_k = skd (exact)
+__device__ __forceinline__ double s_sum(const Hdr& H, int64_t lo, int64_t w, int64_t skd) {
+    if (w < lo) return 0.0;
+    const int64_t nr = w - lo + 1;
+    const int64_t sc = nr * (H.c0 + 1) + (w * (w + 1) - (lo - 1) * lo) / 2;   // sum of c_k
+    return (double)nr * (H.A + 2.0) + (double)skd + kG * (double)sc;
+}
+
+__device__ __forceinline__ RowV row_vals(const Hdr& H, int64_t w, int64_t K, int64_t SK) {
+    RowV v;
+    v.c = H.c0 + w + 1;
+    const double cd = (double)v.c;
+    v.pa = (H.A + (double)K) / cd;
+    v.sa = sqrt(v.pa * (1.0 - v.pa) / cd);
+    v.ps = v.pa + v.sa;
+    v.sd = v.sa > 0.0 ? (1.0 - 2.0 * v.pa) / (2.0 * cd * v.sa) : 0.0;
+    if (w < H.rstar) {
+        v.B = H.B0 > 0.0 ? (double)H.c0 * H.B0 / cd * (1.0 + 0x1p-50) : 0.0;
+    } else {
+        const double S = s_sum(H, H.rstar, w, SK - H.skr);
+        v.B = ((double)H.c0 * H.B0 + kU * S * (1.0 + 0x1p-40)) / cd * (1.0 + 0x1p-50);
+    }
+    return v;
+}
+
+// Is the comparison of row v against (M.p + k M.s) (k == 0: against M.ps) decided the
+// reference's way?  margin = our value of the compared difference.
+__device__ __forceinline__ bool certain(const Hdr& H, const RowV& v, int64_t w, int64_t SK, const MinEl& M, double k,
+                                        double margin, double scale) {
+    double D, Bm, smd, evp, Bmp;
+    if (M.kind == 1) {                              // the incoming minimum (stored reference values)
+        D = v.B + H.Bmin;
+        Bm = H.Bmin;
+        smd = H.Bmin > 0.0 ? sd_of(M.p, M.s) : 0.0;
+        evp = 3.0 * kU * v.pa;
+        Bmp = Bm;
+    } else {
+        if (M.c == v.c) {
+            D = 0.0;
+        } else {
+            const int64_t mw = M.c - H.c0 - 1;      // window row of the minimum
+            const int64_t lo = max(mw + 1, H.rstar);
+            const int64_t skd = lo == mw + 1 ? SK - M.sk : SK - H.skr;
+            D = M.B * (double)(v.c - M.c) / (double)v.c +
+                kU * s_sum(H, lo, w, skd) * (1.0 + 0x1p-40) / (double)v.c;
+        }
+        Bm = M.B;
+        smd = sd_of(M.p, M.s);
+        evp = 3.0 * kU * (v.pa + M.p);
+        Bmp = Bm + 3.0 * kU * M.p;
+    }
+    if (v.B == 0.0 && Bm == 0.0 && D == 0.0) return true;     // the exact regime: exact values
+    if (v.sa == 0.0 || v.B > 0x1p-20 * fmin(v.pa, 1.0 - v.pa)) return false;
+    const double kk = k == 0.0 ? 1.0 : k;
+    const double tol = ((D + evp) * (1.0 + 2.0 * fabs(v.sd)) + 2.0 * fabs(v.sd - kk * smd) * Bmp +
+                        0x1p-50 * (v.ps + M.ps + M.p + kk * M.s)) * scale;
+    return fabs(margin) > tol;
+}
+
+// ---- block helpers
+struct Tri {                   // (errors, sum of prefix counts, rows) of a run of rows
+    int64_t k, sk, l;
+};
+__device__ __forceinline__ Tri tcomb(const Tri& a, const Tri& b) { return {a.k + b.k, a.sk + b.sk + a.k * b.l, a.l + b.l}; }
+
+// exclusive block scan of Tri over threads (Hillis-Steele in LDS)
+__device__ Tri block_excl_tri(Tri x, Tri* sh) {
+    const int t = threadIdx.x;
+    sh[t] = x;
+    __syncthreads();
+    for (int d = 1; d < kThreads; d <<= 1) {
+        Tri y = sh[t];
+        if (t >= d) y = tcomb(sh[t - d], y);
+        __syncthreads();
+        sh[t] = y;
+        __syncthreads();
+    }
+    const Tri r = t ? sh[t - 1] : Tri{0, 0, 0};
+    __syncthreads();
+    return r;
+}
+
+// exclusive block scan of MinEl (thread order); *total gets the block's inclusive result
+__device__ MinEl block_excl_min(MinEl x, MinEl* sh, MinEl* total) {
+    const int t = threadIdx.x;
+    sh[t] = x;
+    __syncthreads();
+    for (int d = 1; d < kThreads; d <<= 1) {
+        MinEl y = sh[t];
+        if (t >= d) y = mcomb(sh[t - d], y);
+        __syncthreads();
+        sh[t] = y;
+        __syncthreads();
+    }
+    MinEl none;
+    none.kind = 0;
+    const MinEl r = t ? sh[t - 1] : none;
+    if (total) *total = sh[kThreads - 1];
+    __syncthreads();
+    return r;
+}
+
+// a thread's rows of a chunk: bytes and count
+struct ThreadRows {
+    uint32_t bits;             // bit j: row j is an error
+    int n;                     // rows present
+};
+
+__device__ __forceinline__ ThreadRows load_rows(const uint8_t* __restrict__ err, int64_t r0, int64_t L) {
+    ThreadRows tr;
+    const int64_t a = r0 + (int64_t)threadIdx.x * kRowsPerThread;
+    const int64_t o = (int64_t)threadIdx.x * kRowsPerThread;
+    tr.n = (int)max((int64_t)0, min((int64_t)kRowsPerThread, L - o));
+    tr.bits = 0;
+    if (tr.n == kRowsPerThread && (a & 15) == 0) {
+        const uint4 q = *reinterpret_cast<const uint4*>(err + a);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) tr.bits |= (((w[j >> 2] >> (8 * (j & 3))) & 0xffu) != 0 ? 1u : 0u) << j;
+    } else {
+        for (int j = 0; j < tr.n; ++j) tr.bits |= (err[a + j] != 0 ? 1u : 0u) << j;
+    }
+    return tr;
+}
+
+__device__ __forceinline__ Tri thread_tri(const ThreadRows& tr) {
+    Tri t{0, 0, tr.n};
+    for (int j = 0; j < tr.n; ++j)
+        if ((tr.bits >> j) & 1u) {
+            t.k += 1;
+            t.sk += tr.n - j;                       // the error counts in the prefix of every later row
+        }
+    return t;
+}
+
+// ---- kernels
+__global__ __launch_bounds__(64) void k_cert_setup(Hdr* __restrict__ hdr, const int64_t* __restrict__ off,
+                                                    const int64_t* __restrict__ end, int64_t n_streams) {
+    const int64_t s = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (s >= n_streams) return;
+    Hdr H = {};
+    H.lo0 = H.lo = off[s];
+    H.hi = end ? end[s] : off[s + 1];
+    H.touched = H.hi > H.lo;
+    H.active = H.touched;
+    H.nev = 0;
+    hdr[s] = H;
+}
+
+__global__ __launch_bounds__(64) void k_cert_advance(Hdr* __restrict__ hdr, int64_t n_streams) {
+    const int64_t s = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (s >= n_streams) return;
+    Hdr& H = hdr[s];
+    H.active = H.cont;                              // done, or the fallback's: no further rounds
+    if (H.cont) H.lo = H.next_lo;
+    H.cont = 0;
+}
+
+__global__ __launch_bounds__(kThreads) void k_cert_count(const Hdr* __restrict__ hdr, const uint8_t* __restrict__ err,
+                                                         int64_t n_streams, int64_t n_chunks, int pb,
+                                                         int32_t* __restrict__ cnt, int64_t* __restrict__ skl,
+                                                         int32_t* __restrict__ f0, int32_t* __restrict__ f1,
+                                                         int32_t* __restrict__ ev, const int64_t* __restrict__ bbase) {
+    const int64_t s = blockIdx.x % n_streams, c = blockIdx.x / n_streams;
+    const Hdr& H = hdr[s];
+    if (!H.active) return;
+    const int64_t r0 = H.lo + c * kChunk;
+    if (r0 >= H.hi) return;
+    const int64_t L = min((int64_t)kChunk, H.hi - r0);
+    const ThreadRows tr = load_rows(err, r0, L);
+    Tri t = thread_tri(tr);
+    // the chunk's totals: errors, sum of its prefix counts (sum over errors of rows after), first 0 / 1
+    __shared__ int64_t s_k, s_sk;
+    __shared__ int s_f0, s_f1;
+    if (threadIdx.x == 0) {
+        s_k = s_sk = 0;
+        s_f0 = s_f1 = 0x7fffffff;
+    }
+    __syncthreads();
+    const int o = threadIdx.x * kRowsPerThread;
+    if (tr.n > 0) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(&s_k), (unsigned long long)t.k);
+        atomicAdd(reinterpret_cast<unsigned long long*>(&s_sk), (unsigned long long)(t.sk + t.k * (L - o - tr.n)));
+        const uint32_t pres = (1u << tr.n) - 1;
+        if (tr.bits) atomicMin(&s_f1, o + __builtin_ctz(tr.bits));
+        if (~tr.bits & pres) atomicMin(&s_f0, o + __builtin_ctz(~tr.bits & pres));
+    }
+    __syncthreads();
+    const int64_t q = s * n_chunks + c;
+    if (threadIdx.x == 0) {
+        cnt[q] = (int32_t)s_k;
+        skl[q] = s_sk;
+        f0[q] = s_f0 == 0x7fffffff ? 0x7fffffff : (int32_t)(c * kChunk + s_f0);
+        f1[q] = s_f1 == 0x7fffffff ? 0x7fffffff : (int32_t)(c * kChunk + s_f1);
+    }
+    // event rows of the batches that start in this chunk: (no warning yet, no change)
+    const int64_t b_first = (r0 - H.lo0 + pb - 1) / pb, b_last = (r0 + L - 1 - H.lo0) / pb;
+    int32_t* e = ev + 2 * bbase[s];
+    for (int64_t b = b_first + threadIdx.x; b <= b_last; b += kThreads) {
+        e[2 * b] = 0x7fffffff;
+        e[2 * b + 1] = -1;
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_cert_scan1(Hdr* __restrict__ hdr, int64_t n_chunks,
+                                                         const int32_t* __restrict__ cnt,
+                                                         const int64_t* __restrict__ skl,
+                                                         const int32_t* __restrict__ f0, const int32_t* __restrict__ f1,
+                                                         int64_t* __restrict__ kb, int64_t* __restrict__ skb,
+                                                         const ddm_state* __restrict__ state,
+                                                         const double* __restrict__ bound_in, int round) {
+    const int64_t s = blockIdx.x;
+    Hdr& H = hdr[s];
+    if (!H.active) return;
+    __shared__ Tri sh[kThreads];
+    __shared__ Tri s_carry;
+    __shared__ int s_f0, s_f1;
+    const int64_t rows = H.hi - H.lo;
+    const int64_t nck = (rows + kChunk - 1) / kChunk;
+    if (threadIdx.x == 0) {
+        s_carry = Tri{0, 0, 0};
+        s_f0 = s_f1 = 0x7fffffff;
+    }
+    __syncthreads();
+    for (int64_t base = 0; base < nck; base += kThreads) {
+        const int64_t c = base + threadIdx.x;
+        Tri x{0, 0, 0};
+        if (c < nck) {
+            const int64_t q = s * n_chunks + c;
+            x = Tri{cnt[q], skl[q], min((int64_t)kChunk, rows - c * kChunk)};
+            atomicMin(&s_f0, f0[q]);
+            atomicMin(&s_f1, f1[q]);
+        }
+        const Tri carry = s_carry;
+        const Tri ex = tcomb(carry, block_excl_tri(x, sh));
+        if (c < nck) {
+            kb[s * n_chunks + c] = ex.k;
+            skb[s * n_chunks + c] = ex.sk;
+        }
+        if (threadIdx.x == kThreads - 1) s_carry = tcomb(ex, x);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const ddm_state st = state[s];
+        const bool dropped = st.in_concept_change != 0;
+        H.c0 = dropped ? 0 : st.sample_count - 1;
+        H.p0 = dropped ? 0.0 : st.miss_prob;
+        H.A = (double)H.c0 * H.p0;
+        H.B0 = (!dropped && bound_in && round == 0) ? bound_in[2 * s] : 0.0;
+        H.Bmin = (!dropped && bound_in && round == 0) ? bound_in[2 * s + 1] : 0.0;
+        H.inmin.kind = 0;
+        if (!dropped && !__builtin_isinf(st.miss_prob_sd_min)) {
+            H.inmin.kind = 1;
+            H.inmin.ps = st.miss_prob_sd_min;
+            H.inmin.p = st.miss_prob_min;
+            H.inmin.s = st.miss_sd_min;
+            H.inmin.B = H.Bmin;
+            H.inmin.c = 0;
+            H.inmin.sk = 0;
+        }
+        if (H.c0 == 0) H.regime = s_f0 == 0 ? 0 : 1;          // a fresh detector: p = x of the first row
+        else if (H.B0 == 0.0 && (H.p0 == 0.0 || H.p0 == 1.0)) H.regime = (int)H.p0;
+        else H.regime = -1;
+        const int64_t fo = H.regime == 0 ? s_f1 : s_f0;
+        H.rstar = H.regime < 0 ? 0 : min(rows, (int64_t)fo);
+        H.skr = H.regime == 1 ? H.rstar * (H.rstar + 1) / 2 : 0;
+        H.fc = H.fu = kNone;
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_cert_eval(const Hdr* __restrict__ hdr, const uint8_t* __restrict__ err,
+                                                        int64_t n_streams, int64_t n_chunks, int min_inst,
+                                                        const int64_t* __restrict__ kb, const int64_t* __restrict__ skb,
+                                                        MinEl* __restrict__ agg) {
+    const int64_t s = blockIdx.x % n_streams, c = blockIdx.x / n_streams;
+    const Hdr& H = hdr[s];
+    if (!H.active) return;
+    const int64_t r0 = H.lo + c * kChunk;
+    if (r0 >= H.hi) return;
+    const int64_t L = min((int64_t)kChunk, H.hi - r0);
+    __shared__ Tri sh[kThreads];
+    __shared__ MinEl shm[kThreads];
+    const ThreadRows tr = load_rows(err, r0, L);
+    const Tri ex = block_excl_tri(thread_tri(tr), sh);
+    const int64_t q = s * n_chunks + c;
+    int64_t K = kb[q] + ex.k;
+    int64_t SK = skb[q] + ex.sk + kb[q] * ex.l;
+    const int64_t w0 = c * kChunk + (int64_t)threadIdx.x * kRowsPerThread;
+    MinEl m;
+    m.kind = 0;
+    for (int j = 0; j < tr.n; ++j) {
+        K += (tr.bits >> j) & 1u;
+        SK += K;
+        const int64_t w = w0 + j;
+        if (H.c0 + w + 2 < min_inst) continue;      // the gate: n (after the row) < min_num_instances
+        const RowV v = row_vals(H, w, K, SK);
+        if (m.kind == 0 || v.ps <= m.ps) {
+            m.ps = v.ps;
+            m.p = v.pa;
+            m.s = v.sa;
+            m.B = v.B;
+            m.c = v.c;
+            m.sk = SK;
+            m.kind = 2;
+        }
+    }
+    MinEl tot;
+    block_excl_min(m, shm, &tot);
+    if (threadIdx.x == 0) agg[q] = tot;
+}
+
+__global__ __launch_bounds__(kThreads) void k_cert_scan2(const Hdr* __restrict__ hdr, int64_t n_chunks,
+                                                         const MinEl* __restrict__ agg, MinEl* __restrict__ minb) {
+    const int64_t s = blockIdx.x;
+    const Hdr& H = hdr[s];
+    if (!H.active) return;
+    __shared__ MinEl shm[kThreads];
+    __shared__ MinEl s_carry;
+    const int64_t nck = (H.hi - H.lo + kChunk - 1) / kChunk;
+    if (threadIdx.x == 0) s_carry = H.inmin;
+    __syncthreads();
+    for (int64_t base = 0; base < nck; base += kThreads) {
+        const int64_t c = base + threadIdx.x;
+        MinEl x;
+        x.kind = 0;
+        if (c < nck) x = agg[s * n_chunks + c];
+        MinEl tot;
+        const MinEl carry = s_carry;
+        const MinEl ex = mcomb(carry, block_excl_min(x, shm, &tot));
+        if (c < nck) minb[s * n_chunks + c] = ex;
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry = mcomb(carry, tot);
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_cert_decide(Hdr* __restrict__ hdr, const uint8_t* __restrict__ err,
+                                                          int64_t n_streams, int64_t n_chunks, ddm_params P,
+                                                          const int64_t* __restrict__ kb,
+                                                          const int64_t* __restrict__ skb,
+                                                          const MinEl* __restrict__ minb, Rec* __restrict__ rec_chg,
+                                                          Rec* __restrict__ rec_end, int32_t* __restrict__ ev,
+                                                          const int64_t* __restrict__ bbase, double scale) {
+    const int64_t s = blockIdx.x % n_streams, c = blockIdx.x / n_streams;
+    Hdr& H = hdr[s];
+    if (!H.active) return;
+    const int64_t r0 = H.lo + c * kChunk;
+    if (r0 >= H.hi) return;
+    const int64_t L = min((int64_t)kChunk, H.hi - r0);
+    const int pb = P.per_batch, min_inst = P.min_num_instances;
+    const double wl = P.warning_level, cl = P.out_control_level;
+    __shared__ Tri sh[kThreads];
+    __shared__ MinEl shm[kThreads];
+    __shared__ int32_t s_warn[kSlots];
+    __shared__ unsigned long long s_fc, s_fu;
+    const int64_t b_lo = (r0 - H.lo0) / pb;          // the first batch a row of the chunk is in
+    const int nslot = (int)((r0 + L - 1 - H.lo0) / pb - b_lo + 1);
+    for (int k = threadIdx.x; k < nslot; k += kThreads) s_warn[k] = 0x7fffffff;
+    if (threadIdx.x == 0) s_fc = s_fu = kNone;
+    const ThreadRows tr = load_rows(err, r0, L);
+    const Tri ex = block_excl_tri(thread_tri(tr), sh);
+    const int64_t q = s * n_chunks + c;
+    const int64_t K0 = kb[q] + ex.k, SK0 = skb[q] + ex.sk + kb[q] * ex.l;
+    const int64_t w0 = c * kChunk + (int64_t)threadIdx.x * kRowsPerThread;
+    // pass 1: the thread's own arg-min (for the thread-exclusive prefix)
+    MinEl m;
+    m.kind = 0;
+    {
+        int64_t K = K0, SK = SK0;
+        for (int j = 0; j < tr.n; ++j) {
+            K += (tr.bits >> j) & 1u;
+            SK += K;
+            const int64_t w = w0 + j;
+            if (H.c0 + w + 2 < min_inst) continue;
+            const RowV v = row_vals(H, w, K, SK);
+            if (m.kind == 0 || v.ps <= m.ps) m = MinEl{v.ps, v.pa, v.sa, v.B, v.c, SK, 2, 0};
+        }
+    }
+    MinEl M = mcomb(minb[q], block_excl_min(m, shm, nullptr));
+    // pass 2: the decisions, in row order, against the running arg-min
+    unsigned long long fc = kNone, fu = kNone;
+    int64_t K = K0, SK = SK0;
+    int chg = 0, warn = 0;
+    RowV v{};
+    for (int j = 0; j < tr.n; ++j) {
+        K += (tr.bits >> j) & 1u;
+        SK += K;
+        const int64_t w = w0 + j;
+        v = row_vals(H, w, K, SK);
+        chg = warn = 0;
+        if (v.c + 1 < min_inst) continue;
+        if (M.kind != 0 && fu == kNone && !certain(H, v, w, SK, M, 0.0, v.ps - M.ps, scale)) fu = (unsigned long long)w;
+        if (M.kind == 0 || v.ps <= M.ps) M = MinEl{v.ps, v.pa, v.sa, v.B, v.c, SK, 2, 0};
+        const double tc = M.p + cl * M.s;
+        if (fu == kNone && !certain(H, v, w, SK, M, cl, v.ps - tc, scale)) fu = (unsigned long long)w;
+        if (v.ps > tc) {
+            chg = 1;
+            fc = (unsigned long long)w;
+            break;                                  // later rows of the thread follow the stream's change
+        }
+        const double tw = M.p + wl * M.s;
+        if (fu == kNone && !certain(H, v, w, SK, M, wl, v.ps - tw, scale)) fu = (unsigned long long)w;
+        if (v.ps > tw) {
+            warn = 1;
+            const int64_t rr = r0 + (w - c * kChunk) - H.lo0;          // stream row
+            atomicMin(&s_warn[rr / pb - b_lo], (int)(rr % pb));
+        }
+    }
+    if (fc != kNone) atomicMin(&s_fc, fc);
+    if (fu != kNone) atomicMin(&s_fu, fu);
+    __syncthreads();
+    // the detector after the chunk's first change (its thread), after the window's last row
+    const Rec r{v.pa, v.sa, v.B, M, v.c + 1, chg, warn};
+    if (fc != kNone && fc == s_fc) rec_chg[q] = r;
+    if (fc == kNone && tr.n > 0 && r0 + w0 - c * kChunk + tr.n == H.hi) rec_end[s] = r;
+    if (threadIdx.x == 0) {
+        if (s_fc != kNone) atomicMin(&H.fc, s_fc);
+        if (s_fu != kNone) atomicMin(&H.fu, s_fu);
+    }
+    int32_t* e = ev + 2 * bbase[s];
+    for (int k = threadIdx.x; k < nslot; k += kThreads)
+        if (s_warn[k] != 0x7fffffff) atomicMin(&e[2 * (b_lo + k)], s_warn[k]);
+}
+
+__global__ __launch_bounds__(64) void k_cert_final(Hdr* __restrict__ hdr, int64_t n_streams, int64_t n_chunks, int pb,
+                                                   int mode, const Rec* __restrict__ rec_chg,
+                                                   const Rec* __restrict__ rec_end, ddm_state* __restrict__ state,
+                                                   double* __restrict__ bound_out, int32_t* __restrict__ stop_out) {
+    const int64_t s = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (s >= n_streams) return;
+    Hdr& H = hdr[s];
+    if (!H.active) return;
+    const unsigned long long fc = H.fc, fu = H.fu;
+    if (fu != kNone && (fc == kNone || fu <= fc)) {  // an uncertified decision before the stop
+        H.fb = 1;
+        H.status = 1;
+        H.active = 0;
+        return;
+    }
+    const Rec r = fc != kNone ? rec_chg[s * n_chunks + (int64_t)(fc / kChunk)] : rec_end[s];
+    ddm_state st;
+    st.miss_prob = r.p;
+    st.miss_std = r.s;
+    if (r.m.kind == 0) {
+        st.miss_prob_min = st.miss_sd_min = st.miss_prob_sd_min = __builtin_inf();
+    } else {
+        st.miss_prob_min = r.m.p;
+        st.miss_sd_min = r.m.s;
+        st.miss_prob_sd_min = r.m.ps;
+    }
+    st.sample_count = r.n;
+    st.in_concept_change = r.chg;
+    st.in_warning_zone = r.warn;
+    const bool dropped = mode == 1 && fc != kNone;  // a fresh DDM takes the next batch (:209, :136-139)
+    if (dropped) {
+        st.miss_prob = 1.0;
+        st.miss_std = 0.0;
+        st.miss_prob_min = st.miss_sd_min = st.miss_prob_sd_min = __builtin_inf();
+        st.sample_count = 1;
+        st.in_concept_change = st.in_warning_zone = 0;
+    }
+    state[s] = st;
+    if (bound_out) {
+        bound_out[2 * s] = dropped ? 0.0 : r.B;
+        bound_out[2 * s + 1] = dropped ? 0.0 : r.m.kind == 2 ? r.m.B : r.m.kind == 1 ? H.Bmin : 0.0;
+    }
+    if (mode == 0) {
+        if (stop_out) stop_out[s] = fc == kNone ? -1 : (int32_t)((H.lo - H.lo0 + (int64_t)fc) / pb);
+    } else {
+        if (stop_out) stop_out[s] = -1;
+        if (fc != kNone) {
+            const int64_t b = (H.lo - H.lo0 + (int64_t)fc) / pb;
+            const int64_t nl = H.lo0 + (b + 1) * pb;
+            if (nl < H.hi) {
+                H.next_lo = nl;
+                H.cont = 1;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_cert_fix(Hdr* __restrict__ hdr, int64_t n_streams, int pb, int mode,
+                                                       int32_t* __restrict__ ev, const int64_t* __restrict__ bbase,
+                                                       const uint8_t* __restrict__ pmap) {
+    const int64_t s = blockIdx.x % n_streams, c = blockIdx.x / n_streams;
+    Hdr& H = hdr[s];
+    if (!H.active) return;
+    const int64_t r0 = H.lo + c * kChunk;
+    if (r0 >= H.hi) return;
+    const int64_t L = min((int64_t)kChunk, H.hi - r0);
+    const unsigned long long fc = H.fc;
+    const int64_t sb = fc == kNone ? INT64_MAX : (H.lo - H.lo0 + (int64_t)fc) / pb;
+    const int32_t sy = fc == kNone ? -1 : (int32_t)((H.lo - H.lo0 + (int64_t)fc) % pb);
+    const int64_t b_first = (r0 - H.lo0 + pb - 1) / pb, b_last = (r0 + L - 1 - H.lo0) / pb;
+    int32_t* e = ev + 2 * bbase[s];
+    int n = 0;
+    for (int64_t b = b_first + threadIdx.x; b <= b_last; b += kThreads) {
+        if (b > sb) {
+            if (mode == 0) {
+                e[2 * b] = -1;
+                e[2 * b + 1] = -1;
+            }
+            continue;                               // mode 1: the next round's
+        }
+        int32_t x = e[2 * b], y = -1;
+        if (x == 0x7fffffff) x = -1;
+        if (b == sb) {
+            y = sy;
+            if (x > y) x = -1;                      // a warning after the change is never fed
+        }
+        n += (x >= 0 || y >= 0);
+        if (pmap) {
+            const int64_t bs = H.lo0 + b * pb;
+            if (x >= 0) x = pmap[bs + x];
+            if (y >= 0) y = pmap[bs + y];
+        }
+        e[2 * b] = x;
+        e[2 * b + 1] = y;
+    }
+    __shared__ int s_n;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    if (n) atomicAdd(&s_n, n);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_n) atomicAdd(reinterpret_cast<unsigned long long*>(&H.nev), (unsigned long long)s_n);
+}
+
+// the exact fallback's arguments: streams still active after the rounds, or uncertified
+__global__ __launch_bounds__(64) void k_cert_prep_fb(Hdr* __restrict__ hdr, int64_t n_streams, int pb,
+                                                     const int64_t* __restrict__ bbase, int64_t* __restrict__ fb_off,
+                                                     int64_t* __restrict__ fb_end, int64_t* __restrict__ fb_bb,
+                                                     int32_t* __restrict__ only) {
+    const int64_t s = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (s >= n_streams) return;
+    Hdr& H = hdr[s];
+    if (H.cont) {                                   // mode 1: rounds exhausted
+        H.lo = H.next_lo;
+        H.fb = 1;
+        H.status = 2;
+        H.cont = 0;
+    }
+    fb_off[s] = H.lo;
+    fb_end[s] = H.hi;
+    fb_bb[s] = bbase[s] + (H.lo - H.lo0) / pb;
+    only[s] = H.fb;
+}
+
+__global__ __launch_bounds__(64) void k_cert_done(const Hdr* __restrict__ hdr, int64_t n_streams,
+                                                  const int64_t* __restrict__ nev_fb, int64_t* __restrict__ nev_out,
+                                                  double* __restrict__ bound_out, int32_t* __restrict__ status) {
+    const int64_t s = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (s >= n_streams) return;
+    const Hdr& H = hdr[s];
+    if (!H.touched) return;
+    if (nev_out) nev_out[s] = H.nev + (H.fb ? nev_fb[s] : 0);
+    if (H.fb && bound_out) {                        // the exact kernel's state is the reference's
+        bound_out[2 * s] = 0.0;
+        bound_out[2 * s + 1] = 0.0;
+    }
+    if (status) status[s] = H.status;
+}
+
+struct CertScratch {
+    Hdr* hdr;
+    int32_t *cnt, *f0, *f1, *only;
+    int64_t *skl, *kb, *skb, *fb_off, *fb_end, *fb_bb, *nev_fb;
+    MinEl *agg, *minb;
+    Rec *rec_chg, *rec_end;
+    void* exact;
+    int64_t bytes;
+};
+
+CertScratch cert_scratch(void* base, int64_t n, int64_t nc, int64_t exact_bytes) {
+    const auto up = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
+    CertScratch sc{};
+    int64_t o = 0;
+    uint8_t* b = static_cast<uint8_t*>(base);
+    const auto take = [&](int64_t bytes) {
+        uint8_t* p = b ? b + o : nullptr;
+        o += up(bytes);
+        return p;
+    };
+    sc.hdr = reinterpret_cast<Hdr*>(take(sizeof(Hdr) * n));
+    sc.cnt = reinterpret_cast<int32_t*>(take(4 * n * nc));
+    sc.f0 = reinterpret_cast<int32_t*>(take(4 * n * nc));
+    sc.f1 = reinterpret_cast<int32_t*>(take(4 * n * nc));
+    sc.only = reinterpret_cast<int32_t*>(take(4 * n));
+    sc.skl = reinterpret_cast<int64_t*>(take(8 * n * nc));
+    sc.kb = reinterpret_cast<int64_t*>(take(8 * n * nc));
+    sc.skb = reinterpret_cast<int64_t*>(take(8 * n * nc));
+    sc.fb_off = reinterpret_cast<int64_t*>(take(8 * n));
+    sc.fb_end = reinterpret_cast<int64_t*>(take(8 * n));
+    sc.fb_bb = reinterpret_cast<int64_t*>(take(8 * n));
+    sc.nev_fb = reinterpret_cast<int64_t*>(take(8 * n));
+    sc.agg = reinterpret_cast<MinEl*>(take(sizeof(MinEl) * n * nc));
+    sc.minb = reinterpret_cast<MinEl*>(take(sizeof(MinEl) * n * nc));
+    sc.rec_chg = reinterpret_cast<Rec*>(take(sizeof(Rec) * n * nc));
+    sc.rec_end = reinterpret_cast<Rec*>(take(sizeof(Rec) * n));
+    sc.exact = take(exact_bytes);
+    sc.bytes = o;
+    return sc;
+}
+
+double g_tol_scale = 1.0;
+
+}  // namespace
+
+extern "C" int ddm_scan_long_only(const uint8_t* err, const int64_t* stream_off, const int64_t* stream_end,
+                                  int64_t n_streams, int64_t max_rows, const ddm_params* prm, ddm_state* state_io,
+                                  const int64_t* batch_base, int32_t* ev_out, int32_t* stop_out, int64_t* nev_out,
+                                  int32_t mode, const uint8_t* perm_map, void* scratch, const int32_t* only,
+                                  ddm_stream_t stream);
+
+extern "C" int64_t ddm_scan_certified_scratch_bytes(int64_t n_streams, int64_t max_rows, int32_t per_batch) {
+    if (n_streams < 0 || max_rows < 0 || per_batch <= 0 || per_batch > kMaxBatch) return -1;
+    const int64_t nc = std::max<int64_t>(1, ddm::ceil_div(max_rows, kChunk));
+    const int64_t eb = ddm_scan_long_scratch_bytes(n_streams, max_rows, per_batch);
+    return cert_scratch(nullptr, std::max<int64_t>(1, n_streams), nc, eb).bytes;
+}
+
+extern "C" int ddm_scan_certified(const uint8_t* err, const int64_t* stream_off, const int64_t* stream_end,
+                                  int64_t n_streams, int64_t max_rows, const ddm_params* prm, ddm_state* state_io,
+                                  double* bound_io, const int64_t* batch_base, int32_t* ev_out, int32_t* stop_out,
+                                  int64_t* nev_out, int32_t mode, const uint8_t* perm_map, int32_t* status_out,
+                                  void* scratch, ddm_stream_t stream, ddm_event_t ev_begin, ddm_event_t ev_end) {
+    if (!err || !stream_off || !prm || !state_io || !batch_base || !ev_out || !scratch || n_streams < 0 ||
+        max_rows < 0 || prm->per_batch <= 0 || prm->per_batch > kMaxBatch || (mode != 0 && mode != 1)) {
+        ddm::set_error("ddm_scan_certified: invalid argument (per_batch must be 1..%d)", kMaxBatch);
+        return DDM_E_ARG;
+    }
+    if (n_streams == 0 || max_rows == 0) return 0;
+    const int64_t nc = ddm::ceil_div(max_rows, kChunk);
+    if (n_streams * nc >= ((int64_t)1 << 31) || max_rows >= ((int64_t)1 << 31) - kChunk) {
+        ddm::set_error("ddm_scan_certified: too many chunks");
+        return DDM_E_ARG;
+    }
+    const CertScratch sc = cert_scratch(scratch, n_streams, nc, ddm_scan_long_scratch_bytes(n_streams, max_rows,
+                                                                                              prm->per_batch));
+    hipStream_t s = ddm::as_hip(stream);
+    if (ev_begin)
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
+    const dim3 gs((unsigned)ddm::ceil_div(n_streams, 64)), gc((unsigned)(n_streams * nc));
+    const int pb = prm->per_batch;
+    hipLaunchKernelGGL(k_cert_setup, gs, dim3(64), 0, s, sc.hdr, stream_off, stream_end, n_streams);
+    const int rounds = mode == 0 ? 1 : kCertRounds;
+    for (int r = 0; r < rounds; ++r) {
+        if (r) hipLaunchKernelGGL(k_cert_advance, gs, dim3(64), 0, s, sc.hdr, n_streams);
+        hipLaunchKernelGGL(k_cert_count, gc, dim3(kThreads), 0, s, sc.hdr, err, n_streams, nc, pb, sc.cnt, sc.skl,
+                           sc.f0, sc.f1, ev_out, batch_base);
+        hipLaunchKernelGGL(k_cert_scan1, dim3((unsigned)n_streams), dim3(kThreads), 0, s, sc.hdr, nc, sc.cnt, sc.skl,
+                           sc.f0, sc.f1, sc.kb, sc.skb, state_io, bound_io, r);
+        hipLaunchKernelGGL(k_cert_eval, gc, dim3(kThreads), 0, s, sc.hdr, err, n_streams, nc, prm->min_num_instances,
+                           sc.kb, sc.skb, sc.agg);
+        hipLaunchKernelGGL(k_cert_scan2, dim3((unsigned)n_streams), dim3(kThreads), 0, s, sc.hdr, nc, sc.agg,
+                           sc.minb);
+        hipLaunchKernelGGL(k_cert_decide, gc, dim3(kThreads), 0, s, sc.hdr, err, n_streams, nc, *prm, sc.kb, sc.skb,
+                           sc.minb, sc.rec_chg, sc.rec_end, ev_out, batch_base, g_tol_scale);
+        hipLaunchKernelGGL(k_cert_final, gs, dim3(64), 0, s, sc.hdr, n_streams, nc, pb, (int)mode, sc.rec_chg,
+                           sc.rec_end, state_io, bound_io, stop_out);
+        hipLaunchKernelGGL(k_cert_fix, gc, dim3(kThreads), 0, s, sc.hdr, n_streams, pb, (int)mode, ev_out, batch_base,
+                           perm_map);
+        if (int rc = ddm::launch_status("ddm_scan_certified")) return rc;
+    }
+    hipLaunchKernelGGL(k_cert_prep_fb, gs, dim3(64), 0, s, sc.hdr, n_streams, pb, batch_base, sc.fb_off, sc.fb_end,
+                       sc.fb_bb, sc.only);
+    if (int rc = ddm::launch_status("ddm_scan_certified")) return rc;
+    // the exact kernel for the streams that need it (the others exit at once); it writes their
+    // events, state, stop and event count from their current start
+    if (int rc = ddm_scan_long_only(err, sc.fb_off, sc.fb_end, n_streams, max_rows, prm, state_io, sc.fb_bb, ev_out,
+                                    stop_out, sc.nev_fb, mode, perm_map, sc.exact, sc.only, stream))
+        return rc;
+    hipLaunchKernelGGL(k_cert_done, gs, dim3(64), 0, s, sc.hdr, n_streams, sc.nev_fb, nev_out, bound_io, status_out);
+    if (int rc = ddm::launch_status("ddm_scan_certified")) return rc;
+    if (ev_end)
+        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
+    return 0;
+}
+
+extern "C" int ddm_scan_certified_set_tol_scale(double scale) {
+    if (!(scale >= 1.0)) {
+        ddm::set_error("ddm_scan_certified_set_tol_scale: scale must be >= 1");
+        return DDM_E_ARG;
+    }
+    g_tol_scale = scale;
+    return 0;
+}

@@ -12,7 +12,7 @@ import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 # DDM_AMD_LIB: an alternative build of the same library (e.g. an instrumented one)
 LIB_PATH = os.environ.get("DDM_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
@@ -96,6 +96,10 @@ SIGNATURES = {
     "ddm_scan_streams_log": (ctypes.c_int, [_vp, _vp, _i64, ctypes.POINTER(DdmParams), _vp, _vp, _vp, _vp, _i64, _vp,
                                             _vp, _i32, _vp, _vp, _vp]),
     "ddm_scan_long_set_spin_limit": (ctypes.c_int, [ctypes.c_uint32]),
+    "ddm_scan_certified_scratch_bytes": (_i64, [_i64, _i64, _i32]),
+    "ddm_scan_certified": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, ctypes.POINTER(DdmParams), _vp, _vp, _vp, _vp,
+                                          _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "ddm_scan_certified_set_tol_scale": (ctypes.c_int, [ctypes.c_double]),
     "ddm_forest_predict_batch": (ctypes.c_int, [_vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "ddm_shuffle_generate_batch": (ctypes.c_int, [_vp, _i32, _vp]),
     "ddm_mt_charpoly": (ctypes.c_int, [_vp]),

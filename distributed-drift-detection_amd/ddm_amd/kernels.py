@@ -255,6 +255,25 @@ def scan_long(err, offsets, params, state, batch_base, ev, max_rows, scratch, en
                             *_evs(timer)), "ddm_scan_long")
 
 
+def scan_certified_scratch_size(n_streams, max_rows, per_batch=100):
+    """Bytes of device scratch ddm_scan_certified needs."""
+    return int(lib.ddm_scan_certified_scratch_bytes(int(n_streams), int(max_rows), int(per_batch)))
+
+
+def scan_certified(err, offsets, params, state, batch_base, ev, max_rows, scratch, ends=None, stop=None, nev=None,
+                   mode=0, perm_map=None, bound=None, status=None, stream=None, timer=None):
+    """ddm_scan_certified: ddm_scan_long's results with row-parallel certified decisions
+    (include/ddm_amd.h); bound: float64 [n, 2] device tensor (in/out) or None; status:
+    int32 [n] device tensor or None."""
+    n = offsets.numel() - (0 if ends is not None else 1)
+    assert scratch.numel() >= scan_certified_scratch_size(n, max_rows, params.per_batch)
+    assert bound is None or (bound.dtype == torch.float64 and bound.numel() >= 2 * n)
+    check(lib.ddm_scan_certified(err.data_ptr(), offsets.data_ptr(), _ptr(ends), int(n), int(max_rows),
+                                 ctypes.byref(params), state.data_ptr(), _ptr(bound), batch_base.data_ptr(),
+                                 ev.data_ptr(), _ptr(stop), _ptr(nev), int(mode), _ptr(perm_map), _ptr(status),
+                                 scratch.data_ptr(), _stream(err, stream), *_evs(timer)), "ddm_scan_certified")
+
+
 def scan_long_raw(err_ptr, off_ptr, end_ptr, n_streams, max_rows, params, state_ptr, batch_base_ptr, ev_ptr, stop_ptr,
                   nev_ptr, mode, perm_map_ptr, scratch_ptr, stream, timer=None):
     """Pointer-level ddm_scan_long (the controller's long carried windows)."""

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 16
+#define DDM_AMD_ABI_VERSION 17
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -286,6 +286,32 @@ int ddm_scan_long(const uint8_t* err, const int64_t* stream_off, const int64_t* 
                   void* scratch, ddm_stream_t stream, ddm_event_t ev_begin, ddm_event_t ev_end);
 /* Test hook: look-back spins before a chunk gives up (default 2^24, about 1 s). */
 int ddm_scan_long_set_spin_limit(uint32_t spins);
+
+/* run_DDM over long carried segments, row-parallel with CERTIFIED decisions
+ * (DDM_Process.py:135-159, the DDM carried across batches at :144-152, :202; the same
+ * arguments and results as ddm_scan_long).  Every row is evaluated from the running mean
+ * pa_i = (c0 p0 + K_i) / c_i (prefix error counts) instead of the reference's rounded
+ * recurrence; every decision (the arg-min update, the change and warning tests) carries a
+ * rigorous bound on the recurrence's rounding since the compared row (csrc/scan_cert.hip),
+ * and a stream with any decision inside its bound is rescanned by ddm_scan_long.  Events,
+ * stop, event counts, n and the flags are therefore the reference's exactly; p, s, p_min,
+ * s_min and p_min+s_min are pa's, within bound_io's bound of the reference's.
+ *   bound_io  NULL (the incoming states are the reference's) or double[2 * n_streams]:
+ *             in: (bound of |p - p_ref|, bound of |p_min - p_min_ref|) of the incoming
+ *             state; out: the same for the state handed back (0 for exact rescans).
+ *   status_out NULL or int32[n_streams]: 0 certified, 1 rescanned exactly (a decision
+ *             within its bound), 2 (mode 1) rescanned exactly after 4 certified rounds.
+ * Mode 1 runs a certified round per change (the batch after a change starts fresh), up to
+ * 4, then ddm_scan_long.  scratch: ddm_scan_certified_scratch_bytes(...) bytes, 256-byte
+ * aligned; per_batch 1..256.  Streams with an empty range are left untouched. */
+int64_t ddm_scan_certified_scratch_bytes(int64_t n_streams, int64_t max_rows, int32_t per_batch);
+int ddm_scan_certified(const uint8_t* err, const int64_t* stream_off, const int64_t* stream_end, int64_t n_streams,
+                       int64_t max_rows, const ddm_params* prm, ddm_state* state_io, double* bound_io,
+                       const int64_t* batch_base, int32_t* ev_out, int32_t* stop_out, int64_t* nev_out, int32_t mode,
+                       const uint8_t* perm_map, int32_t* status_out, void* scratch, ddm_stream_t stream,
+                       ddm_event_t ev_begin, ddm_event_t ev_end);
+/* Test hook: multiply every decision bound by scale (>= 1; huge forces the exact rescans). */
+int ddm_scan_certified_set_tol_scale(double scale);
 
 /* Timing events for the ev_begin / ev_end arguments (hipEventCreate / Destroy /
  * ElapsedTime; elapsed needs both events completed, e.g. after a stream sync). */
