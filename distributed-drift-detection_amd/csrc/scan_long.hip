@@ -70,7 +70,9 @@ __global__ __launch_bounds__(64) void k_scan_long(
     int64_t n_streams, int64_t n_chunks, ddm_params P, ddm_state* __restrict__ state,
     const int64_t* __restrict__ batch_base, int32_t* __restrict__ ev, int32_t* __restrict__ stop_out,
     int64_t* __restrict__ nev_out, int mode, const uint8_t* __restrict__ pmap, uint32_t* __restrict__ ticket,
-    int32_t* __restrict__ flag, Carry* __restrict__ carry, uint32_t spin_limit, const int32_t* __restrict__ only) {
+    int32_t* __restrict__ flag, Carry* __restrict__ carry, uint32_t spin_limit, const int32_t* __restrict__ only,
+    const int32_t* __restrict__ any) {
+    if (any && *any == 0) return;                              // (the certified scan's: nothing to rescan)
     __shared__ uint4 sbytes[kLongChunkMax / 16 + 1];
     __shared__ uint64_t smask[kLongChunkMax / 64];
     __shared__ int2 sev[64];
@@ -298,7 +300,8 @@ static int scan_long_launch(const uint8_t* err, const int64_t* stream_off, const
                             int64_t n_streams, int64_t max_rows, const ddm_params* prm, ddm_state* state_io,
                             const int64_t* batch_base, int32_t* ev_out, int32_t* stop_out, int64_t* nev_out,
                             int32_t mode, const uint8_t* perm_map, void* scratch, ddm_stream_t stream,
-                            ddm_event_t ev_begin, ddm_event_t ev_end, bool zero, const int32_t* only = nullptr) {
+                            ddm_event_t ev_begin, ddm_event_t ev_end, bool zero, const int32_t* only = nullptr,
+                            const int32_t* any = nullptr) {
     if (!err || !stream_off || !prm || !state_io || !batch_base || !ev_out || !scratch || n_streams < 0 ||
         max_rows < 0 || prm->per_batch <= 0 || prm->per_batch > kLongMaxBatch || (mode != 0 && mode != 1)) {
         ddm::set_error("ddm_scan_long: invalid argument (per_batch must be 1..%d)", kLongMaxBatch);
@@ -320,7 +323,7 @@ static int scan_long_launch(const uint8_t* err, const int64_t* stream_off, const
             return rc;
     hipLaunchKernelGGL(k_scan_long, dim3((unsigned)grid), dim3(64), 0, s, err, stream_off, stream_end, n_streams,
                        n_chunks, *prm, state_io, batch_base, ev_out, stop_out, nev_out, (int)mode, perm_map,
-                       sc.ticket, sc.flag, sc.carry, g_spin_limit, only);
+                       sc.ticket, sc.flag, sc.carry, g_spin_limit, only, any);
     if (int rc = ddm::launch_status("ddm_scan_long")) return rc;
     if (ev_end)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
@@ -346,14 +349,22 @@ extern "C" int ddm_scan_long_reuse(const uint8_t* err, const int64_t* stream_off
                             stop_out, nev_out, mode, perm_map, scratch, stream, nullptr, nullptr, false);
 }
 
-// The certified scan's exact fallback (csrc/scan_cert.hip): only the streams with only[s] != 0.
+// The certified scan's exact fallback (csrc/scan_cert.hip): only the streams with only[s] != 0,
+// and nothing at all (every block returns at once) while *any == 0.  The caller zeroes the
+// scratch's first ddm_scan_long_flag_bytes(...) bytes beforehand (no memset here).
 extern "C" int ddm_scan_long_only(const uint8_t* err, const int64_t* stream_off, const int64_t* stream_end,
                                   int64_t n_streams, int64_t max_rows, const ddm_params* prm, ddm_state* state_io,
                                   const int64_t* batch_base, int32_t* ev_out, int32_t* stop_out, int64_t* nev_out,
                                   int32_t mode, const uint8_t* perm_map, void* scratch, const int32_t* only,
-                                  ddm_stream_t stream) {
+                                  const int32_t* any, ddm_stream_t stream) {
     return scan_long_launch(err, stream_off, stream_end, n_streams, max_rows, prm, state_io, batch_base, ev_out,
-                            stop_out, nev_out, mode, perm_map, scratch, stream, nullptr, nullptr, true, only);
+                            stop_out, nev_out, mode, perm_map, scratch, stream, nullptr, nullptr, false, only, any);
+}
+
+extern "C" int64_t ddm_scan_long_flag_bytes(int64_t n_streams, int64_t max_rows, int32_t per_batch) {
+    if (n_streams < 0 || max_rows < 0 || per_batch <= 0 || per_batch > kLongMaxBatch) return 0;
+    return long_scratch(nullptr, n_streams, std::max<int64_t>(1, ddm::ceil_div(max_rows, 64 * (int64_t)per_batch)))
+        .flag_bytes;
 }
 
 extern "C" int ddm_scan_long_set_spin_limit(uint32_t spins) {
