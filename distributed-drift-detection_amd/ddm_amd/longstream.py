@@ -8,10 +8,13 @@ scanned at once, each speculatively from a fresh detector, by ddm_scan_batches (
 segments are its "streams").  The carries are then resolved in stream order: a segment
 whose true carry-in is fresh (the batch before it changed) keeps its speculative result;
 a run of segments entered with a carried detector is rescanned from it in ONE
-ddm_scan_long call (the carried detector's rows are exact arithmetic, chained through
-the run), up to the first segment boundary whose carry is fresh again.  On reset-heavy
-streams almost every carry is fresh, so the resolution is a host loop over the segments'
-end states plus a few rescans.
+ddm_scan_certified call (row-parallel, every decision certified against the reference's
+rounded recurrence, csrc/scan_cert.hip; ddm_scan_long, the exact chained recurrence, with
+certified=False), up to the first segment boundary whose carry is fresh again.  On
+reset-heavy streams almost every carry is fresh, so the resolution is a host loop over the
+segments' end states plus a few rescans.  A certified rescan hands back its detector with a
+bound on |p - p_ref| (0 when it is exact, e.g. p stuck at 1); the bound travels with the
+carry into the next rescan and across ranks.
 
 Across GPUs every rank owns a contiguous run of segments (chunk_bounds).  The ranks scan
 and resolve their segments in parallel as if their carry-in were fresh, then ONE
@@ -66,33 +69,41 @@ class Segments:
         self.n = len(self.lens)
 
 
-def _carried(scanner, row0, n_rows, state):
-    """Mode-1 scan of rows [row0, row0 + n_rows) as one stream from `state`."""
+_NO_BOUND = np.zeros(2)
+
+
+def _carried(scanner, row0, n_rows, state, bound):
+    """Mode-1 scan of rows [row0, row0 + n_rows) as one stream from `state` (whose p and
+    p_min are within `bound` of the reference's); (events, end state, its bound)."""
     if hasattr(scanner, "carried"):
-        return scanner.carried(row0, n_rows, state)
+        out = scanner.carried(row0, n_rows, state, bound)
+        return out if len(out) == 3 else (out[0], out[1], _NO_BOUND)
     st = np.empty(1, STATE_DTYPE)
     st[0] = state
     e, f = scanner.scan(row0, 1, n_rows, st)
-    return e, f[0]
+    return e, f[0], _NO_BOUND
 
 
-def resolve(carry, spec_final, segs, ev, scanner, chain=4):
-    """The segments' true carries in stream order, from carry-in `carry`.  spec_final[k]:
-    segment k's end state from a fresh carry-in; ev: the speculative event rows, overwritten
-    where a segment is rescanned.  A run of segments entered with a carried detector is
-    rescanned in one carried scan of up to `chain` segments (doubling while the run goes on),
-    up to the first of them whose last batch changed (the carry after it is fresh again).
-    Returns (the end state after the last segment, segments rescanned)."""
+def resolve(carry, spec_final, segs, ev, scanner, chain=4, bound=None):
+    """The segments' true carries in stream order, from carry-in `carry` (p and p_min within
+    `bound` of the reference's; None: exact).  spec_final[k]: segment k's end state from a
+    fresh carry-in; ev: the speculative event rows, overwritten where a segment is rescanned.
+    A run of segments entered with a carried detector is rescanned in one carried scan of up
+    to `chain` segments (doubling while the run goes on), up to the first of them whose last
+    batch changed (the carry after it is fresh again).  Returns (the end state after the last
+    segment, segments rescanned, the end state's bound)."""
     k, redone = 0, 0
     n = segs.n
+    bd = _NO_BOUND if bound is None else np.asarray(bound, np.float64)
     while k < n:
         if state_fresh(carry):
             carry = spec_final[k]
+            bd = _NO_BOUND                              # ddm_scan_batches: exact from a fresh carry
             k += 1
             continue
         m = min(n, k + chain)
         rows = sum(segs.lens[k:m])
-        e, f = _carried(scanner, segs.rows0[k], rows, carry)
+        e, f, fb = _carried(scanner, segs.rows0[k], rows, carry, bd)
         base = segs.ev_off[k]
         j_end = None
         for j in range(k, m - 1):                       # a change in segment j's last batch
@@ -101,27 +112,32 @@ def resolve(carry, spec_final, segs, ev, scanner, chain=4):
                 break
         if j_end is None:
             ev[base:segs.ev_off[m]] = e
-            carry = f
+            carry, bd = f, fb
             redone += m - k
             k = m
             chain *= 2
         else:
             ev[base:segs.ev_off[j_end + 1]] = e[:segs.ev_off[j_end + 1] - base]
-            carry = _FRESH
+            carry, bd = _FRESH, _NO_BOUND
             redone += j_end + 1 - k
             k = j_end + 1
-    return carry, redone
+    return carry, redone, bd
 
 
 class DeviceScanner:
     """ddm_scan_batches over equal-length segments of a device error buffer and
-    ddm_scan_long for carried runs (the product path; the CPU tests inject a scanner with
-    the same interface).  Scratch buffers are kept and reused across calls."""
+    ddm_scan_certified (certified=False: ddm_scan_long) for carried runs (the product path;
+    the CPU tests inject a scanner with the same interface).  Scratch buffers are kept and
+    reused across calls; `status` counts the certified calls by outcome: [certified, handed
+    to the exact kernel for a decision inside its bound, (mode 1) handed over after four
+    changes in the run]."""
 
-    def __init__(self, err, params, stream=None):
+    def __init__(self, err, params, stream=None, certified=True):
         import torch
         self.err, self.params, self.stream = err, params, stream
         self.torch = torch
+        self.certified = certified
+        self.status = [0, 0, 0]
         self._scratch = {}
 
     def _buf(self, key, nbytes):
@@ -146,9 +162,9 @@ class DeviceScanner:
         torch.cuda.synchronize(dev)
         return ev[:n_segments * nb].cpu().numpy(), st.cpu().numpy().view(STATE_DTYPE).copy()
 
-    def carried(self, row0, n_rows, state):
-        """(ev int32 [nb, 2], end state) of rows [row0, row0 + n_rows) as ONE mode-1 stream from
-        `state` (ddm_scan_long: the carried detector's rows chained through the run)."""
+    def carried(self, row0, n_rows, state, bound=None):
+        """(ev int32 [nb, 2], end state, its bound) of rows [row0, row0 + n_rows) as ONE mode-1
+        stream from `state` (p and p_min within `bound` of the reference's)."""
         from . import kernels
         from ._capi import DDM_STOP_FAILED
         torch = self.torch
@@ -161,13 +177,26 @@ class DeviceScanner:
         off = torch.tensor([row0], dtype=torch.int64, device=dev)
         end = torch.tensor([row0 + n_rows], dtype=torch.int64, device=dev)
         base = torch.zeros(1, dtype=torch.int64, device=dev)
-        scratch = self._buf("long", kernels.scan_long_scratch_size(1, n_rows, pb))
-        kernels.scan_long(self.err, off, self.params, st, base, ev, n_rows, scratch, ends=end, stop=stop, mode=1,
-                          stream=self.stream)
+        if not self.certified:
+            if bound is not None and np.any(np.asarray(bound) != 0):
+                raise ValueError("ddm_scan_long needs the reference's exact state (bound 0)")
+            scratch = self._buf("long", kernels.scan_long_scratch_size(1, n_rows, pb))
+            kernels.scan_long(self.err, off, self.params, st, base, ev, n_rows, scratch, ends=end, stop=stop, mode=1,
+                              stream=self.stream)
+            torch.cuda.synchronize(dev)
+            if int(stop.item()) == DDM_STOP_FAILED:
+                raise RuntimeError("ddm_scan_long gave up waiting for a carried state")
+            return ev[:nb].cpu().numpy(), st.cpu().numpy().view(STATE_DTYPE)[0].copy(), _NO_BOUND
+        bd = torch.from_numpy(np.asarray(_NO_BOUND if bound is None else bound, np.float64).reshape(2).copy()).to(dev)
+        status = torch.empty(1, dtype=torch.int32, device=dev)
+        scratch = self._buf("cert", kernels.scan_certified_scratch_size(1, n_rows, pb))
+        kernels.scan_certified(self.err, off, self.params, st, base, ev, n_rows, scratch, ends=end, stop=stop, mode=1,
+                               bound=bd, status=status, stream=self.stream)
         torch.cuda.synchronize(dev)
         if int(stop.item()) == DDM_STOP_FAILED:
             raise RuntimeError("ddm_scan_long gave up waiting for a carried state")
-        return ev[:nb].cpu().numpy(), st.cpu().numpy().view(STATE_DTYPE)[0].copy()
+        self.status[int(status.item())] += 1
+        return ev[:nb].cpu().numpy(), st.cpu().numpy().view(STATE_DTYPE)[0].copy(), bd.cpu().numpy()
 
 
 def _coll_device():
@@ -179,31 +208,35 @@ def _coll_device():
     return torch.device("cpu")
 
 
-def _all_gather_states(state, valid):
-    """Every rank's (valid, 56-byte state) -> [(valid, state)] in rank order (one all_gather)."""
+def _all_gather_states(state, valid, bound=None):
+    """Every rank's (valid, 56-byte state, its 16-byte bound) -> [(valid, state, bound)] in
+    rank order (one all_gather of 80-byte records)."""
     import torch
     import torch.distributed as dist
     dev = _coll_device()
-    rec = np.zeros(64, dtype=np.uint8)
+    rec = np.zeros(80, dtype=np.uint8)
     rec[:56] = np.array([state], dtype=STATE_DTYPE).view(np.uint8)
     rec[56] = 1 if valid else 0
+    rec[64:80] = np.asarray(_NO_BOUND if bound is None else bound, np.float64).reshape(2).view(np.uint8)
     t = torch.from_numpy(rec).to(dev)
     out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
     res = []
     for o in out:
         b = o.cpu().numpy()
-        res.append((bool(b[56]), b[:56].view(STATE_DTYPE)[0].copy()))
+        res.append((bool(b[56]), b[:56].view(STATE_DTYPE)[0].copy(), b[64:80].view(np.float64).copy()))
     return res
 
 
-def scan_long_stream(scanner, n_rows, per_batch, seg_batches=64, state_in=None, distributed=False, first_batch=0):
+def scan_long_stream(scanner, n_rows, per_batch, seg_batches=64, state_in=None, distributed=False, first_batch=0,
+                     with_bound=False):
     """Mode-1 DDM over the rows [0, n_rows) the scanner holds, as ONE stream (the whole
     stream, or this rank's chunk of it when `distributed`: the ranks of the default
     torch.distributed group, chunks as chunk_bounds gives them, rank order = stream order).
     Returns (ev int32 [nb, 2] of this rank's batches, the stream's end state (on the last
     rank; the carry out of this rank's chunk elsewhere), the first change's global batch
-    index or -1).  first_batch: the global index of this chunk's first batch."""
+    index or -1), plus the end state's bound (p, p_min) when with_bound.  first_batch: the
+    global index of this chunk's first batch."""
     import torch
     import torch.distributed as dist
     seg_len = segment_rows(seg_batches, per_batch)
@@ -222,25 +255,25 @@ def scan_long_stream(scanner, n_rows, per_batch, seg_batches=64, state_in=None, 
     spec_final = np.concatenate(finals) if finals else np.empty(0, STATE_DTYPE)
     carry0 = (fresh_states(1) if state_in is None else np.asarray(state_in, STATE_DTYPE).reshape(1))[0]
 
-    def resolved(carry):
+    def resolved(carry, bound):
         ev = spec_ev.copy()
-        end, _ = resolve(carry, spec_final, segs, ev, scanner)
-        return ev, end
+        end, _, bd = resolve(carry, spec_final, segs, ev, scanner, bound=bound)
+        return ev, end, bd
 
     if not distributed:
-        ev, end = resolved(carry0)
+        ev, end, bd = resolved(carry0, None)
     else:
         # every rank resolves as if its carry-in were fresh; one all-gather of the carry-outs
         # tells each rank its true carry-in unless a carried detector crosses a rank boundary
-        ev_f, end_f = resolved(_FRESH)
-        ends_f = [s for _, s in _all_gather_states(end_f, True)]
-        carry_in = [carry0] + [None] * (world - 1)
+        ev_f, end_f, bd_f = resolved(_FRESH, None)
+        ends_f = [(s, b) for _, s, b in _all_gather_states(end_f, True, bd_f)]
+        carry_in = [(carry0, None)] + [None] * (world - 1)
         true_end = {}
         mine = None
         while True:                       # every rank takes the same decisions (same data)
             for q in range(1, world):
                 if carry_in[q] is None and carry_in[q - 1] is not None:
-                    if state_fresh(carry_in[q - 1]):
+                    if state_fresh(carry_in[q - 1][0]):
                         carry_in[q] = ends_f[q - 1]
                     elif q - 1 in true_end:
                         carry_in[q] = true_end[q - 1]
@@ -249,20 +282,21 @@ def scan_long_stream(scanner, n_rows, per_batch, seg_batches=64, state_in=None, 
             # a carried detector crosses a rank boundary: the ranks whose carry-in is known and
             # carried resolve from it and publish their true carry-out (at least one per round)
             new = None
-            if carry_in[rank] is not None and not state_fresh(carry_in[rank]) and rank not in true_end:
-                mine = resolved(carry_in[rank])
-                new = mine[1]
-            for q, (ok, st) in enumerate(_all_gather_states(new if new is not None else _FRESH, new is not None)):
+            if carry_in[rank] is not None and not state_fresh(carry_in[rank][0]) and rank not in true_end:
+                mine = resolved(*carry_in[rank])
+                new = mine
+            for q, (ok, st, b) in enumerate(_all_gather_states(new[1] if new is not None else _FRESH,
+                                                               new is not None, new[2] if new is not None else None)):
                 if ok:
-                    true_end[q] = st
-        if state_fresh(carry_in[rank]):
-            ev, end = ev_f, end_f
+                    true_end[q] = (st, b)
+        if state_fresh(carry_in[rank][0]):
+            ev, end, bd = ev_f, end_f, bd_f
         else:
-            ev, end = mine if mine is not None else resolved(carry_in[rank])
+            ev, end, bd = mine if mine is not None else resolved(*carry_in[rank])
     hit = np.nonzero(ev[:, 1] >= 0)[0]
     first = int(first_batch + hit[0]) if len(hit) else -1
     if distributed:
         t = torch.tensor([first if first >= 0 else _I64_MAX], dtype=torch.int64, device=_coll_device())
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         first = int(t.item()) if int(t.item()) != _I64_MAX else -1
-    return ev, end, first
+    return (ev, end, first, bd) if with_bound else (ev, end, first)
