@@ -344,9 +344,10 @@ extern "C" int ddm_scan_long(const uint8_t* err, const int64_t* stream_off, cons
 extern "C" int ddm_scan_long_reuse(const uint8_t* err, const int64_t* stream_off, const int64_t* stream_end,
                                    int64_t n_streams, int64_t max_rows, const ddm_params* prm, ddm_state* state_io,
                                    const int64_t* batch_base, int32_t* ev_out, int32_t* stop_out, int64_t* nev_out,
-                                   int32_t mode, const uint8_t* perm_map, void* scratch, ddm_stream_t stream) {
+                                   int32_t mode, const uint8_t* perm_map, void* scratch, const int32_t* any,
+                                   ddm_stream_t stream) {
     return scan_long_launch(err, stream_off, stream_end, n_streams, max_rows, prm, state_io, batch_base, ev_out,
-                            stop_out, nev_out, mode, perm_map, scratch, stream, nullptr, nullptr, false);
+                            stop_out, nev_out, mode, perm_map, scratch, stream, nullptr, nullptr, false, nullptr, any);
 }
 
 // The certified scan's exact fallback (csrc/scan_cert.hip): only the streams with only[s] != 0,

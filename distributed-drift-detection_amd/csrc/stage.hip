@@ -14,6 +14,7 @@
 // seeds of the refit (:102), from words staged in LDS (one lane runs Fisher-Yates).
 // One workgroup per partition; nothing here decides anything, the host still does.
 #include "common.h"
+#include "ctl_dev.h"
 
 namespace {
 
@@ -55,7 +56,7 @@ static_assert(sizeof(Job) == sizeof(ddm_stage_job), "Job must mirror ddm_stage_j
 // refit goes through, on the device or the host, from the draw after the seeds), or no
 // change at all; windows reaching a short last batch stay with the host.  Written by one
 // thread; W = 0 when not planned.
-__device__ void plan_next(const Job& jb, int32_t stop, bool drawn, int64_t p_seeds) {
+__device__ void plan_next(const Job& jb, int32_t stop, bool drawn, int64_t p_seeds, int64_t pickv) {
     int64_t jn, Pn, g0n, winn;
     bool ok = true;
     if (stop >= 0) {
@@ -70,7 +71,7 @@ __device__ void plan_next(const Job& jb, int32_t stop, bool drawn, int64_t p_see
         jn = jb.b_end;
         ok = jb.tail == 0;
         const int64_t Wg = max((int64_t)0, min(jb.b_end, jb.n_full) - jb.g0);
-        Pn = Wg > 0 ? *jb.pick + 1 : (jb.p_after_first >= 0 ? jb.p_after_first : jb.p_now);
+        Pn = Wg > 0 ? pickv + 1 : (jb.p_after_first >= 0 ? jb.p_after_first : jb.p_now);
         g0n = jn;
         winn = jb.win * 2;
     }
@@ -100,7 +101,9 @@ __device__ void plan_next(const Job& jb, int32_t stop, bool drawn, int64_t p_see
     }
 }
 
-__global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__ jobs) {
+// One partition's staging (the workgroup's); pickv: the RNG position the pick found (the
+// draw before the window's first unused batch shuffle), read where the host's pick is.
+__device__ void stage_body(const Job& jb, int64_t pickv) {
     __shared__ int counts[kStageThreads / 64];
 #ifdef DDM_STAGE_PROFILE
     const uint64_t t0 = wall_clock64();
@@ -109,7 +112,6 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
 #else
 #define STAGE_MARK(k) do { } while (0)
 #endif
-    const Job jb = jobs[blockIdx.x];
     const int t = threadIdx.x;
     if (jb.stall && *jb.stall) {            // device-resident runner: this partition waits for the host
         if (t == 0) {
@@ -196,7 +198,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
         if (t == 0) {
             jb.info_out[0] = -1;
             jb.info_out[3] = -1;
-            if (jb.plan_out) plan_next(jb, stop, false, -1);
+            if (jb.plan_out) plan_next(jb, stop, false, -1, pickv);
         }
         return;
     }
@@ -206,7 +208,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     int64_t P;
     if (d < jb.g0) P = jb.p_after_first;                        // the refit batch itself
     else if (jb.tail && d == jb.nb - 1) P = jb.p_tail_after;    // the short last batch
-    else P = *jb.pick + 1;
+    else P = pickv + 1;
     if (t == 0) {
         jb.info_out[0] = P;
         jb.info_out[3] = d;
@@ -246,7 +248,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     if (!jb.R || !jb.perm_w || !jb.seeds_out || j >= jb.nb) {
         if (t == 0) {
             jb.info_out[6] = 0;
-            if (jb.plan_out) plan_next(jb, stop, false, -1);
+            if (jb.plan_out) plan_next(jb, stop, false, -1, pickv);
         }
         return;
     }
@@ -332,7 +334,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     if (!ok) {
         if (t == 0) {
             jb.info_out[6] = 0;
-            if (jb.plan_out) plan_next(jb, stop, false, -1);
+            if (jb.plan_out) plan_next(jb, stop, false, -1, pickv);
         }
         return;
     }
@@ -353,7 +355,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
         jb.info_out[4] = pos[0];
         jb.info_out[5] = pos[1];
         jb.info_out[6] = 1;
-        if (jb.plan_out) plan_next(jb, stop, true, pos[1]);
+        if (jb.plan_out) plan_next(jb, stop, true, pos[1], pickv);
     }
 #ifdef DDM_STAGE_PROFILE
     __syncthreads();
@@ -364,7 +366,59 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
 #endif
 }
 
+__global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__ jobs) {
+    const Job jb = jobs[blockIdx.x];
+    stage_body(jb, jb.pick ? *jb.pick : -1);
+}
+
+// The device-resident runner's epoch tail in one launch, a workgroup per partition: the
+// pick of the RNG position (ddm_shuffle_pick_batch), the staging (k_stage), the partition's
+// decisions (k_ctl's commit + plan); the last workgroup to finish splits the predict grid.
+__global__ __launch_bounds__(kStageThreads) void k_stage_ctl(const Job* __restrict__ jobs,
+                                                             const ddm_shuffle_job* __restrict__ sjobs,
+                                                             const ddm_ctl c) {
+    __shared__ int64_t s_pick;
+    __shared__ ddm_ctl_part s_part;
+    __shared__ int s_last;
+    const int t = threadIdx.x;
+    const Job jb = jobs[blockIdx.x];
+    if (t == 0) {
+        const ddm_shuffle_job& sj = sjobs[blockIdx.x];
+        int64_t v = -1;
+        if (sj.pick_out) {
+            const int64_t k = (sj.stop && sj.stop[0] >= 0 ? (int64_t)sj.stop[0] : sj.pick_last) - sj.pick_offset;
+            v = (sj.W > 0 && k >= 0 && k < sj.W) ? sj.E[k] : -1;
+            sj.pick_out[0] = v;
+        }
+        s_pick = v;
+    }
+    __syncthreads();
+    stage_body(jb, s_pick);
+    __syncthreads();
+    if (t < 64) ctl_record(c, (int)blockIdx.x, &s_part, t, 0);
+    __threadfence();
+    __syncthreads();
+    if (t == 0) s_last = atomicAdd(c.sync, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (s_last && t == 0) {
+        __threadfence();
+        ctl_split(c);
+        c.sync[0] = 0;                              // the ticket, for the next epoch
+    }
+}
+
 }  // namespace
+
+extern "C" int ddm_epoch_stage_ctl(const ddm_stage_job* jobs_dev, const ddm_shuffle_job* shuffle_jobs,
+                                   const ddm_ctl* ctl, ddm_stream_t stream) {
+    if (!jobs_dev || !shuffle_jobs || !ctl || !ctl->sync || ctl->n <= 0) {
+        ddm::set_error("ddm_epoch_stage_ctl: invalid argument");
+        return DDM_E_ARG;
+    }
+    hipLaunchKernelGGL(k_stage_ctl, dim3((unsigned)ctl->n), dim3(kStageThreads), 0, ddm::as_hip(stream),
+                       reinterpret_cast<const Job*>(jobs_dev), shuffle_jobs, *ctl);
+    return ddm::launch_status("ddm_epoch_stage_ctl");
+}
 
 extern "C" int ddm_epoch_stage(const ddm_stage_job* jobs_dev, int32_t n_jobs, ddm_stream_t stream) {
     if (!jobs_dev || n_jobs < 0) {

@@ -12,7 +12,7 @@ import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 # DDM_AMD_LIB: an alternative build of the same library (e.g. an instrumented one)
 LIB_PATH = os.environ.get("DDM_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
@@ -67,7 +67,7 @@ class DdmCtl(ctypes.Structure):
     _fields_ = [("parts", _vp), ("n", _i32), ("entry", _i32), ("jobs", _vp), ("segs", _vp), ("seg_res", _vp),
                 ("stage", _vp), ("off", _vp), ("end", _vp), ("state", _vp), ("first", _vp), ("stop", _vp),
                 ("pick", _vp), ("loff", _vp), ("lend", _vp), ("pstall", _vp), ("predict_blocks", _i64),
-                ("status", _vp), ("logs", _vp), ("log_b0", _vp)]
+                ("status", _vp), ("logs", _vp), ("log_b0", _vp), ("sync", _vp)]
 
 
 class DdmCtlEpoch(ctypes.Structure):

@@ -9,9 +9,9 @@ enqueues groups of epochs ahead and only polls the partitions' records between g
 
     host:    enter (upload the records, plan + shuffle the first windows)
              [K epochs][K epochs] ... poll the records of the group before the last one
-    device:  predict -> scan (+ long scan) -> pick -> staging (events into a per-partition
-             log, batch d+1's shuffle, the refit's seeds) -> k_ctl (decisions, next tables)
-             -> next windows' shuffles (side stream) | device refits -> ...
+    device:  predict -> scan (+ long scan) -> [pick -> staging (events into a per-partition
+             log, batch d+1's shuffle, the refit's seeds) -> decisions, next tables: one
+             kernel, k_stage_ctl] -> next windows' shuffles (side stream) | device refits -> ...
 
 A partition the device cannot carry on alone stalls (a refit that reported a status or did
 not compile, stream words that ran out) or parks (a short last batch still to shuffle);
@@ -51,6 +51,9 @@ class DeviceController:
         self.poll_h = [torch.zeros(n * CTL.itemsize, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
         self.res_ptrs = torch.zeros(n, dtype=torch.int64, device=dev)
         self.pstall = torch.zeros(n, dtype=torch.int32, device=dev)
+        # [0] the fused staging + decision kernel's block ticket (it leaves it 0), [1] the next
+        # epoch has a long window (ddm_scan_long's blocks return at once otherwise)
+        self.sync = torch.zeros(2, dtype=torch.int32, device=dev)
         self.logs = [torch.empty(3 * max(1, nb), dtype=torch.int32, device=dev) for nb in r.nbs]
         self.log_off = np.concatenate([[0], np.cumsum([3 * max(1, nb) for nb in r.nbs])]).astype(np.int64)
         self.logs_h = torch.empty(int(self.log_off[-1]), dtype=torch.int32, pin_memory=True)   # read-back of all
@@ -99,6 +102,7 @@ class DeviceController:
         c.stop, c.pick, c.loff, c.lend = base + r.o_stop, base + r.o_pick, base + r.o_loff, base + r.o_lend
         c.pstall, c.predict_blocks, c.status = self.pstall.data_ptr(), PREDICT_BLOCKS, None
         c.logs, c.log_b0 = self.log_ptrs.data_ptr(), self.log_b0.data_ptr()
+        c.sync = self.sync.data_ptr()
         E.n, E.per_batch = self.n, r.s.per_batch
         E.err, E.params, E.batch_base = r.err_all.data_ptr(), ctypes.addressof(r.params), base + r.o_bbase
         E.n_batches_total, E.ev_out, E.nev, E.perm_map = r.ev_total, r.ev_d.data_ptr(), base + r.o_nev, \

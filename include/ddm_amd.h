@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 17
+#define DDM_AMD_ABI_VERSION 18
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -617,6 +617,9 @@ typedef struct ddm_ctl {
     int64_t* status;                               /* [4]: active, stalled, parked, done       */
     int32_t* const* logs;                          /* per partition: its event log             */
     int64_t* log_b0;                               /* per partition: the window's first batch  */
+    uint32_t* sync;                                /* NULL or uint32[2], zeroed: [0] the fused
+                                                      staging's block ticket (left 0), [1] set
+                                                      when the next epoch has a long window    */
 } ddm_ctl;
 
 typedef struct ddm_ctl_epoch {
@@ -639,7 +642,9 @@ int64_t ddm_ctl_epoch_bytes(void);
 int ddm_ctl_enter(const ddm_ctl_epoch* e);
 /* n_epochs device epochs on e->stream: predict, scan (+ long), pick, staging, decisions and
  * the next windows' plan, then the next windows' shuffles on side_stream beside the device
- * refits.  Epochs after every partition is done, parked or stalled do no work. */
+ * refits.  Epochs after every partition is done, parked or stalled do no work.  With
+ * ctl.sync, pick + staging + decisions are one kernel (the last workgroup splits the predict
+ * grid) and the long scan's blocks return at once in epochs without a long window. */
 int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs);
 
 /* Forest predict for the device-resident runner: one launch, fixed grid, segments and block
