@@ -3,13 +3,14 @@
 // The host trainer (rf_fit.cpp, pinned to scikit-learn 1.7.2 by tests/test_trainer.py)
 // is restated here with the same arithmetic, so that both build the same trees:
 //   k_dfit_prep    one workgroup per job: gate, NaN check, classes_ (np.unique) and the
-//                  class index of every row, per-feature presorted row orders;
-//   k_dfit_trees   one wave per (job, tree):
+//                  class index of every row, per-feature presorted row orders; beside
+//                  it, boot workgroups (one wave per tree):
 //                    * RandomState(seed): init_genrand on lane 0 (a serial recurrence),
 //                      the 624-word twist in three lane-parallel phases, tempering;
 //                    * the splitter seed = the first randint(0, 2**31-1) of that stream
 //                      (peeked) and the bootstrap = randint(0, L, L) from the same start
 //                      (accept/reject by ballot, counts by LDS atomics);
+//   k_dfit_trees   one wave per (job, tree), from the boot workgroups' draws:
 //                    * depth-first BestSplitter: the feature draws (our_rand_r) and the
 //                      constant-feature bookkeeping run identically in every lane; a
 //                      node's rows in feature order come from the presorted order by a
@@ -83,7 +84,7 @@ struct Stump {
 
 // ---- per-job scratch layout -------------------------------------------------------
 struct Layout {
-    int64_t yidx, order, tnodes, tvals, tmeta, bfs, cslot, cstump, ctree, cnode, cleaf, cframe, csort, total;
+    int64_t yidx, order, tnodes, tvals, tmeta, bfs, cslot, cstump, ctree, cnode, cleaf, cframe, csort, boot, total;
 };
 
 __host__ __device__ inline int64_t al16(int64_t v) { return (v + 15) & ~(int64_t)15; }
@@ -104,7 +105,8 @@ __host__ __device__ inline Layout layout(int L, int F, int T, int K) {
     o.cleaf = al16(o.cnode + (int64_t)sizeof(ddm_cforest_node) * T * (kMaxCfLeaves - 1));
     o.cframe = al16(o.cleaf + (int64_t)T * kMaxCfLeaves);
     o.csort = al16(o.cframe + 16 * (int64_t)2 * kMaxCfLeaves);
-    o.total = al16(o.csort + 4 * (int64_t)T);
+    o.boot = al16(o.csort + 4 * (int64_t)T);
+    o.total = al16(o.boot + 4 * (int64_t)T * (L + 1));
     return o;
 }
 
@@ -195,11 +197,90 @@ __device__ __forceinline__ int wave_scan_i(int v, int lane) {
     return v;
 }
 
-// ---- k_dfit_prep --------------------------------------------------------------------
-constexpr int kPrepThreads = 1024;         // presort tasks: every (feature, row) pair
+// RandomState(seed) of one tree (init_genrand on lane 0: a serial recurrence, on the
+// scalar unit it made the trees kernel slower, 46 -> 54 us with 800 waves sharing one
+// scalar unit per CU; the 624-word twist lane-parallel), the splitter seed = the first
+// randint(0, 2**31 - 1) of that stream (peeked, not consumed) and the bootstrap =
+// randint(0, L, L) from the same start, as multiplicities in cnt[0..L).  One wave; returns
+// the splitter seed.
+__device__ uint32_t tree_boot(uint32_t seed, int L, uint32_t* mt, int32_t* cnt, int lane) {
+    if (lane == 0) {
+        uint32_t v = seed;
+        mt[0] = v;
+        for (int i = 1; i < 624; ++i) {
+            v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
+            mt[i] = v;
+        }
+    }
+    wave_sync();
+    twist(mt, lane);
+    for (int k = lane; k < L; k += 64) cnt[k] = 0;
+    wave_sync();
+    uint32_t rstate = 0;
+    for (int j0 = 0; j0 < 624; j0 += 64) {
+        const int j = j0 + lane;
+        const uint32_t v = j < 624 ? (temper(mt[j]) & 0x7fffffffu) : 0xffffffffu;
+        const uint64_t m = __ballot(j < 624 && v <= kRandRMax - 1u);
+        if (m) {
+            rstate = __shfl(v, __builtin_ctzll(m), 64);
+            break;
+        }
+    }
+    if (L > 1) {
+        const uint32_t mx = (uint32_t)(L - 1);
+        const uint32_t mask = 0xffffffffu >> __builtin_clz(mx);
+        int taken = 0;
+        for (;;) {
+            for (int j0 = 0; j0 < 624 && taken < L; j0 += 64) {
+                const int j = j0 + lane;
+                const uint32_t v = j < 624 ? (temper(mt[j]) & mask) : 0xffffffffu;
+                const bool acc = j < 624 && v <= mx;
+                const uint64_t m = __ballot(acc);
+                if (acc && taken + __popcll(m & lanemask_lt(lane)) < L) atomicAdd(&cnt[v], 1);
+                taken += __popcll(m);
+            }
+            if (taken >= L) break;
+            twist(mt, lane);
+        }
+    } else if (lane == 0) {
+        cnt[0] = 1;                                 // interval(0) draws nothing
+    }
+    wave_sync();
+    return rstate;
+}
 
+// k_dfit_prep's boot workgroups (blockIdx.y > 0): one tree per wave, the draws tree_boot
+// makes, stored for k_dfit_trees (rstate, then the L bootstrap counts).  They run beside
+// the presort instead of at the head of every tree wave (init_genrand alone is ~15 us).
+// Only the first wave of each SIMD works: the init recurrence runs on one lane, but every
+// wave64 VALU instruction holds its SIMD for 4 cycles, so 16 such waves per CU (4 per
+// SIMD) took 58 us instead of ~20 and slowed the window shuffles beside them.
+constexpr int kPrepThreads = 1024;         // presort tasks: every (feature, row) pair
+constexpr int kBootWaves = 4;              // working waves (trees) per boot workgroup
+
+__device__ void dfit_boot(const Job& jb, int bblk) {
+    __shared__ uint32_t s_mt[kBootWaves][624];
+    __shared__ int32_t s_cnt[kBootWaves][kMaxL];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tree = bblk * kBootWaves + w;
+    const int L = jb.L;
+    if (w >= kBootWaves || gated_off(jb) || L < 1 || L > kMaxL || jb.F < 1 || jb.F > kMaxF || jb.n_trees < 1 || jb.n_trees > 256 ||
+        jb.k_cap < 1 || jb.k_cap > kMaxK || jb.max_features < 1 || tree >= jb.n_trees)
+        return;
+    const Layout lo = layout(L, jb.F, jb.n_trees, jb.k_cap);
+    int32_t* bt = reinterpret_cast<int32_t*>(jb.scratch + lo.boot) + (int64_t)tree * (L + 1);
+    const uint32_t rs = tree_boot((uint32_t)jb.seeds[tree], L, s_mt[w], s_cnt[w], lane);
+    if (lane == 0) bt[0] = (int32_t)rs;
+    for (int k = lane; k < L; k += 64) bt[1 + k] = s_cnt[w][k];
+}
+
+// ---- k_dfit_prep --------------------------------------------------------------------
 __global__ __launch_bounds__(kPrepThreads) void k_dfit_prep(const Job* __restrict__ jobs) {
     const Job jb = jobs[blockIdx.x];
+    if (blockIdx.y > 0) {
+        dfit_boot(jb, (int)blockIdx.y - 1);
+        return;
+    }
     const int t = threadIdx.x;
     __shared__ int32_t s_y[kMaxL];
     __shared__ float s_tile[kPrepTile];
@@ -283,7 +364,6 @@ __global__ __launch_bounds__(kPrepThreads) void k_dfit_prep(const Job* __restric
 // ---- k_dfit_trees -------------------------------------------------------------------
 struct WaveLds {
     uint32_t mt[624];      // raw MT state
-    uint32_t tw[624];      // tempered words of the current block
     int32_t cnt[kMaxL];    // bootstrap multiplicity
     int16_t key[kMaxL];    // node key of each in-bag row (-1: out of bag)
     uint8_t crow[kMaxL];   // the node's rows in the current feature's order
@@ -447,7 +527,7 @@ __device__ __forceinline__ Best node_split(WaveLds& S, const float* __restrict__
 
 __device__ __forceinline__ void build_tree(const Job& jb, const Layout& lo, int tree, int K, WaveLds& S, int lane,
                                            const float* __restrict__ X, const uint8_t* __restrict__ order,
-                                           const uint8_t* __restrict__ yidx) {
+                                           const uint8_t* __restrict__ yidx, const int32_t* __restrict__ boot) {
     const int L = jb.L, F = jb.F;
     const int64_t M = 2 * (int64_t)L - 1;
     TNode* nodes = reinterpret_cast<TNode*>(jb.scratch + lo.tnodes) + tree * M;
@@ -457,62 +537,21 @@ __device__ __forceinline__ void build_tree(const Job& jb, const Layout& lo, int 
 #ifdef DDM_DFIT_PROFILE
     const uint64_t t_a = wall_clock64();
 #endif
-    // ---- RandomState(seed): init_genrand (serial), first block, on lane 0 (on the scalar
-    // unit instead it made the trees kernel slower: 46 -> 54 us per launch with 800 waves,
-    // which share one scalar unit per CU)
-    if (lane == 0) {
-        uint32_t v = (uint32_t)jb.seeds[tree];
-        S.mt[0] = v;
-        for (int i = 1; i < 624; ++i) {
-            v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
-            S.mt[i] = v;
-        }
+    // ---- RandomState(seed), the splitter seed and the bootstrap counts: drawn by
+    // k_dfit_prep's boot workgroups beside the presort when it ran (boot != nullptr)
+    uint32_t rstate = 0;
+    if (boot) {
+        const int32_t* bt = boot + (int64_t)tree * (L + 1);
+        for (int k = lane; k < L; k += 64) S.cnt[k] = bt[1 + k];
+        rstate = (uint32_t)bt[0];
+        wave_sync();
+    } else {
+        rstate = tree_boot((uint32_t)jb.seeds[tree], L, S.mt, S.cnt, lane);
     }
-    wave_sync();
 #ifdef DDM_DFIT_PROFILE
     const uint64_t t_a1 = wall_clock64();
+    const uint64_t t_b = t_a1;
 #endif
-    twist(S.mt, lane);
-    for (int k = lane; k < 624; k += 64) S.tw[k] = temper(S.mt[k]);
-    for (int k = lane; k < L; k += 64) S.cnt[k] = 0;
-    wave_sync();
-#ifdef DDM_DFIT_PROFILE
-    const uint64_t t_b = wall_clock64();
-#endif
-    // splitter seed: first randint(0, 2**31 - 1) of the stream, not consumed
-    uint32_t rstate = 0;
-    for (int j0 = 0; j0 < 624; j0 += 64) {
-        const int j = j0 + lane;
-        const uint32_t v = j < 624 ? (S.tw[j] & 0x7fffffffu) : 0xffffffffu;
-        const uint64_t m = __ballot(j < 624 && v <= kRandRMax - 1u);
-        if (m) {
-            rstate = __shfl(v, __builtin_ctzll(m), 64);
-            break;
-        }
-    }
-    // bootstrap: randint(0, L, L) from the start of the same stream
-    if (L > 1) {
-        const uint32_t mx = (uint32_t)(L - 1);
-        const uint32_t mask = 0xffffffffu >> __builtin_clz(mx);
-        int taken = 0;
-        for (;;) {
-            for (int j0 = 0; j0 < 624 && taken < L; j0 += 64) {
-                const int j = j0 + lane;
-                const uint32_t v = j < 624 ? (S.tw[j] & mask) : 0xffffffffu;
-                const bool acc = j < 624 && v <= mx;
-                const uint64_t m = __ballot(acc);
-                if (acc && taken + __popcll(m & lanemask_lt(lane)) < L) atomicAdd(&S.cnt[v], 1);
-                taken += __popcll(m);
-            }
-            if (taken >= L) break;
-            twist(S.mt, lane);
-            for (int k = lane; k < 624; k += 64) S.tw[k] = temper(S.mt[k]);
-            wave_sync();
-        }
-    } else {
-        if (lane == 0) S.cnt[0] = 1;           // interval(0) draws nothing
-    }
-    wave_sync();
     for (int k = lane; k < L; k += 64) S.key[k] = S.cnt[k] > 0 ? 0 : -1;
     for (int f = lane; f < F; f += 64) S.feats[f] = (int16_t)f;
     wave_sync();
@@ -729,7 +768,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfit_trees(const Job* __restric
         int K = 0;
         if (!fused_prep<true>(jb, s_X, s_ord, s_yi, K)) return;
         const Layout lo = layout(jb.L, jb.F, jb.n_trees, jb.k_cap);
-        if (tree < jb.n_trees) build_tree(jb, lo, tree, K, lds[w], lane, s_X, s_ord, s_yi);
+        if (tree < jb.n_trees) build_tree(jb, lo, tree, K, lds[w], lane, s_X, s_ord, s_yi, nullptr);
         return;
     }
     if (gated_off(jb) || jb.result[DDM_DFIT_STATUS] != 0) return;
@@ -738,6 +777,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfit_trees(const Job* __restric
     const int LF = jb.L * jb.F;
     const uint8_t* yidx = jb.scratch + lo.yidx;
     const uint8_t* order = jb.scratch + lo.order;
+    const int32_t* boot = reinterpret_cast<const int32_t*>(jb.scratch + lo.boot);
     if (LF <= kTreeTile) {
         for (int e = threadIdx.x; e < LF; e += 64 * kWaves) {
             s_X[e] = jb.X[e];
@@ -745,9 +785,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfit_trees(const Job* __restric
         }
         for (int e = threadIdx.x; e < jb.L; e += 64 * kWaves) s_yi[e] = yidx[e];
         __syncthreads();
-        if (tree < jb.n_trees) build_tree(jb, lo, tree, K, lds[w], lane, s_X, s_ord, s_yi);
+        if (tree < jb.n_trees) build_tree(jb, lo, tree, K, lds[w], lane, s_X, s_ord, s_yi, boot);
     } else if (tree < jb.n_trees) {
-        build_tree(jb, lo, tree, K, lds[w], lane, jb.X, order, yidx);
+        build_tree(jb, lo, tree, K, lds[w], lane, jb.X, order, yidx, boot);
     }
 }
 
@@ -1259,7 +1299,8 @@ extern "C" int ddm_rf_fit_device_lf(const ddm_dfit_job* jobs_dev, int32_t n_jobs
     const Job* jobs = reinterpret_cast<const Job*>(jobs_dev);
     const bool fused = max_lf > 0 && max_lf <= kTreeTile;
     if (!fused) {
-        hipLaunchKernelGGL(k_dfit_prep, dim3((unsigned)n_jobs), dim3(kPrepThreads), 0, s, jobs);
+        hipLaunchKernelGGL(k_dfit_prep, dim3((unsigned)n_jobs, 1u + (unsigned)ddm::ceil_div(max_trees, kBootWaves)),
+                           dim3(kPrepThreads), 0, s, jobs);
         if (int rc = ddm::launch_status("ddm_rf_fit_device/prep")) return rc;
     }
     hipLaunchKernelGGL(fused ? k_dfit_trees<true> : k_dfit_trees<false>,
