@@ -29,6 +29,16 @@ extern "C" int ddm_event_create(ddm_event_t* ev) {
     return 0;
 }
 
+// An event for stream ordering only (no timestamps): the epochs' fork / join events.
+extern "C" int ddm_event_create_sync(ddm_event_t* ev) {
+    if (!ev) return DDM_E_ARG;
+    hipEvent_t e;
+    if (int rc = ddm::hip_status(hipEventCreateWithFlags(&e, hipEventDisableTiming), "ddm_event_create_sync"))
+        return rc;
+    *ev = reinterpret_cast<ddm_event_t>(e);
+    return 0;
+}
+
 extern "C" int ddm_event_destroy(ddm_event_t ev) {
     return ddm::hip_status(hipEventDestroy(reinterpret_cast<hipEvent_t>(ev)), "ddm_event_destroy");
 }

@@ -51,6 +51,7 @@ int launch_ctl(const ddm_ctl& c, int entry, hipStream_t s) {
 // largest window the runner allows (65,536 batches) launched ~13k mostly idle blocks per
 // epoch (C5: 64 us of every epoch).
 constexpr int64_t kShufW = 64 * 256, kShufPieces = 256;
+constexpr int32_t kPermBlocks = 256;            // ddm_err_permute_dev blocks per partition
 
 }  // namespace
 
@@ -59,8 +60,14 @@ extern "C" int ddm_scan_long_reuse(const uint8_t* err, const int64_t* stream_off
                                    const int64_t* batch_base, int32_t* ev_out, int32_t* stop_out, int64_t* nev_out,
                                    int32_t mode, const uint8_t* perm_map, void* scratch, const int32_t* any,
                                    ddm_stream_t stream);
+extern "C" int ddm_forest_predict_dev_orig(const ddm_predict_segment* segs_dev, const int64_t* const* res_dev,
+                                           int32_t n_segs, int32_t per_batch, int64_t grid, int32_t* stall,
+                                           int64_t delta, ddm_stream_t stream);
+extern "C" int ddm_err_permute_dev(const ddm_predict_segment* segs_dev, int32_t n_segs, int32_t per_batch,
+                                   int64_t delta, int32_t blocks_per_seg, ddm_stream_t stream);
 extern "C" int ddm_epoch_stage_ctl(const ddm_stage_job* jobs_dev, const ddm_shuffle_job* shuffle_jobs,
-                                   const ddm_ctl* ctl, ddm_stream_t stream);
+                                   const ddm_ctl* ctl, const uint8_t* err, const ddm_params* prm,
+                                   const uint8_t* perm_map, ddm_stream_t stream);
 
 namespace {
 
@@ -101,19 +108,42 @@ extern "C" int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs) {
     hipStream_t s = ddm::as_hip(e->stream);
     hipStream_t side = ddm::as_hip(e->side_stream);
     const ddm_ctl& c = e->ctl;
+    // decoupled epochs: the predict writes row-order errors (it needs the refit's forest, not
+    // the window's shuffle) and waits for the shuffles only before the permutation into DDM
+    // order, so the side stream's window shuffles overlap the refit AND the predict
+    const bool dec = e->decouple && e->row_order_delta != 0 && c.sync;
+    auto join = [&]() {
+        return ddm::hip_status(hipStreamWaitEvent(s, reinterpret_cast<hipEvent_t>(e->join_ev), 0), "join");
+    };
     for (int32_t k = 0; k < n_epochs; ++k) {
+        if (!dec)
+            if (int rc = join()) return rc;         // the last epoch's shuffles of this window
         if (int rc = rec(e->ev[0], s)) return rc;
-        if (int rc = ddm_forest_predict_dev(c.segs, c.seg_res, c.n, e->per_batch, c.predict_blocks, c.pstall,
-                                            e->stream, nullptr, nullptr))
-            return rc;
+        if (dec) {
+            if (int rc = ddm_forest_predict_dev_orig(c.segs, c.seg_res, c.n, e->per_batch, c.predict_blocks, c.pstall,
+                                                     e->row_order_delta, e->stream))
+                return rc;
+        } else {
+            if (int rc = ddm_forest_predict_dev(c.segs, c.seg_res, c.n, e->per_batch, c.predict_blocks, c.pstall,
+                                                e->stream, nullptr, nullptr))
+                return rc;
+        }
         if (int rc = rec(e->ev[1], s)) return rc;
+        if (dec)
+            if (int rc = join()) return rc;
         if (int rc = rec(e->ev[2], s)) return rc;
-        if (int rc = ddm_scan_streams_log(e->err, c.off, c.n, e->params, c.state, c.first, c.logs,
-                                          reinterpret_cast<int64_t*>(reinterpret_cast<uint8_t*>(c.parts) +
-                                                                     offsetof(ddm_ctl_part, n_log)),
-                                          (int64_t)(sizeof(ddm_ctl_part) / sizeof(int64_t)), c.log_b0,
-                                          const_cast<int32_t*>(c.stop), 0, e->perm_map, c.end, e->stream))
-            return rc;
+        if (dec)
+            if (int rc = ddm_err_permute_dev(c.segs, c.n, e->per_batch, e->row_order_delta, kPermBlocks, e->stream))
+                return rc;
+        // fused tail (c.sync): the one-lane scan runs inside the staging kernel, after the
+        // long scan of the windows it does not take
+        if (!c.sync)
+            if (int rc = ddm_scan_streams_log(e->err, c.off, c.n, e->params, c.state, c.first, c.logs,
+                                              reinterpret_cast<int64_t*>(reinterpret_cast<uint8_t*>(c.parts) +
+                                                                         offsetof(ddm_ctl_part, n_log)),
+                                              (int64_t)(sizeof(ddm_ctl_part) / sizeof(int64_t)), c.log_b0,
+                                              const_cast<int32_t*>(c.stop), 0, e->perm_map, c.end, e->stream))
+                return rc;
         if (e->long_max_rows > 0)
             if (int rc = ddm_scan_long_reuse(e->err, c.loff, c.lend, c.n, e->long_max_rows, e->params, c.state,
                                              e->batch_base, e->ev_out, const_cast<int32_t*>(c.stop), e->nev, 0,
@@ -121,10 +151,11 @@ extern "C" int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs) {
                                              c.sync ? reinterpret_cast<const int32_t*>(c.sync + 1) : nullptr,
                                              e->stream))
                 return rc;
-        if (c.sync) {                               // pick + staging + decisions: one launch
+        if (c.sync) {                               // scan + pick + staging + decisions: one launch
             if (int rc = rec(e->ev[3], s)) return rc;
             if (int rc = rec(e->ev[4], s)) return rc;
-            if (int rc = ddm_epoch_stage_ctl(c.stage, c.jobs, &c, e->stream)) return rc;
+            if (int rc = ddm_epoch_stage_ctl(c.stage, c.jobs, &c, e->err, e->params, e->perm_map, e->stream))
+                return rc;
         } else {
             if (int rc = ddm_shuffle_pick_batch(c.jobs, c.n, e->stream)) return rc;
             if (int rc = rec(e->ev[3], s)) return rc;
@@ -150,8 +181,8 @@ extern "C" int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs) {
             if (int rc = ddm_rf_fit_device_lf(e->dfit_jobs, e->n_dfit, e->max_trees, e->dfit_max_lf, e->stream)) return rc;
             if (int rc = rec(e->ev[7], s)) return rc;
         }
-        if (int rc = ddm::hip_status(hipStreamWaitEvent(s, reinterpret_cast<hipEvent_t>(e->join_ev), 0), "join"))
-            return rc;
     }
+    // the next call's first epoch waits for the last shuffles (the caller synchronises the
+    // side stream before it reads anything they write)
     return 0;
 }

@@ -78,6 +78,12 @@ struct Seg {
 };
 static_assert(sizeof(Seg) == sizeof(ddm_predict_segment) && sizeof(Seg) == 176, "Seg must mirror ddm_predict_segment");
 
+// Internal segment flag (device-resident epochs, ddm_forest_predict_dev_orig): err is written
+// in ROW order (position g gets the error of row g - row_base, no perm read; first_err notes
+// the first error row) and ddm_err_permute_dev puts the bytes into DDM order once the
+// window's shuffles are done.  The predict then needs the forest only, not the shuffle.
+constexpr int32_t kSegRowOrder = 1 << 8;
+
 template <bool kPure, int kK, bool kLdsForest>
 __device__ __forceinline__ void predict_segment(const Seg& sg, int64_t blk, int64_t nblk, int64_t per_batch,
                                                 unsigned char* smem) {
@@ -428,7 +434,7 @@ __device__ __forceinline__ void cf_segment(const Seg& sg, int64_t blk, int64_t n
             const int64_t g = g0 + i * tile + tid;
             int e = 0;
             if (tid < tile && g < sg.pos_end) {
-                const int k = i * kCfThreads + tb + (int)sg.perm[g];
+                const int k = i * kCfThreads + ((sg.flags & kSegRowOrder) ? tid : tb + (int)sg.perm[g]);
                 e = s_e[k];
                 sg.err[g] = (uint8_t)e;
                 if (sg.pred) sg.pred[g] = s_pred[k];
@@ -566,7 +572,8 @@ __device__ __forceinline__ void cf_segment_vec(const Seg& sg, int64_t blk, int64
         int e_any = 0;
         int64_t g_first = g;
         if (q0 < tile && g < sg.pos_end) {
-            const uint32_t p4 = *reinterpret_cast<const uint32_t*>(sg.perm + g);
+            const uint32_t p4 = (sg.flags & kSegRowOrder) ? 0x03020100u + (uint32_t)(q0 % pb) * 0x01010101u
+                                                          : *reinterpret_cast<const uint32_t*>(sg.perm + g);
             uint32_t out = 0;
             int first = -1;
 #pragma unroll
@@ -723,6 +730,7 @@ bool cf_usable(const Seg& g, int pb) {
 // not compile, or needs more LDS than the launch has) sets stall[s]: the partition waits
 // for the host, which refits or walks it.
 constexpr size_t kDevLds = 80 * 1024;
+constexpr size_t kDevLdsRowOrder = 48 * 1024;
 
 __device__ __forceinline__ int cf_rows_dev(const Seg& g, int pb) {
     if (g.cf_leaves > 0) return 1;
@@ -734,7 +742,8 @@ __device__ __forceinline__ int cf_rows_dev(const Seg& g, int pb) {
 
 __global__ __launch_bounds__(kCfThreads) void k_cforest_predict_dev(const Seg* __restrict__ segs,
                                                                     const int64_t* const* __restrict__ res,
-                                                                    int n_segs, int pb, int32_t* __restrict__ stall) {
+                                                                    int n_segs, int pb, int32_t* __restrict__ stall,
+                                                                    int64_t row_order_delta, int lds_cap) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int64_t gb = blockIdx.x;
     int s = 0;
@@ -742,6 +751,10 @@ __global__ __launch_bounds__(kCfThreads) void k_cforest_predict_dev(const Seg* _
     if (s == n_segs) return;
     Seg sg = ldu(segs + s);
     if (sg.pos_end <= sg.pos_begin) return;
+    if (row_order_delta) {                          // row order into err + delta (kSegRowOrder)
+        sg.err += row_order_delta;                  // first_err: the first error ROW (a valid hint)
+        sg.flags |= kSegRowOrder;
+    }
     const int64_t* r = ldu(res + s);
     if (r) {       // the refit's result words (written by an earlier kernel: read-only here)
         sg.n_classes = (int32_t)ldu(r + DDM_DFIT_CLASSES);
@@ -756,7 +769,7 @@ __global__ __launch_bounds__(kCfThreads) void k_cforest_predict_dev(const Seg* _
     const int rows = cf_rows_dev(sg, pb);
     const bool usable = sg.cforest && sg.cf_slots >= 0 && sg.cf_slots <= 32 && sg.cf_vote_regs >= 1 &&
                         sg.cf_vote_regs <= 4 && sg.cf_tab_words >= 0 && sg.pos_begin % pb == 0 &&
-                        cf_lds_bytes(sg.cf_leaves, sg.cf_slots, sg.cf_tab_words, rows) <= kDevLds;
+                        cf_lds_bytes(sg.cf_leaves, sg.cf_slots, sg.cf_tab_words, rows) <= (size_t)lds_cap;
     if (!usable) {
         if (threadIdx.x == 0) stall[s] = 1;
         return;
@@ -984,9 +997,97 @@ extern "C" int ddm_forest_predict_dev(const ddm_predict_segment* segs_dev, const
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
     hipLaunchKernelGGL(k_cforest_predict_dev, dim3((unsigned)grid), dim3(kCfThreads), kDevLds, s,
-                       reinterpret_cast<const Seg*>(segs_dev), res_dev, (int)n_segs, (int)per_batch, stall);
+                       reinterpret_cast<const Seg*>(segs_dev), res_dev, (int)n_segs, (int)per_batch, stall,
+                       (int64_t)0, (int)kDevLds);
     if (int rc = ddm::launch_status("ddm_forest_predict_dev")) return rc;
     if (ev_end)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
     return 0;
+}
+
+// ---- row-order predict + the permutation into DDM order (device-resident epochs) --------
+namespace {
+
+// err[g] = err_rows[(g / pb) * pb + perm[g]] over every segment's positions (err_rows =
+// err + delta, written by ddm_forest_predict_dev_orig).  The row-order predict noted its
+// first error ROW in first_err: every batch before that row's batch is error-free, so
+// those positions are only zero-filled (16-byte stores), and the hint the scan gets is that
+// batch's first position (the row itself is no hint: the batch's shuffle may put an error
+// row ahead of it).  From that batch on, a thread takes 4 positions of one batch
+// (pb % 4 == 0) or single positions otherwise.
+constexpr int kPermThreads = 256;
+
+__global__ __launch_bounds__(kPermThreads) void k_err_permute(const Seg* __restrict__ segs, int64_t delta, int pb) {
+    const Seg sg = ldu(segs + blockIdx.y);
+    if (sg.pos_end <= sg.pos_begin) return;
+    const uint8_t* src = sg.err + delta;
+    const int64_t tid = (int64_t)blockIdx.x * kPermThreads + threadIdx.x;
+    const int64_t step = (int64_t)gridDim.x * kPermThreads;
+    const unsigned long long f = sg.first_err ? *sg.first_err : ~0ull;
+    const int64_t zend = f >= (unsigned long long)sg.pos_end
+                             ? sg.pos_end
+                             : max(sg.pos_begin, ((int64_t)f / pb) * pb);
+    // every block computes the same zend from f or from zend itself: the store is idempotent
+    if (blockIdx.x == 0 && threadIdx.x == 0 && zend < sg.pos_end) *sg.first_err = (unsigned long long)zend;
+    // zeros: [pos_begin, zend)
+    {
+        const int64_t a0 = min(zend, (sg.pos_begin + 15) & ~(int64_t)15), a1 = max(a0, zend & ~(int64_t)15);
+        for (int64_t g = sg.pos_begin + tid; g < a0; g += step) sg.err[g] = 0;
+        for (int64_t w = a0 / 16 + tid; w < a1 / 16; w += step) reinterpret_cast<uint4*>(sg.err)[w] = make_uint4(0, 0, 0, 0);
+        for (int64_t g = a1 + tid; g < zend; g += step) sg.err[g] = 0;
+    }
+    // the permutation: [zend, pos_end); zend is batch-aligned
+    if (pb % 4 == 0 && zend % 4 == 0) {
+        for (int64_t g = zend + 4 * tid; g < sg.pos_end; g += 4 * step) {
+            const int64_t b0 = (g / pb) * pb;
+            const uint32_t p4 = *reinterpret_cast<const uint32_t*>(sg.perm + g);
+            uint32_t out = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const bool ok = g + i < sg.pos_end;
+                const uint32_t e = ok ? src[b0 + ((p4 >> (8 * i)) & 0xffu)] : 0u;
+                out |= e << (8 * i);
+            }
+            if (g + 4 <= sg.pos_end) {
+                *reinterpret_cast<uint32_t*>(sg.err + g) = out;
+            } else {
+                for (int i = 0; g + i < sg.pos_end; ++i) sg.err[g + i] = (uint8_t)((out >> (8 * i)) & 0xffu);
+            }
+        }
+    } else {
+        for (int64_t g = zend + tid; g < sg.pos_end; g += step) sg.err[g] = src[(g / pb) * pb + sg.perm[g]];
+    }
+}
+
+}  // namespace
+
+// Internal (csrc/ctl.hip): the device-table predict writing err + delta in row order.
+extern "C" int ddm_forest_predict_dev_orig(const ddm_predict_segment* segs_dev, const int64_t* const* res_dev,
+                                           int32_t n_segs, int32_t per_batch, int64_t grid, int32_t* stall,
+                                           int64_t delta, ddm_stream_t stream) {
+    if (!segs_dev || !res_dev || !stall || n_segs <= 0 || per_batch <= 0 || per_batch > 256 || grid <= 0 ||
+        grid >= ((int64_t)1 << 31) || delta == 0) {
+        ddm::set_error("ddm_forest_predict_dev_orig: invalid argument");
+        return DDM_E_ARG;
+    }
+    // 48 KB of LDS per workgroup instead of 80: two predict workgroups per CU (their VGPR
+    // limit) leave 64 KB, so the window shuffles on the side stream find room beside them
+    // (a forest that needs more stalls its partition to the host, as any unusable forest)
+    hipLaunchKernelGGL(k_cforest_predict_dev, dim3((unsigned)grid), dim3(kCfThreads), kDevLdsRowOrder,
+                       ddm::as_hip(stream), reinterpret_cast<const Seg*>(segs_dev), res_dev, (int)n_segs,
+                       (int)per_batch, stall, delta, (int)kDevLdsRowOrder);
+    return ddm::launch_status("ddm_forest_predict_dev_orig");
+}
+
+// Internal (csrc/ctl.hip): row-order errors (err + delta) into DDM order, every segment.
+extern "C" int ddm_err_permute_dev(const ddm_predict_segment* segs_dev, int32_t n_segs, int32_t per_batch,
+                                   int64_t delta, int32_t blocks_per_seg, ddm_stream_t stream) {
+    if (!segs_dev || n_segs <= 0 || n_segs > 65535 || per_batch <= 0 || per_batch > 256 || delta == 0 ||
+        blocks_per_seg <= 0) {
+        ddm::set_error("ddm_err_permute_dev: invalid argument");
+        return DDM_E_ARG;
+    }
+    hipLaunchKernelGGL(k_err_permute, dim3((unsigned)blocks_per_seg, (unsigned)n_segs), dim3(kPermThreads), 0,
+                       ddm::as_hip(stream), reinterpret_cast<const Seg*>(segs_dev), delta, (int)per_batch);
+    return ddm::launch_status("ddm_err_permute_dev");
 }

@@ -13,8 +13,11 @@
 // shuffle (written into the partition's perm array, DDM_Process.py:190) and the T tree
 // seeds of the refit (:102), from words staged in LDS (one lane runs Fisher-Yates).
 // One workgroup per partition; nothing here decides anything, the host still does.
+#include <cstddef>
+
 #include "common.h"
 #include "ctl_dev.h"
+#include "scan_fast.h"
 
 namespace {
 
@@ -103,7 +106,11 @@ __device__ void plan_next(const Job& jb, int32_t stop, bool drawn, int64_t p_see
 
 // One partition's staging (the workgroup's); pickv: the RNG position the pick found (the
 // draw before the window's first unused batch shuffle), read where the host's pick is.
-__device__ void stage_body(const Job& jb, int64_t pickv) {
+// pos_next >= 0: batch d + 1 of a change in batch d lies in the window, whose shuffles
+// (ddm_shuffle_window_batch) already drew it from the draw after batch d's shuffle, as the
+// reference does (DDM_Process.py:190 follows :187/:190 of batch d directly); its perm bytes
+// are in place and pos_next is the draw after it, so only the seeds are drawn here.
+__device__ void stage_body(const Job& jb, int64_t pickv, int64_t pos_next = -1) {
     __shared__ int counts[kStageThreads / 64];
 #ifdef DDM_STAGE_PROFILE
     const uint64_t t0 = wall_clock64();
@@ -253,7 +260,9 @@ __device__ void stage_body(const Job& jb, int64_t pickv) {
         return;
     }
     const int Lj = j == jb.nb - 1 ? jb.last_len : jb.pb;
-    for (int w = t; w < kStageWords; w += kStageThreads) words[w] = jb.R[P + w];
+    const bool pre = pos_next >= 0;                 // batch j shuffled by the window already
+    const int64_t Pw = pre ? pos_next : P;
+    for (int w = t; w < kStageWords; w += kStageThreads) words[w] = jb.R[Pw + w];
     __syncthreads();
     STAGE_MARK(2);
     if (wv == 0) {
@@ -265,7 +274,7 @@ __device__ void stage_body(const Job& jb, int64_t pickv) {
         // of one interval per round.
         int k = 0;
         bool good = true;
-        int i = Lj - 1;
+        int i = pre ? 0 : Lj - 1;
         while (i >= 1) {
             const int il = i - lane, wi = k + lane;
             bool acc = false;
@@ -301,7 +310,7 @@ __device__ void stage_body(const Job& jb, int64_t pickv) {
             }
             if (!good) break;
         }
-        if (lane == 0) pos[0] = P + k;
+        if (lane == 0) pos[0] = Pw + k;
         STAGE_MARK(3);
         int got = 0;                                                 // seeds drawn so far
         while (good && got < jb.n_trees) {
@@ -325,7 +334,7 @@ __device__ void stage_body(const Job& jb, int64_t pickv) {
             }
         }
         if (lane == 0) {
-            pos[1] = P + k;
+            pos[1] = Pw + k;
             ok = good ? 1 : 0;
         }
     }
@@ -340,7 +349,7 @@ __device__ void stage_body(const Job& jb, int64_t pickv) {
     }
     // the swaps, all elements at once: element e starts at position e and follows the
     // transpositions i <-> js[i] for i = Lj-1 .. 1; it ends where Fisher-Yates puts it
-    if (t < Lj) {
+    if (!pre && t < Lj) {
         int q = t;
 #pragma unroll 8
         for (int i = Lj - 1; i >= 1; --i) {
@@ -350,7 +359,8 @@ __device__ void stage_body(const Job& jb, int64_t pickv) {
         perm[q] = (uint8_t)t;
     }
     __syncthreads();
-    for (int i = t; i < Lj; i += kStageThreads) jb.perm_w[jb.base + j * jb.pb + i] = perm[i];
+    if (!pre)
+        for (int i = t; i < Lj; i += kStageThreads) jb.perm_w[jb.base + j * jb.pb + i] = perm[i];
     if (t == 0) {
         jb.info_out[4] = pos[0];
         jb.info_out[5] = pos[1];
@@ -371,31 +381,59 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     stage_body(jb, jb.pick ? *jb.pick : -1);
 }
 
+// The one-lane DDM scan of the epoch's windows, when the fused kernel runs it (err set).
+struct FoldScan {
+    const uint8_t* err;
+    const uint8_t* perm_map;
+    ddm_params P;
+};
+
 // The device-resident runner's epoch tail in one launch, a workgroup per partition: the
-// pick of the RNG position (ddm_shuffle_pick_batch), the staging (k_stage), the partition's
-// decisions (k_ctl's commit + plan); the last workgroup to finish splits the predict grid.
+// partition's one-lane DDM scan (ddm_scan_streams_log's k_scan_fast worker; a window on
+// ddm_scan_long was scanned before this launch), the pick of the RNG position
+// (ddm_shuffle_pick_batch), the staging (k_stage), the partition's decisions (k_ctl's
+// commit + plan); the last workgroup to finish splits the predict grid.
 __global__ __launch_bounds__(kStageThreads) void k_stage_ctl(const Job* __restrict__ jobs,
                                                              const ddm_shuffle_job* __restrict__ sjobs,
-                                                             const ddm_ctl c) {
-    __shared__ int64_t s_pick;
+                                                             const ddm_ctl c, const FoldScan fs) {
+    __shared__ int64_t s_pick, s_next;
     __shared__ ddm_ctl_part s_part;
     __shared__ int s_last;
+    __shared__ double s_rcp[kRcpN];
     const int t = threadIdx.x;
-    const Job jb = jobs[blockIdx.x];
+    const int i = (int)blockIdx.x;
+    const Job jb = jobs[i];
+    if (fs.err) {
+        for (int k = t; k < kRcpN; k += kStageThreads) s_rcp[k] = 1.0 / (double)(k > 0 ? k : 1);
+        __syncthreads();
+        if (t == 0 && !(c.lend[i] > c.loff[i])) {
+            const EvSink sink{nullptr, c.logs,
+                              reinterpret_cast<int64_t*>(reinterpret_cast<uint8_t*>(c.parts) + offsetof(ddm_ctl_part, n_log)),
+                              (int64_t)(sizeof(ddm_ctl_part) / sizeof(int64_t)), c.log_b0};
+            scan_fast_worker(fs.err, c.off, c.n, fs.P, c.state, c.first, nullptr, sink, const_cast<int32_t*>(c.stop),
+                             nullptr, 0, fs.perm_map, c.end, i, (int64_t)c.n, s_rcp);
+            __threadfence();                        // stop, state and the log count for the block
+        }
+        __syncthreads();
+    }
     if (t == 0) {
-        const ddm_shuffle_job& sj = sjobs[blockIdx.x];
-        int64_t v = -1;
+        const ddm_shuffle_job& sj = sjobs[i];
+        int64_t v = -1, nx = -1;
         if (sj.pick_out) {
-            const int64_t k = (sj.stop && sj.stop[0] >= 0 ? (int64_t)sj.stop[0] : sj.pick_last) - sj.pick_offset;
+            const bool chg = sj.stop && sj.stop[0] >= 0;
+            const int64_t k = (chg ? (int64_t)sj.stop[0] : sj.pick_last) - sj.pick_offset;
             v = (sj.W > 0 && k >= 0 && k < sj.W) ? sj.E[k] : -1;
             sj.pick_out[0] = v;
+            // a change in batch d: batch d + 1 (window index k + 1) was shuffled by the window
+            if (chg && sj.W > 0 && k + 1 >= 0 && k + 1 < sj.W) nx = sj.E[k + 1] + 1;
         }
         s_pick = v;
+        s_next = nx;
     }
     __syncthreads();
-    stage_body(jb, s_pick);
+    stage_body(jb, s_pick, s_next);
     __syncthreads();
-    if (t < 64) ctl_record(c, (int)blockIdx.x, &s_part, t, 0);
+    if (t < 64) ctl_record(c, i, &s_part, t, 0);
     __threadfence();
     __syncthreads();
     if (t == 0) s_last = atomicAdd(c.sync, 1u) == gridDim.x - 1;
@@ -409,14 +447,19 @@ __global__ __launch_bounds__(kStageThreads) void k_stage_ctl(const Job* __restri
 
 }  // namespace
 
+// err != NULL: the kernel also runs the epoch's one-lane DDM scan (mode 0) on err with the
+// params and perm_map given.
 extern "C" int ddm_epoch_stage_ctl(const ddm_stage_job* jobs_dev, const ddm_shuffle_job* shuffle_jobs,
-                                   const ddm_ctl* ctl, ddm_stream_t stream) {
-    if (!jobs_dev || !shuffle_jobs || !ctl || !ctl->sync || ctl->n <= 0) {
+                                   const ddm_ctl* ctl, const uint8_t* err, const ddm_params* prm,
+                                   const uint8_t* perm_map, ddm_stream_t stream) {
+    if (!jobs_dev || !shuffle_jobs || !ctl || !ctl->sync || ctl->n <= 0 || (err && (!prm || prm->per_batch <= 0))) {
         ddm::set_error("ddm_epoch_stage_ctl: invalid argument");
         return DDM_E_ARG;
     }
+    FoldScan fs{err, perm_map, {}};
+    if (err) fs.P = *prm;
     hipLaunchKernelGGL(k_stage_ctl, dim3((unsigned)ctl->n), dim3(kStageThreads), 0, ddm::as_hip(stream),
-                       reinterpret_cast<const Job*>(jobs_dev), shuffle_jobs, *ctl);
+                       reinterpret_cast<const Job*>(jobs_dev), shuffle_jobs, *ctl, fs);
     return ddm::launch_status("ddm_epoch_stage_ctl");
 }
 

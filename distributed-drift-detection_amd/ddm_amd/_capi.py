@@ -12,7 +12,7 @@ import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 # DDM_AMD_LIB: an alternative build of the same library (e.g. an instrumented one)
 LIB_PATH = os.environ.get("DDM_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
@@ -77,7 +77,7 @@ class DdmCtlEpoch(ctypes.Structure):
                 ("batch_base", _vp), ("n_batches_total", _i64), ("ev_out", _vp), ("nev", _vp), ("perm_map", _vp),
                 ("long_max_rows", _i64), ("long_scratch", _vp), ("dfit_jobs", _vp), ("n_dfit", _i32),
                 ("max_trees", _i32), ("max_W", _i64), ("max_pieces", _i64), ("dfit_max_lf", _i64),
-                ("ev", _vp * 12)]
+                ("ev", _vp * 12), ("row_order_delta", _i64), ("decouple", _i32), ("pad_dc", _i32)]
 
 # name -> (restype, argtypes); every symbol include/ddm_amd.h declares.
 SIGNATURES = {
@@ -121,6 +121,7 @@ SIGNATURES = {
                                           _vp, _vp, _vp]),
     "ddm_shuffle_pick": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
     "ddm_event_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
+    "ddm_event_create_sync": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
     "ddm_event_destroy": (ctypes.c_int, [_vp]),
     "ddm_event_elapsed_ms": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(ctypes.c_float)]),
     "ddm_event_record": (ctypes.c_int, [_vp, _vp]),

@@ -903,8 +903,8 @@ class BatchRunner:
         self.side_stream = torch.cuda.Stream(self.device, priority=-1)   # the next windows' shuffles: as long as the refits
         E.side_stream = self.side_stream.cuda_stream
         self._fork_ev, self._join_ev = ctypes.c_void_p(), ctypes.c_void_p()
-        check(lib.ddm_event_create(ctypes.byref(self._fork_ev)), "ddm_event_create")
-        check(lib.ddm_event_create(ctypes.byref(self._join_ev)), "ddm_event_create")
+        check(lib.ddm_event_create_sync(ctypes.byref(self._fork_ev)), "ddm_event_create_sync")
+        check(lib.ddm_event_create_sync(ctypes.byref(self._join_ev)), "ddm_event_create_sync")
         E.fork_ev, E.join_ev = self._fork_ev.value, self._join_ev.value
         if self.dfit_rows:
             # split read-back: the host works on the epoch while the refits run

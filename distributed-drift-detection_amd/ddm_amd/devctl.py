@@ -34,6 +34,13 @@ CTL = kernels.CTL_PART_DTYPE
 _OFF = {name: CTL.fields[name][1] for name in CTL.names}
 PREDICT_BLOCKS = 2048
 GROUP = 4                       # epochs per enqueued group
+# Decoupled epochs (csrc/ctl.hip): when the partitions' windows average at least this many
+# rows, the predict writes row-order errors without waiting for the window's shuffles (a
+# serial chain of ~130 us at C3's 14k-batch windows, longer than the refit beside it) and a
+# permutation kernel puts them into DDM order after it; small windows (C5, c2) keep the
+# shuffles before the predict (they finish under the refit, and the permutation would be one
+# launch more per epoch).
+DECOUPLE_ROWS = 200_000
 
 
 class DeviceController:
@@ -62,6 +69,8 @@ class DeviceController:
         self.avail_h = torch.zeros(64 * n, dtype=torch.int64, pin_memory=True)   # H2D sources (a ring)
         self._avail_k = 0
         self.long_min_rows, self.long_cap_rows = int(long_min_rows), int(long_cap_rows)
+        # row-order errors of decoupled epochs: a buffer shaped like the runner's err
+        self.err_rows = torch.empty_like(r.err_all)
         self.timers = []             # per-epoch HIP event pairs when the runner times kernels
         self.seg_log = None          # (segs, res) device copies per epoch when the runner logs predicts
         self._E = None
@@ -113,6 +122,8 @@ class DeviceController:
         E.max_W = mw
         E.dfit_max_lf = dfit.max_lf(r.s.per_batch, max(p.X.shape[0] for p in r.parts))
         E.max_pieces = 2 + 64 + r.shuffles[0].window_draws(mw) // 8192
+        E.row_order_delta = self.err_rows.data_ptr() - r.err_all.data_ptr()
+        E.decouple = 0
         self._E = E
         return E
 
@@ -243,6 +254,7 @@ class DeviceController:
                 r.dfit_jobs.h[:self.n * dfit.DFIT_DTYPE.itemsize], non_blocking=True)
         self._publish_avail()
         E = self._epoch_struct()
+        E.decouple = self._decouple([(ps.win, r.max_wins[ps.i]) for ps in live])
         check(lib.ddm_ctl_enter(ctypes.byref(E)), "ddm_ctl_enter")
         r._mark("device phase entered")
         timing = r.t_pred is not None
@@ -270,6 +282,7 @@ class DeviceController:
                 if not self._extend(rec):
                     r._mark("poll: stream buffers would overflow")
                     break
+                E.decouple = self._decouple([(int(rec["win"][i]), r.max_wins[i]) for i in np.nonzero(active)[0]])
                 r._enqueue_rest()
                 self._publish_avail()
             pending = (ev, slot)
@@ -288,6 +301,14 @@ class DeviceController:
         out = self._take_back(live)
         r._mark("records taken back")
         return out
+
+    def _decouple(self, wins):
+        """1 when the active partitions' windows ((win, max_win) pairs) average at least
+        DECOUPLE_ROWS rows."""
+        w = [min(int(a), int(b)) for a, b in wins]
+        if not w:
+            return 0
+        return int(sum(w) * self.r.s.per_batch >= DECOUPLE_ROWS * len(w))
 
     def _one_epoch_instrumented(self, E, timing, logging):
         r = self.r

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 18
+#define DDM_AMD_ABI_VERSION 19
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -316,6 +316,8 @@ int ddm_scan_certified_set_tol_scale(double scale);
 /* Timing events for the ev_begin / ev_end arguments (hipEventCreate / Destroy /
  * ElapsedTime; elapsed needs both events completed, e.g. after a stream sync). */
 int ddm_event_create(ddm_event_t* ev);
+/* ABI 19: an event for stream ordering only (hipEventDisableTiming): fork / join events. */
+int ddm_event_create_sync(ddm_event_t* ev);
 int ddm_event_destroy(ddm_event_t ev);
 int ddm_event_record(ddm_event_t ev, ddm_stream_t stream);
 int ddm_event_synchronize(ddm_event_t ev);
@@ -635,6 +637,12 @@ typedef struct ddm_ctl_epoch {
     int64_t dfit_max_lf;                           /* ddm_rf_fit_device_lf's max_lf             */
     ddm_event_t ev[12];                            /* optional begin/end pairs: predict, scan, long,
                                                       stage + ctl, refit, next shuffles        */
+    int64_t row_order_delta;                       /* ABI 19: a buffer shaped like err at err +
+                                                      delta (0: none) for decoupled epochs     */
+    int32_t decouple, pad_dc;                      /* 1: the predict writes row-order errors
+                                                      there without waiting for the window's
+                                                      shuffles, which are waited for only by
+                                                      the permutation into err (DDM order)     */
 } ddm_ctl_epoch;
 int64_t ddm_ctl_part_bytes(void);
 int64_t ddm_ctl_epoch_bytes(void);

@@ -57,6 +57,29 @@ def test_device_epochs_equal_host_epochs(case):
     assert st.refits == st_h.refits
 
 
+@pytest.mark.parametrize("case", ["blocks", "noise", "tails"])
+def test_decoupled_epochs_equal_host_epochs(case, monkeypatch):
+    """Decoupled device epochs (row-order predict, permutation into DDM order after the
+    window's shuffles, csrc/ctl.hip) forced on for every group: the same events, RNG
+    positions and refits as host epochs."""
+    from ddm_amd import devctl
+    monkeypatch.setattr(devctl, "DECOUPLE_ROWS", 0)
+    if case == "blocks":
+        parts = _parts((60_000,) * 4, 28, 20_011, 3)
+    elif case == "noise":
+        parts = _parts((30_000, 30_000), 27, 0, 7, flip=0.01, jitter=True)
+    else:
+        parts = _parts((24_037, 17_055, 4_321, 9_999), 27, 6_007, 9)
+    seeds = [200 + k for k in range(len(parts))]
+    dev_out, dev_rng, st = _run(parts, True, seeds)
+    host_out, host_rng, st_h = _run(parts, False, seeds)
+    assert st.device_epochs > 0 and st_h.device_epochs == 0
+    for k in range(len(parts)):
+        assert np.array_equal(dev_out[k], host_out[k]), k
+        assert np.array_equal(dev_rng[k][0], host_rng[k][0]) and dev_rng[k][1] == host_rng[k][1], k
+    assert st.refits == st_h.refits
+
+
 def test_device_epochs_vs_oracle():
     """Partitions with many refits, run with device epochs, == the oracle on each."""
     from oracle.controller import run_partition

@@ -5,7 +5,7 @@ import csv
 import statistics
 import sys
 
-KERNELS = ["k_cforest_predict_dev", "k_scan_fast", "k_scan_long", "k_pick_batch", "k_stage_ctl", "k_stage", "k_ctl",
+KERNELS = ["k_cforest_predict_dev", "k_err_permute", "k_scan_fast", "k_scan_long", "k_pick_batch", "k_stage_ctl", "k_stage", "k_ctl",
            "k_fsm_first_batch", "k_fsm_walk_batch", "k_fsm_replay_batch", "k_fsm_perms_batch", "k_dfit_prep",
            "k_dfit_trees", "k_dfit_pack"]
 
@@ -21,9 +21,9 @@ rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Time
 ev = [(short(r["Kernel_Name"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows]
 ev = [e for e in ev if e[0]]
 idx = [i for i, e in enumerate(ev) if e[0] == "k_cforest_predict_dev"]
-# epochs: a predict followed by a scan before the next predict (the bench's back-to-back
-# roofline replays of the predict are not epochs)
-idx = [a for a, b in zip(idx, idx[1:] + [len(ev)]) if any(n == "k_scan_fast" for n, _, _ in ev[a:b])]
+# epochs: a predict followed by a scan (k_scan_fast, or the fused k_stage_ctl that runs it)
+# before the next predict (the bench's back-to-back roofline replays are not epochs)
+idx = [a for a, b in zip(idx, idx[1:] + [len(ev)]) if any(n in ("k_scan_fast", "k_stage_ctl") for n, _, _ in ev[a:b])]
 lo, hi = len(idx) // 3, 2 * len(idx) // 3          # the middle third (steady epochs)
 spans = []
 for a, b in zip(idx[lo:hi], idx[lo + 1:hi + 1]):
