@@ -275,7 +275,12 @@ __device__ void dfit_boot(const Job& jb, int bblk) {
 }
 
 // ---- k_dfit_prep --------------------------------------------------------------------
+// The refit kernels are the epoch's critical path while the next windows' shuffles run on
+// the side stream on the same CUs: their waves take issue priority over the shuffles'.
+__device__ __forceinline__ void refit_priority() { __builtin_amdgcn_s_setprio(2); }
+
 __global__ __launch_bounds__(kPrepThreads) void k_dfit_prep(const Job* __restrict__ jobs) {
+    refit_priority();
     const Job jb = jobs[blockIdx.x];
     if (blockIdx.y > 0) {
         dfit_boot(jb, (int)blockIdx.y - 1);
@@ -761,6 +766,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfit_trees(const Job* __restric
     __shared__ float s_X[kTreeTile];
     __shared__ uint8_t s_ord[kTreeTile];
     __shared__ uint8_t s_yi[kMaxL];
+    refit_priority();
     const Job jb = jobs[blockIdx.y];
     const int w = threadIdx.x / 64, lane = threadIdx.x & 63;
     const int tree = blockIdx.x * kWaves + w;
@@ -1214,6 +1220,7 @@ __device__ void pack_tree(const TNode* tn, int m, int16_t* new_id, int16_t* queu
 }
 
 __global__ __launch_bounds__(kPackThreads) void k_dfit_pack(const Job* __restrict__ jobs) {
+    refit_priority();
     const Job jb = jobs[blockIdx.x];
 #ifdef DDM_DFIT_PROFILE
     const uint64_t t_pack0 = wall_clock64();
