@@ -730,7 +730,7 @@ bool cf_usable(const Seg& g, int pb) {
 // not compile, or needs more LDS than the launch has) sets stall[s]: the partition waits
 // for the host, which refits or walks it.
 constexpr size_t kDevLds = 80 * 1024;
-constexpr size_t kDevLdsRowOrder = 48 * 1024;
+constexpr size_t kDevLdsRowOrder = 24 * 1024;
 
 __device__ __forceinline__ int cf_rows_dev(const Seg& g, int pb) {
     if (g.cf_leaves > 0) return 1;
@@ -1070,9 +1070,11 @@ extern "C" int ddm_forest_predict_dev_orig(const ddm_predict_segment* segs_dev, 
         ddm::set_error("ddm_forest_predict_dev_orig: invalid argument");
         return DDM_E_ARG;
     }
-    // 48 KB of LDS per workgroup instead of 80: two predict workgroups per CU (their VGPR
-    // limit) leave 64 KB, so the window shuffles on the side stream find room beside them
-    // (a forest that needs more stalls its partition to the host, as any unusable forest)
+    // 24 KB of LDS per workgroup instead of 80 (a stump forest's tables, labels and errors
+    // take ~16 KB): the side stream's replay workgroups hold ~134 KB of a CU's 160 while they
+    // run, and a predict workgroup that does not fit waits for them (a 20 us gap per C3
+    // epoch at 48 KB).  A forest that needs more stalls its partition to the host, as any
+    // unusable forest, and the runner stops decoupling (ddm_amd/devctl.py).
     hipLaunchKernelGGL(k_cforest_predict_dev, dim3((unsigned)grid), dim3(kCfThreads), kDevLdsRowOrder,
                        ddm::as_hip(stream), reinterpret_cast<const Seg*>(segs_dev), res_dev, (int)n_segs,
                        (int)per_batch, stall, delta, (int)kDevLdsRowOrder);

@@ -71,6 +71,7 @@ class DeviceController:
         self.long_min_rows, self.long_cap_rows = int(long_min_rows), int(long_cap_rows)
         # row-order errors of decoupled epochs: a buffer shaped like the runner's err
         self.err_rows = torch.empty_like(r.err_all)
+        self.decouple_ok = True      # off after a decoupled predict found a forest it cannot take
         self.timers = []             # per-epoch HIP event pairs when the runner times kernels
         self.seg_log = None          # (segs, res) device copies per epoch when the runner logs predicts
         self._E = None
@@ -306,7 +307,7 @@ class DeviceController:
         """1 when the active partitions' windows ((win, max_win) pairs) average at least
         DECOUPLE_ROWS rows."""
         w = [min(int(a), int(b)) for a, b in wins]
-        if not w:
+        if not w or not self.decouple_ok:
             return 0
         return int(sum(w) * self.r.s.per_batch >= DECOUPLE_ROWS * len(w))
 
@@ -391,6 +392,9 @@ class DeviceController:
             st.refits += int(q["refits"]) - applied
             st.device_refits += int(q["refits"]) - applied
             stall = int(q["stall"])
+            if stall == kernels.CTL_STALL_REFIT and self._E is not None and self._E.decouple:
+                # the row-order predict's smaller LDS (csrc/forest_predict.hip) may be why
+                self.decouple_ok = False
             if stall == kernels.CTL_STALL_SCAN:
                 raise RuntimeError(f"ddm_scan_long gave up waiting for a carried state (partition {ps.i}): the "
                                    "epoch's results are void")
