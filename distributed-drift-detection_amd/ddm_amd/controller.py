@@ -771,8 +771,10 @@ class BatchRunner:
         ready.record(torch.cuda.current_stream(self.device))
         for s_ in (self.stream, self.gen_stream, self.tab_stream):
             s_.wait_event(ready)
+        for s_ in (self.stream, self.gen_stream, self.tab_stream):   # nothing of the last run
+            s_.synchronize()                                          # may still read the streams
         for ps, rng in zip(pss, rngs):
-            self.shuffles[ps.i].reset(rng)
+            self.shuffles[ps.i].reset(rng, synced=True)
         started = []
         try:
             # each partition's whole stream up front (one batched generate + tables);

@@ -156,21 +156,28 @@ class GpuShuffle:
         self.R, self.Tpre, self.Tchunk, self.cap = R, Tp, Tc, cap
         self.ptrs = (R.data_ptr(), Tp.data_ptr(), Tc.data_ptr())    # changes only here
 
-    def reset(self, rng):
-        """Draw 0 of the device stream = the next draw of `rng` (an MTStream)."""
+    def reset(self, rng, synced=False):
+        """Draw 0 of the device stream = the next draw of `rng` (an MTStream).  synced: the
+        caller has synchronised this stream's three HIP streams already (a runner resets all
+        its partitions after one synchronisation)."""
         self.init_key = rng.key.copy()
         self.init_pos = int(rng.pos.value)
-        st = np.empty(625, dtype=np.uint32)
+        if not synced:
+            self.stream.synchronize()
+            self.gen_stream.synchronize()       # nothing of the previous run may still read R
+            self.tab_stream.synchronize()
+        # the state goes up from a pinned buffer of this stream's own (asynchronous copy; the
+        # previous run's copy from it is done: gen_stream was synchronised)
+        if getattr(self, "_st_h", None) is None:
+            self._st_h = torch.empty(625, dtype=torch.int32, pin_memory=True)
+        st = self._st_h.numpy().view(np.uint32)
         st[:624] = self.init_key
         st[624] = self.init_pos
-        self.stream.synchronize()
-        self.gen_stream.synchronize()       # nothing of the previous run may still read R
-        self.tab_stream.synchronize()
         self.n_seg = self._segments_for(self.cap)
         with torch.cuda.stream(self.gen_stream):   # allocated, filled and read on gen_stream
             if getattr(self, "seg", None) is None or self.seg.shape[0] < self.n_seg:
                 self.seg = torch.zeros((self.n_seg, 640), dtype=torch.int32, device=self.device)
-            self.mt.copy_(torch.from_numpy(st.view(np.int32)))
+            self.mt.copy_(self._st_h, non_blocking=True)
             self.seg[0, :625].copy_(self.mt)
         self.jumped = 1                     # segments whose start state exists
         self._keep = []
