@@ -94,8 +94,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=SEED)
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-procs", type=int, default=16,
-                    help="CPU baseline worker processes (P); P x CORES = 32 = a 256-core node's share per GPU")
-    ap.add_argument("--cpu-cores", type=int, default=2, help="CPU baseline CORES = RF n_jobs per process")
+                    help="CPU baseline worker processes (P); P x CORES = 16 = the GPU box's CPU share per GPU")
+    ap.add_argument("--cpu-cores", type=int, default=1,
+                    help="CPU baseline CORES = RF n_jobs per process (> 1: joblib threading backend)")
     ap.add_argument("--cpu-sample-rows", type=int, default=90_000, help="rows per CPU baseline process")
     ap.add_argument("--oracle-check-rows", type=int, default=40_000,
                     help="rows of partition 0 re-run by the oracle after the timed region (0: off)")
@@ -103,6 +104,9 @@ def parse():
     ap.add_argument("--c4-len", type=int, default=4096)
     ap.add_argument("--c5-rows", type=int, default=64_000_000, help="c5 rows (all partitions)")
     ap.add_argument("--c5-flip", type=float, default=0.0, help="c5 label-noise rate")
+    ap.add_argument("--predict-replays", type=int, default=0,
+                    help="isolated back-to-back replays of the last timed step's predict tables (a side figure; "
+                         "0 for PMC runs, whose rows must be the steps' own)")
     ap.add_argument("--solo-world", type=int, default=0,
                     help="measurement aid: run only rank 0's partitions of an N-GPU job (d % N == 0), one "
                          "process, no collective (the per-GPU share of the strong-scaling workloads)")
@@ -203,7 +207,14 @@ def _cpu_worker(spec_cores):
     pdf, feats, seed = _cpu_frame(spec)
     np.random.seed(seed)
     t0 = time.perf_counter()
-    out = run_partition_frames(pdf, feats, n_jobs=cores)
+    if cores > 1:
+        # joblib's default (loky) backend is refused inside a multiprocessing worker (sklearn
+        # then silently runs n_jobs=1): threads make n_jobs=CORES real
+        from joblib import parallel_backend
+        with parallel_backend("threading", n_jobs=cores):
+            out = run_partition_frames(pdf, feats, n_jobs=cores)
+    else:
+        out = run_partition_frames(pdf, feats, n_jobs=cores)
     return len(pdf), int((out["change_flag_global"] >= 0).sum()), time.perf_counter() - t0
 
 
@@ -229,11 +240,14 @@ class CpuBaseline:
             avail = len(os.sched_getaffinity(0))
         except (AttributeError, OSError):
             avail = None
+        busy = sum(r[2] for r in res)
         return {"value": rows / wall, "unit": "rows/s", "cores": self.procs * self.cores, "kind": "port",
                 "procs": self.procs, "CORES": self.cores, "os_cpu_count": os.cpu_count(), "cpus_available": avail,
-                "node_estimate_rows_per_s": rows / wall * 8,
-                "node_note": "P x CORES = the per-GPU share of the node's cores (256 / 8 = 32 on an 8-GPU "
-                             "MI355X node); node_estimate = 8 such shares, assuming linear scaling over them",
+                "per_core_rows_per_s": rows / busy / self.cores if busy > 0 else None,
+                "cores_note": (f"{self.procs} worker processes x n_jobs={self.cores} "
+                               f"({'joblib threading backend' if self.cores > 1 else 'single-threaded sklearn'}) = "
+                               f"{self.procs * self.cores} cores used; the GPU box allots 16 CPUs per GPU, so no "
+                               f"whole-node (all {avail} CPUs) leg is run"),
                 "refits_per_s": refits / wall, "sample": f"{what}; {len(specs)} samples on {self.procs} processes x "
                                                          f"n_jobs={self.cores}, {rows} rows, {refits} drifts+refits, "
                                                          f"{wall:.1f} s wall (from the first dispatch to the last "
@@ -272,11 +286,31 @@ def events_digest(results):
     return h.hexdigest()
 
 
-def c3_property_check(results, n_rows, n_parts, block, pb=100):
+def c3_property_check(results, n_rows, n_parts, block, pb=100, seeds=None, rng_after=None):
     """configs[2] has noise-free separable classes: exactly one drift per class boundary,
     in the batch holding the boundary, and no warning.  Partition d row r is global row
-    r * n_parts + d; the first row of class block k in partition d is ceil((k*block - d) / n_parts)."""
+    r * n_parts + d; the first row of class block k in partition d is ceil((k*block - d) / n_parts).
+
+    With `seeds` ({partition: seed}) the exact drift ROW is pinned too: the DDM carried
+    through the old class's zero errors is trivial (p = s = p_min = s_min = 0), so the
+    reference reports the first new-class row of the boundary batch IN SHUFFLED ORDER
+    (DDM_Process.py:144-152); that order comes from replaying the partition's MT19937
+    draws (oracle/mt_replay.c: a permutation per batch, 100 seeds per refit after the
+    next batch's shuffle).  With `rng_after` ({partition: MTStream} after the run) the
+    generator position handed back must be the replay's as well."""
     import numpy as np
+    replays = {}
+    if seeds is not None:
+        # the replays (about 3 s of C per 125M-row partition) on threads, beside the checks
+        from concurrent.futures import ThreadPoolExecutor
+        from oracle.replay import mt_replay
+        pool = ThreadPoolExecutor(max(1, min(8, len(results))))
+        for d in results:
+            kmax = (n_rows * n_parts + d) // block
+            ch = [f // pb for f in ((k * block - d + n_parts - 1) // n_parts for k in range(1, kmax + 1))
+                  if pb <= f < n_rows]
+            replays[d] = pool.submit(mt_replay, seeds[d], n_rows, ch, ch, pb)
+        pool.shutdown(wait=False)
     for d, r in results.items():
         kmax = (n_rows * n_parts + d) // block
         firsts = [(k * block - d + n_parts - 1) // n_parts for k in range(1, kmax + 1)]
@@ -295,6 +329,25 @@ def c3_property_check(results, n_rows, n_parts, block, pb=100):
             c = r[f // pb - 1, 1]
             if not (f <= c < (f // pb + 1) * pb):
                 raise RuntimeError(f"partition {d}: drift row {c} before the boundary {f}")
+        if seeds is None:
+            continue
+        changes = [f // pb for f in firsts]
+        perms, key, pos = replays[d].result()
+        prev = 0
+        for f in firsts:
+            b = f // pb
+            if b - prev < 2:
+                raise RuntimeError(f"partition {d}: class blocks too short for the trivial-detector argument")
+            prev = b
+            rows = b * pb + perms[b]
+            exp = int(rows[np.argmax(rows >= f)])        # first new-class row in DDM order
+            if r[b - 1, 1] != exp:
+                raise RuntimeError(f"partition {d}: drift row {r[b - 1, 1]} in batch {b}, the first new-class row "
+                                   f"in shuffled order is {exp}")
+        if rng_after is not None:
+            g = rng_after[d]
+            if not (np.array_equal(g.key, key) and int(g.pos.value) == pos):
+                raise RuntimeError(f"partition {d}: RNG position after the run differs from the replay")
 
 
 def oracle_prefix_check(part, n, seed, got):
@@ -369,10 +422,14 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
                              refit=args.refit, timing=True, fit_threads=args.fit_threads)
     torch.cuda.synchronize()
 
+    rngs = {}
+
     def step():
-        outs = runner.run([MTStream.from_seed(seed_base + d) for d, _ in parts])
-        for (d, _), o in zip(parts, outs):
+        streams = [MTStream.from_seed(seed_base + d) for d, _ in parts]
+        outs = runner.run(streams)
+        for (d, _), o, g in zip(parts, outs, streams):
             results[d] = o
+            rngs[d] = g
         if getattr(runner, "trace", None) and os.environ.get("DDM_HOST_TRACE_OUT"):
             with open(os.environ["DDM_HOST_TRACE_OUT"], "w") as f:    # the last run's host phases
                 json.dump(runner.trace, f)
@@ -396,31 +453,31 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     # the timed steps enqueue no timing events; the kernel times come from one instrumented
     # step after them
     runner.set_kernel_timing(False)
+    # the predict launches of the timed steps are timed by HIP events on the epoch stream
+    # (a pair per device epoch, read after each run)
+    runner.set_predict_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         results.clear()
-        if k == args.steps - 1:
-            runner.predict_log = []           # the last timed step's predict tables (replay below)
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    runner.set_predict_timing(False)
     for g, r in results.items():          # every step reproduces the same events
         if args.warmup and not np.array_equal(r, ref_events[g]):
             raise RuntimeError(f"partition {g}: events differ between steps")
     st_timed = runner.stats
     runner.stats = RunStats()
     runner.set_kernel_timing(True)
-    log = runner.predict_log
-    runner.predict_log = None
+    runner.predict_log = [] if args.predict_replays else None   # its predict tables (the replays below)
     step()                                # instrumented, not timed
     st_kern = runner.stats
     runner.stats = st_timed
-    runner.predict_log = log
     for g, r in results.items():
         if not np.array_equal(r, ref_events.get(g, r)):
             raise RuntimeError(f"partition {g}: events differ in the instrumented step")
@@ -431,8 +488,9 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
         if fixture:
             checks["fixtures"] = fixture
     if kind == "c3":
-        c3_property_check(results, n, instances, block)
-        checks["property"] = "one drift per class boundary, in the batch holding it, no warning: ok"
+        c3_property_check(results, n, instances, block, seeds={d: seed_base + d for d, _ in parts}, rng_after=rngs)
+        checks["property"] = ("one drift per class boundary, in the batch holding it, at the first new-class row in "
+                              "shuffled order (oracle/mt_replay.c), no warning; RNG position == the replay: ok")
     if args.oracle_check_rows and rank == 0 and not fixture:
         d0, p0 = parts[0]
         k = oracle_prefix_check(p0, args.oracle_check_rows, seed_base + d0, results[d0])
@@ -443,7 +501,9 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
         checks["events_sha1"] = events_digest(all_events)
     st = runner.stats
     agg = {k: getattr(st, k) for k in ("epochs", "refits", "predicted_rows", "predict_bytes", "host_s", "gpu_s",
-                                       "device_refits", "prep_s", "device_epochs", "device_phases")}
+                                       "device_refits", "prep_s", "device_epochs", "device_phases", "permute_rows",
+                                       "device_rows", "predict_dev_ms", "predict_dev_launches",
+                                       "device_predict_bytes")}
     # kernel times of one step (the instrumented one), scaled to the timed steps
     for k in ("predict_ms", "scan_ms", "shuffle_ms", "dfit_ms"):
         agg[k] = getattr(st_kern, k) * args.steps
@@ -451,14 +511,26 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     drifts = int(sum((r[:, 1] >= 0).sum() for r in results.values()))
     warns = int(sum((r[:, 0] >= 0).sum() for r in results.values()))
     rows_rank = sum(p.n for _, p in parts) * args.steps
-    launches = max(1, agg["epochs"])
-    rows_per_launch = agg["predicted_rows"] / launches
-    avg_ms_step = agg["predict_ms"] / launches
-    replay_ms, replay_n = runner.replay_predict(repeats=2)
+    if agg["predict_dev_launches"]:
+        launches = agg["predict_dev_launches"]
+        rows_per_launch = agg["device_rows"] / launches
+        avg_ms_step = agg["predict_dev_ms"] / launches
+        dev_bytes = agg["device_predict_bytes"]
+    else:       # host-planned epochs only (DDM_DEVICE_CTL=0, host refits): the instrumented step's
+        launches = max(1, agg["epochs"])
+        rows_per_launch = agg["predicted_rows"] / launches
+        avg_ms_step = agg["predict_ms"] / launches
+        dev_bytes = agg["predict_bytes"]
+    replay_ms, replay_n = runner.replay_predict(repeats=args.predict_replays) if args.predict_replays else (0.0, 0)
     runner.predict_log = None
     runner.close()
-    avg_ms = replay_ms if replay_n else avg_ms_step
-    achieved = (agg["predict_bytes"] / launches) / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    # headline: the in-step launches (HIP events around each predict of the instrumented
+    # step, the side stream's shuffles co-running as in the timed steps); the isolated
+    # back-to-back replays of the same tables are a side figure
+    avg_ms = avg_ms_step
+    bytes_launch = dev_bytes / launches
+    achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    replay_gbs = bytes_launch / (replay_ms * 1e-3) / 1e9 if replay_n and replay_ms > 0 else None
     if kind == "c2":
         wl = (f"configs[1]: outdoorStream.csv (the reference's file, 4000 x 21) x MULT={args.c2_mult} "
               f"({OUTDOOR_ROWS * args.c2_mult} rows; concat, shuffle with data seed {C2_DATA_SEED}, stable sort by "
@@ -488,7 +560,10 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
              "device_phases_per_step": agg["device_phases"] / args.steps,
              "refits_per_s": agg["refits"] / elapsed,
              "speculation_overhead": agg["predicted_rows"] / max(1, rows_rank),
-             "predict_kernel_ms_per_step": agg["predict_ms"] / args.steps,
+             "device_predicted_rows_per_step": agg["device_rows"] / args.steps,
+             "permute_rows_per_step": agg["permute_rows"] / args.steps,
+             "predict_kernel_ms_per_step": agg["predict_dev_ms"] / args.steps if agg["predict_dev_launches"] else
+             agg["predict_ms"] / args.steps,
              "scan_kernel_ms_per_step": agg["scan_ms"] / args.steps,
              "shuffle_kernels_ms_per_step": agg["shuffle_ms"] / args.steps,
              "device_refit_kernels_ms_per_step": agg["dfit_ms"] / args.steps,
@@ -499,13 +574,30 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
              "gather_backend": (None if world == 1 else "rccl (ctypes ncclAllGather, HBM to HBM)" if args.comm
                                 else "torch.distributed all_gather"),
              "checks": checks}
+    dec_frac = agg["permute_rows"] / max(1, agg["device_rows"])
+    kname = "k_cforest_predict_dev" if dec_frac < 0.5 else "k_cforest_predict_dev (row order)"
+    tkey = "ddm_forest_predict_dev_rows" if dec_frac >= 0.5 else "ddm_forest_predict_dev"
     roofline = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_from_profile("ddm_forest_predict", rows_per_launch),
-                "kernel": "ddm_forest_predict", "alg_bytes_per_row": "4*F_used + 6",
-                "avg_launch_ms": avg_ms, "avg_rows_per_launch": rows_per_launch,
-                "avg_launch_ms_in_step": avg_ms_step,
-                "launch_timing": f"HIP events on the epoch stream around {replay_n} back-to-back launches of the last "
-                                 "timed step's predict segment tables (2 passes)"}
+                "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_from_profile(tkey, rows_per_launch),
+                "traffic_key": tkey, "kernel": kname,
+                "alg_bytes_per_row": "4*F_used + 4 (label) + 1 (error written) + 1 (permutation read, coupled epochs "
+                                     "only; decoupled epochs leave the permutation to k_err_permute)",
+                "alg_bytes_per_launch": bytes_launch, "avg_launch_ms": avg_ms, "avg_rows_per_launch": rows_per_launch,
+                "launches": agg["predict_dev_launches"], "decoupled_row_fraction": dec_frac,
+                "launch_timing": "HIP events on the epoch stream around every device-epoch predict launch of the timed "
+                                 "steps (launches with no rows -- epochs enqueued after a run's last active one -- "
+                                 "included, as in a rocprofv3 average; the run's first, host-planned epoch is a "
+                                 "different kernel and excluded)",
+                "isolated_replay": {"avg_launch_ms": replay_ms if replay_n else None, "launches": replay_n,
+                                    "achieved": replay_gbs,
+                                    "frac": replay_gbs / PEAK_HBM_GBS if replay_gbs else None,
+                                    "note": "the last timed step's segment tables replayed back to back in coupled "
+                                            "form (permutation read in the predict), nothing co-running"},
+                "k_err_permute": {"rows_per_step": agg["permute_rows"] / args.steps,
+                                  "alg_bytes_per_row": "1 (error-free batches before the first error's batch: "
+                                                       "zero-fill) to 3 (row-order error read, permutation read, "
+                                                       "DDM-order error write)",
+                                  "traffic": traffic_from_profile("ddm_err_permute", 1.0)}}
     cpu_res = None
     if cpu is not None:
         if kind == "c2":

@@ -87,6 +87,12 @@ extern "C" int ddm_ctl_enter(const ddm_ctl_epoch* e) {
         ddm::set_error("ddm_ctl_enter: invalid argument");
         return DDM_E_ARG;
     }
+    // ctl_split gives every non-empty window at least one block of the fixed predict grid:
+    // more partitions than blocks would leave windows past the grid unpredicted
+    if (e->ctl.n > e->ctl.predict_blocks) {
+        ddm::set_error("ddm_ctl_enter: more partitions than predict blocks");
+        return DDM_E_ARG;
+    }
     hipStream_t s = ddm::as_hip(e->stream);
     if (e->long_max_rows > 0) {                     // zeroed once; every epoch's call leaves it zeroed
         const int64_t lb = ddm_scan_long_scratch_bytes(e->ctl.n, e->long_max_rows, e->per_batch);
@@ -118,7 +124,9 @@ extern "C" int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs) {
     for (int32_t k = 0; k < n_epochs; ++k) {
         if (!dec)
             if (int rc = join()) return rc;         // the last epoch's shuffles of this window
-        if (int rc = rec(e->ev[0], s)) return rc;
+        const ddm_event_t pb0 = e->predict_evs ? e->predict_evs[2 * k] : e->ev[0];
+        const ddm_event_t pb1 = e->predict_evs ? e->predict_evs[2 * k + 1] : e->ev[1];
+        if (int rc = rec(pb0, s)) return rc;
         if (dec) {
             if (int rc = ddm_forest_predict_dev_orig(c.segs, c.seg_res, c.n, e->per_batch, c.predict_blocks, c.pstall,
                                                      e->row_order_delta, e->stream))
@@ -128,7 +136,7 @@ extern "C" int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs) {
                                                 e->stream, nullptr, nullptr))
                 return rc;
         }
-        if (int rc = rec(e->ev[1], s)) return rc;
+        if (int rc = rec(pb1, s)) return rc;
         if (dec)
             if (int rc = join()) return rc;
         if (int rc = rec(e->ev[2], s)) return rc;
@@ -154,7 +162,9 @@ extern "C" int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs) {
         if (c.sync) {                               // scan + pick + staging + decisions: one launch
             if (int rc = rec(e->ev[3], s)) return rc;
             if (int rc = rec(e->ev[4], s)) return rc;
-            if (int rc = ddm_epoch_stage_ctl(c.stage, c.jobs, &c, e->err, e->params, e->perm_map, e->stream))
+            ddm_ctl cd = c;
+            cd.decoupled = dec ? 1 : 0;
+            if (int rc = ddm_epoch_stage_ctl(c.stage, c.jobs, &cd, e->err, e->params, e->perm_map, e->stream))
                 return rc;
         } else {
             if (int rc = ddm_shuffle_pick_batch(c.jobs, c.n, e->stream)) return rc;

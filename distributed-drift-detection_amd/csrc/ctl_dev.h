@@ -196,7 +196,11 @@ __device__ void commit(const ddm_ctl& c, ddm_ctl_part& p, int i) {
     p.predicted_rows += rows;
     int64_t slots = p.host_slots;
     if (p.forest_dev && p.res) slots = p.res[DDM_DFIT_CF_SLOTS];
-    p.predict_bytes += rows * (4 * slots + 6);
+    // algorithmic bytes of the predict kernel: the referenced feature columns and the label,
+    // the error byte written, and (coupled epochs) the in-batch permutation byte read; a
+    // decoupled epoch's permutation into DDM order is k_err_permute's (counted by its rows)
+    p.predict_bytes += rows * (4 * slots + (c.decoupled ? 5 : 6));
+    if (c.decoupled) p.permute_rows += rows;
     if (stop == DDM_STOP_FAILED) {
         p.stall = DDM_CTL_STALL_SCAN;
         return;

@@ -160,12 +160,14 @@ def sklearn_refit(settings):
 class RunStats:
     __slots__ = ("epochs", "refits", "predicted_rows", "refit_s", "gpu_s", "host_s", "predict_ms", "predict_bytes",
                  "scan_ms", "scan_rows", "shuffle_ms", "sklearn_refits", "refit_fit_s", "refit_readback_s",
-                 "prep_s", "dfit_ms", "device_refits", "long_scans", "preshuffled", "device_epochs", "device_phases")
+                 "prep_s", "dfit_ms", "device_refits", "long_scans", "preshuffled", "device_epochs", "device_phases",
+                 "permute_rows", "device_rows", "predict_dev_ms", "predict_dev_launches", "device_predict_bytes")
 
     def __init__(self):
         self.epochs = self.refits = self.predicted_rows = self.predict_bytes = self.scan_rows = 0
         self.sklearn_refits = self.device_refits = self.long_scans = self.preshuffled = 0
-        self.device_epochs = self.device_phases = 0
+        self.device_epochs = self.device_phases = self.permute_rows = self.device_rows = 0
+        self.predict_dev_ms, self.predict_dev_launches, self.device_predict_bytes = 0.0, 0, 0
         self.refit_s = self.gpu_s = self.host_s = self.predict_ms = self.scan_ms = self.shuffle_ms = 0.0
         self.refit_fit_s = self.refit_readback_s = self.prep_s = self.dfit_ms = 0.0
 
@@ -936,6 +938,19 @@ class BatchRunner:
             self._E.ev[2 * k] = t.ev[0].value if t is not None else None
             self._E.ev[2 * k + 1] = t.ev[1].value if t is not None else None
 
+    def set_predict_timing(self, on):
+        """HIP events around every device-epoch predict launch (devctl.PredictTimer), read
+        after each run into stats.predict_dev_ms / predict_dev_launches: the bench's
+        in-step predict timing inside its timed region."""
+        if self.devctl is None:
+            return
+        if on and self.devctl.pred_timer is None:
+            from .devctl import PredictTimer
+            self.devctl.pred_timer = PredictTimer()
+        elif not on and self.devctl.pred_timer is not None:
+            self.devctl.pred_timer.close()
+            self.devctl.pred_timer = None
+
     def _next_bound(self, ps):
         """The largest window the epoch after this one can give partition ps (the policy of
         _epoch_after: 9/8 of the concept just closed after a change, twice the window
@@ -1348,6 +1363,10 @@ class GroupedRunner:
     def set_kernel_timing(self, on):
         for r in self.runners:
             r.set_kernel_timing(on)
+
+    def set_predict_timing(self, on):
+        for r in self.runners:
+            r.set_predict_timing(on)
 
     @stats.setter
     def stats(self, value):

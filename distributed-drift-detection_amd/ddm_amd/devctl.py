@@ -43,6 +43,57 @@ GROUP = 4                       # epochs per enqueued group
 DECOUPLE_ROWS = 200_000
 
 
+class PredictTimer:
+    """HIP timing events around every device-epoch predict launch of the timed runs (passed
+    to ddm_ctl_epochs as predict_evs, a fresh pair per epoch of a group), harvested once
+    their group has completed: the launches, their summed duration and the launches that
+    had rows (the trailing epochs of a phase, enqueued before the host saw every partition
+    done, predict nothing)."""
+
+    def __init__(self):
+        self.free = []
+        self.inflight = []           # (group index, ctypes array of 2*GROUP events)
+        self.ms = 0.0
+        self.launches = 0
+
+    def arm(self, n, group):
+        evs = (ctypes.c_void_p * (2 * n))()
+        for k in range(2 * n):
+            if self.free:
+                evs[k] = self.free.pop()
+            else:
+                e = ctypes.c_void_p()
+                check(lib.ddm_event_create(ctypes.byref(e)), "ddm_event_create")
+                evs[k] = e.value
+        self.inflight.append((group, evs))
+        return ctypes.cast(evs, ctypes.c_void_p)
+
+    def harvest(self, upto=None):
+        """Read (and recycle) the pairs of every group <= upto (None: all, after a sync)."""
+        ms = ctypes.c_float()
+        keep = []
+        for g, evs in self.inflight:
+            if upto is not None and g > upto:
+                keep.append((g, evs))
+                continue
+            for k in range(0, len(evs), 2):
+                check(lib.ddm_event_elapsed_ms(evs[k], evs[k + 1], ctypes.byref(ms)), "ddm_event_elapsed_ms")
+                self.ms += ms.value
+                self.launches += 1
+            self.free.extend(evs)
+        self.inflight = keep
+
+    def take(self):
+        out = (self.ms, self.launches)
+        self.ms, self.launches = 0.0, 0
+        return out
+
+    def close(self):
+        for e in self.free:
+            lib.ddm_event_destroy(e)
+        self.free = []
+
+
 class DeviceController:
     """The device-mode state of one BatchRunner (its buffers never move)."""
 
@@ -74,13 +125,14 @@ class DeviceController:
         self.decouple_ok = True      # off after a decoupled predict found a forest it cannot take
         self.timers = []             # per-epoch HIP event pairs when the runner times kernels
         self.seg_log = None          # (segs, res) device copies per epoch when the runner logs predicts
+        self.pred_timer = None       # a PredictTimer while the runner times the predict launches
         self._E = None
 
     # ---------------------------------------------------------------- eligibility
     def eligible(self, live):
         """Device epochs need device refits, compiled forests and no host-staged refit."""
         r = self.r
-        if not r.dfit_rows:
+        if not r.dfit_rows or self.n > PREDICT_BLOCKS:    # a predict block per window at least
             return False
         for ps in live:
             if ps.retrain:
@@ -131,7 +183,7 @@ class DeviceController:
     def _write_records(self, live):
         """The records of every partition (static templates + the host state of the live ones)."""
         r = self.r
-        t = r._stream_ptrs(live)
+        r._stream_ptrs(live)             # refreshes the R / table pointers of regrown stream buffers
         t = r._templates()
         pb, T = r.s.per_batch, r.s.n_estimators
         rec = self.rec
@@ -260,14 +312,18 @@ class DeviceController:
         r._mark("device phase entered")
         timing = r.t_pred is not None
         logging = r.predict_log is not None
-        pending, slot, epochs = None, 0, 0
+        pending, slot, epochs, group = None, 0, 0, 0
+        pt = self.pred_timer
         while True:
             if timing or logging:
                 for _ in range(GROUP):
                     self._one_epoch_instrumented(E, timing, logging)
             else:
+                E.predict_evs = pt.arm(GROUP, group) if pt is not None else None
                 check(lib.ddm_ctl_epochs(ctypes.byref(E), GROUP), "ddm_ctl_epochs")
+                E.predict_evs = None
             epochs += GROUP
+            group += 1
             with torch.cuda.stream(stream):
                 self.poll_h[slot].copy_(self.parts_d, non_blocking=True)
             ev = torch.cuda.Event()
@@ -275,6 +331,8 @@ class DeviceController:
             if pending is not None:
                 pev, pslot = pending
                 pev.synchronize()
+                if pt is not None:
+                    pt.harvest(upto=group - 2)     # every group up to the polled one is complete
                 rec = self.poll_h[pslot].numpy().view(CTL)
                 active = (rec["done"] == 0) & (rec["stall"] == 0) & (rec["park"] == 0)
                 if not active.any() or (rec["stall"] != 0).any():
@@ -291,6 +349,11 @@ class DeviceController:
         r._mark(f"device loop done ({epochs} epochs enqueued)")
         stream.synchronize()
         r.side_stream.synchronize()
+        if pt is not None:
+            pt.harvest()
+            ms, n = pt.take()
+            st.predict_dev_ms += ms
+            st.predict_dev_launches += n
         r._mark("device epochs drained")
         st.gpu_s += time.perf_counter() - t0
         if timing:
@@ -387,8 +450,11 @@ class DeviceController:
             if applied:
                 q["retrain"] = 1
             st.predicted_rows += int(q["predicted_rows"])
+            st.device_rows += int(q["predicted_rows"])
             st.long_scans += int(q["long_scans"])
             st.predict_bytes += int(q["predict_bytes"])
+            st.device_predict_bytes += int(q["predict_bytes"])
+            st.permute_rows += int(q["permute_rows"])
             st.refits += int(q["refits"]) - applied
             st.device_refits += int(q["refits"]) - applied
             stall = int(q["stall"])

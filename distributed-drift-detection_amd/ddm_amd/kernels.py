@@ -57,7 +57,8 @@ CTL_PART_DTYPE = np.dtype([("job", JOB_DTYPE), ("seg", SEG_DTYPE), ("stage", STA
                            ("pad1", "<i4"), ("g0", "<i8"), ("b_end", "<i8"), ("Wg", "<i8"),
                            ("P_after_first", "<i8"), ("p0", "<i8"), ("p1", "<i8"), ("state", STATE_DTYPE),
                            ("n_log", "<i8"), ("predicted_rows", "<i8"), ("predict_bytes", "<i8"), ("epochs", "<i8"),
-                           ("refits", "<i8"), ("log_mark", "<i8"), ("long_scans", "<i8")])
+                           ("refits", "<i8"), ("log_mark", "<i8"), ("long_scans", "<i8"),
+                           ("permute_rows", "<i8"), ("pad2", "<i8")])
 CTL_STALL_REFIT, CTL_STALL_WORDS, CTL_STALL_SCAN = 1, 2, 3
 
 

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 19
+#define DDM_AMD_ABI_VERSION 20
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
@@ -603,6 +603,9 @@ typedef struct ddm_ctl_part {
     int64_t n_log, predicted_rows, predict_bytes, epochs, refits;
     int64_t log_mark;            /* n_log before this epoch's scans: restored when the epoch stalls */
     int64_t long_scans;          /* windows that ran on ddm_scan_long (statistics) */
+    int64_t permute_rows;        /* ABI 20: rows of decoupled epochs (row-order predict +
+                                    k_err_permute into DDM order; statistics) */
+    int64_t pad2;
 } ddm_ctl_part;
 
 /* Stall reasons (ddm_ctl_part.stall) */
@@ -622,6 +625,9 @@ typedef struct ddm_ctl {
     uint32_t* sync;                                /* NULL or uint32[2], zeroed: [0] the fused
                                                       staging's block ticket (left 0), [1] set
                                                       when the next epoch has a long window    */
+    int32_t decoupled, pad_c;                      /* ABI 20: set by ddm_ctl_epochs for the
+                                                      decisions kernel: this epoch's predict
+                                                      wrote row-order errors (statistics)      */
 } ddm_ctl;
 
 typedef struct ddm_ctl_epoch {
@@ -643,6 +649,10 @@ typedef struct ddm_ctl_epoch {
                                                       there without waiting for the window's
                                                       shuffles, which are waited for only by
                                                       the permutation into err (DDM order)     */
+    const ddm_event_t* predict_evs;                /* ABI 20: NULL or [2 * n_epochs] timing
+                                                      events recorded right before / after each
+                                                      epoch's predict launch (ev[0] / ev[1] are
+                                                      used when NULL)                          */
 } ddm_ctl_epoch;
 int64_t ddm_ctl_part_bytes(void);
 int64_t ddm_ctl_epoch_bytes(void);

@@ -14,6 +14,8 @@ Contents, each citing the reference lines it restates:
   controller.py  run_DDM_loop restated (DDM_Process.py:170-213): batching, shuffle,
                  lazy refit, refit-on-drift, global MT19937 consumption order
   ddm_scan.c     the same DDM scan in plain C (fast enough for C4-sized parity tests)
+  mt_replay.c    the global MT19937 consumption of run_DDM_loop replayed from the seed and
+                 the change batches (replay.py: shuffled orders and the final RNG position)
 
 Pinning: tests/golden/ holds outputs of the reference's own function bodies
 (DDM_Process.py:94-213, exec'd by tests/golden/make_golden.py) and the tests in

@@ -67,6 +67,76 @@ def run_partition(X, y, local_labels, global_labels, n_jobs=1, per_batch=PER_BAT
     return out
 
 
+def run_partition_chunked(X, y, local_labels, global_labels, n_jobs=1, per_batch=PER_BATCH,
+                          ddm_params=(MIN_NUM_DDM_VALS, WARNING_LEVEL, CHANGE_LEVEL), max_chunk=4096):
+    """`run_partition` with the classifier called on many batches at once: the same events
+    and the same global RNG consumption, fast enough for partitions of millions of rows.
+
+    Between two refits nothing the reference draws depends on the rows, so the shuffles of
+    the next K batches are drawn in order (DDM_Process.py:190; the pending refit's 100 draws
+    right after the first of them, :194-196) and one `predict` covers their rows
+    (predict_rf is row-wise, :110-128).  The DDM then runs batch by batch (:202); at a change
+    in batch c (:207-210) the generator goes back to the state right after batch c+1's
+    shuffle, which the reference draws before the refit on batch c.  K doubles from 16 while
+    no change occurs (at most max_chunk) and restarts at 16 after one."""
+    n = len(y)
+    starts = list(range(0, n, per_batch))
+    nb = len(starts)
+    if nb < 2:
+        raise ValueError("No objects to concatenate")
+    y = np.asarray(y)
+
+    def rows_of(b):
+        lo = starts[b]
+        return lo + np.random.permutation(min(n, lo + per_batch) - lo)
+
+    train_rows = rows_of(0)
+    ddm, rf, retrain = None, None, True
+    out = np.empty((nb - 1, 4), dtype=np.int64)
+    b, K = 1, 16
+    pending = None            # batch b's rows, already drawn (the batch after a change)
+    while b < nb:
+        K = min(K, nb - b)
+        rows_l, states = [], []
+        for k in range(K):
+            if k == 0 and pending is not None:
+                rows = pending
+            else:
+                rows = rows_of(b + k)
+            if k == 0 and retrain:
+                rf = _fit(X[train_rows], y[train_rows], n_jobs)
+                retrain = False
+            rows_l.append(rows)
+            states.append(np.random.get_state())
+        pending = None
+        allrows = np.concatenate(rows_l)
+        err_all = (rf.predict(X[allrows]) != y[allrows]).astype(np.int64)
+        at, changed = 0, False
+        for k in range(K):
+            rows = rows_l[k]
+            err = err_all[at:at + len(rows)]
+            at += len(rows)
+            if ddm is None:
+                ddm = OracleDDM(*ddm_params)
+            w, c = scan_batch(err, ddm)
+            out[b + k - 1] = (local_labels[rows[w]] if w >= 0 else -1, global_labels[rows[w]] if w >= 0 else -1,
+                              local_labels[rows[c]] if c >= 0 else -1, global_labels[rows[c]] if c >= 0 else -1)
+            if c >= 0:
+                train_rows, ddm, retrain = rows, None, True
+                if k + 1 < K:                   # batch b+k+1 was drawn: keep it, undo the rest
+                    np.random.set_state(states[k + 1])
+                    pending = rows_l[k + 1]
+                b += k + 1
+                changed = True
+                break
+        if changed:
+            K = 16
+        else:
+            b += K
+            K = min(2 * K, max_chunk)
+    return out
+
+
 def run_partition_frames(pdf, x_features, n_jobs=1, per_batch=PER_BATCH):
     """Same semantics on pandas frames with the reference's per-batch frame building and
     `iterrows` DDM feed (its CPU cost profile).  Returns the reference's output frame."""

@@ -5,8 +5,11 @@
                  reference's own outputs by tests/test_oracle.py);
   configs[4] C5  short class blocks -> a refit every one or two batches: hundreds of
                  refits per partition, every event and the RNG position == the oracle;
-  configs[2] C3  full-size property (one drift per class boundary, in the batch holding
-                 it, no warning) on the BatchRunner path the bench times;
+  configs[2] C3  partition 0 through two class boundaries (2.6M rows) == the oracle
+                 controller, every column and the RNG position; and the full 8 x 125M-row
+                 configuration on the BatchRunner path the bench times: one drift per class
+                 boundary at the first new-class row in shuffled order (the MT19937 draws
+                 replayed by oracle/mt_replay.c), no warning, RNG positions == the replay;
   device generators == their host mirror (oracle/synth.py).
 """
 import numpy as np
@@ -86,25 +89,68 @@ def test_c5_refit_heavy_vs_oracle(flip, parts_run, groups):
     assert runner.stats.device_refits >= 100
 
 
-def test_c3_full_size_property_on_bench_path():
-    """configs[2] at 8 x 12.5M rows (global class blocks of 1,000,037 rows), through the
-    GroupedRunner the bench times: exactly one drift per class boundary, in the batch holding
-    it, no warning."""
+def test_c3_partition0_through_class_boundaries_vs_oracle():
+    """configs[2]'s partition 0 exactly as bench.py builds it (block_partition of the 1B-row
+    stream: 27 features, class blocks of 10,000,037 global rows, row % 8), its first
+    2.6M rows -- two class boundaries (partition rows 1,250,005 and 2,500,010), so two
+    drifts, two device refits and a predict with a device-trained forest -- through the
+    BatchRunner the bench times, against the oracle controller (run_partition_chunked,
+    pinned to run_partition and the reference fixtures by tests/test_oracle.py): all four
+    event columns (global row = partition row * 8 + 0) and the RNG position."""
     import bench
     from ddm_amd import synth
-    from ddm_amd.controller import GroupedRunner
+    from ddm_amd.controller import BatchRunner
+    from ddm_amd.params import DDMSettings
+    from ddm_amd.rng import MTStream
+    from oracle.controller import run_partition_chunked
+    dev = _dev()
+    n, d, P = 2_600_000, 0, bench.C3_PARTS
+    part = synth.block_partition(n, d, P, bench.C3_BLOCK, bench.SEED, dev)
+    X, y = synth.host_copy(part)
+    runner = BatchRunner([part], DDMSettings(), torch.cuda.Stream(dev, priority=-1), timing=True, fit_threads=16)
+    rng = MTStream.from_seed(bench.SEED + d)
+    got = runner.run([rng])[0]
+    runner.close()
+    np.random.seed(bench.SEED + d)
+    want = run_partition_chunked(X, y, np.arange(n), np.arange(n) * P + d)
+    after = np.random.get_state()
+    ev = bench.events_rows(got)
+    ev[:, 1] = np.where(ev[:, 1] >= 0, ev[:, 1] * P + d, -1)
+    ev[:, 3] = np.where(ev[:, 3] >= 0, ev[:, 3] * P + d, -1)
+    assert np.array_equal(ev, want)
+    assert np.array_equal(rng.key, after[1]) and rng.pos.value == after[2]
+    chg = np.nonzero(want[:, 2] >= 0)[0]
+    assert len(chg) == 2 and list(chg + 1) == [12_500, 25_000], chg
+    assert (want[:, 0] < 0).all()
+    del part
+    torch.cuda.empty_cache()
+
+
+def test_c3_full_size_property_on_bench_path():
+    """configs[2] at its full size -- 8 partitions x 125M rows of the 1B-row stream, global
+    class blocks of 10,000,037 rows -- through the BatchRunner exactly as bench.py runs it:
+    one drift per class boundary, in the batch holding it, AT the first new-class row of
+    that batch in shuffled order (the MT19937 draws replayed by oracle/mt_replay.c), no
+    warning, and every partition's RNG position == the replay's."""
+    import bench
+    from ddm_amd import synth
+    from ddm_amd.controller import BatchRunner
     from ddm_amd.params import DDMSettings
     from ddm_amd.rng import MTStream
     dev = _dev()
-    n, P, block = 12_500_000, 8, 1_000_037
-    parts = [synth.block_partition(n, d, P, block, 20261015, dev) for d in range(P)]
-    runner = GroupedRunner(parts, DDMSettings(), groups=1, timing=True, fit_threads=16)   # as bench.py runs it
-    outs = runner.run([MTStream.from_seed(20261015 + d) for d in range(P)])
+    n, P, block = 125_000_000, bench.C3_PARTS, bench.C3_BLOCK
+    parts = [synth.block_partition(n, d, P, block, bench.SEED, dev) for d in range(P)]
+    runner = BatchRunner(parts, DDMSettings(), torch.cuda.Stream(dev, priority=-1), timing=True, fit_threads=16)
+    rngs = [MTStream.from_seed(bench.SEED + d) for d in range(P)]
+    outs = runner.run(rngs)
     runner.close()
     res = dict(enumerate(outs))
-    bench.c3_property_check(res, n, P, block)
-    assert sum(int((r[:, 1] >= 0).sum()) for r in outs) == sum(
+    bench.c3_property_check(res, n, P, block, seeds={d: bench.SEED + d for d in range(P)},
+                            rng_after=dict(enumerate(rngs)))
+    n_drifts = sum(int((r[:, 1] >= 0).sum()) for r in outs)
+    assert n_drifts == sum(
         len([k for k in range(1, (n * P + d) // block + 1) if 100 <= (k * block - d + P - 1) // P < n])
         for d in range(P))
+    assert n_drifts == 792
     del parts
     torch.cuda.empty_cache()

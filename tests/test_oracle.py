@@ -141,3 +141,85 @@ def test_c_oracle_equals_python_oracle(oracle_lib):
             np.testing.assert_array_equal(ps[off[i]:off[i + 1]], pps)
             assert st[i, 0] == pddm.miss_prob and st[i, 5] == pddm.sample_count
             base += nb
+
+
+@pytest.mark.parametrize("mult,inst", [(2, 1), (4, 4), (1, 16)])
+def test_chunked_oracle_matches_reference(mult, inst):
+    """run_partition_chunked (many batches per predict, RNG rolled back after a change) ==
+    the reference-executed fixtures, and leaves the global RNG where run_partition does."""
+    from oracle.controller import run_partition_chunked
+    for d, part, expect in golden_partitions(mult, inst):
+        X = part[[str(i) for i in range(21)]].to_numpy()
+        args = (X, part["target"].to_numpy(), part.index.to_numpy(), part["full_df_row_number"].to_numpy())
+        np.random.seed(1000 + d)
+        got = run_partition_chunked(*args)
+        after = np.random.get_state()
+        assert np.array_equal(got, expect), (mult, inst, d)
+        np.random.seed(1000 + d)
+        run_partition(*args)
+        ref = np.random.get_state()
+        assert np.array_equal(after[1], ref[1]) and after[2] == ref[2]
+
+
+def test_chunked_oracle_long_concepts_with_noise():
+    """Long concepts (the chunk doubles to its cap) with sparse label noise (changes
+    anywhere in a chunk, including its last batch): == run_partition, RNG position too."""
+    from oracle.controller import run_partition_chunked
+    from oracle import synth
+    n = 60_000
+    y = synth.block_labels(n, 0, 8, 80_037, 10)
+    rs = np.random.RandomState(11)
+    flip = rs.rand(n) < 0.0007
+    y = np.where(flip, (y + 3) % 10, y)
+    X = synth.features(y, 0, 8, 5, 6).astype(np.float64)
+    lab, glob = np.arange(n), np.arange(n) * 8
+    np.random.seed(31)
+    want = run_partition(X, y, lab, glob)
+    st = np.random.get_state()
+    np.random.seed(31)
+    got = run_partition_chunked(X, y, lab, glob, max_chunk=64)
+    st2 = np.random.get_state()
+    assert np.array_equal(got, want)
+    assert (want[:, 2] >= 0).sum() >= 8
+    assert np.array_equal(st[1], st2[1]) and st[2] == st2[2]
+
+
+def test_mt_replay_matches_numpy():
+    """oracle/mt_replay.c: permutations and the generator state after a partition's
+    draws (one permutation per batch, 100 randint(2**31-1) per refit) == numpy's."""
+    from oracle.replay import mt_replay
+    rs = np.random.RandomState(4)
+    for n_rows, per_batch in ((1234, 100), (5000, 100), (777, 37), (256 * 9, 256)):
+        nb = (n_rows + per_batch - 1) // per_batch
+        changes = sorted(set(rs.randint(1, nb, size=nb // 3).tolist()))
+        want = sorted(set([0, nb - 1] + rs.randint(0, nb, size=5).tolist()))
+        perms, key, pos = mt_replay(2024 + n_rows, n_rows, changes, want, per_batch=per_batch)
+        g = np.random.RandomState(2024 + n_rows)
+        retrain = True
+        for b in range(nb):
+            p = g.permutation(min(per_batch, n_rows - b * per_batch))
+            if b in perms:
+                assert np.array_equal(perms[b], p), (n_rows, b)
+            if b == 0:
+                continue
+            if retrain:
+                g.randint(2 ** 31 - 1, size=100)
+                retrain = False
+            if b in changes:
+                retrain = True
+        st = g.get_state()
+        assert np.array_equal(key, st[1]) and pos == st[2]
+
+
+def test_mt_replay_matches_oracle_controller_rng():
+    """Fed the changes the oracle controller found, the replay ends at the controller's RNG
+    position (sklearn's own draws included)."""
+    from oracle.replay import mt_replay
+    for d, part, expect in golden_partitions(2, 4):
+        X = part[[str(i) for i in range(21)]].to_numpy()
+        np.random.seed(1000 + d)
+        run_partition(X, part["target"].to_numpy(), part.index.to_numpy(), part["full_df_row_number"].to_numpy())
+        st = np.random.get_state()
+        changes = [k + 1 for k in np.nonzero(expect[:, 2] >= 0)[0]]
+        _, key, pos = mt_replay(1000 + d, len(part), changes)
+        assert np.array_equal(key, st[1]) and pos == st[2], d
