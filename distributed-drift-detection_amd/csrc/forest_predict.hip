@@ -792,17 +792,25 @@ __global__ __launch_bounds__(kCfThreads) void k_cforest_predict_dev(const Seg* _
 using predict_fn = void (*)(Seg, int64_t);
 using predict_batch_fn = void (*)(const Seg*, int, int64_t, int64_t);
 
+// Up to kMaxClasses classes: a batch of per_batch <= 256 rows holds at most 256.  More than
+// 64 is a rare shape (the wide variants' vote arrays live partly in scratch), kept so that
+// such a batch's forest (refit by sklearn on the host: the device and native trainers take
+// up to 64) is still predicted on the device instead of failing.
+constexpr int kMaxClasses = 256;
+
 template <bool kLds>
 predict_fn pick(bool pure, int k) {
     if (pure) {
         if (k <= 4) return k_forest_predict<true, 4, kLds>;
         if (k <= 8) return k_forest_predict<true, 8, kLds>;
         if (k <= 16) return k_forest_predict<true, 16, kLds>;
-        return k_forest_predict<true, 64, kLds>;
+        if (k <= 64) return k_forest_predict<true, 64, kLds>;
+        return k_forest_predict<true, kMaxClasses, kLds>;
     }
     if (k <= 4) return k_forest_predict<false, 4, kLds>;
     if (k <= 16) return k_forest_predict<false, 16, kLds>;
-    return k_forest_predict<false, 64, kLds>;
+    if (k <= 64) return k_forest_predict<false, 64, kLds>;
+    return k_forest_predict<false, kMaxClasses, kLds>;
 }
 
 template <bool kLds>
@@ -811,11 +819,13 @@ predict_batch_fn pick_batch(bool pure, int k) {
         if (k <= 4) return k_forest_predict_batch<true, 4, kLds>;
         if (k <= 8) return k_forest_predict_batch<true, 8, kLds>;
         if (k <= 16) return k_forest_predict_batch<true, 16, kLds>;
-        return k_forest_predict_batch<true, 64, kLds>;
+        if (k <= 64) return k_forest_predict_batch<true, 64, kLds>;
+        return k_forest_predict_batch<true, kMaxClasses, kLds>;
     }
     if (k <= 4) return k_forest_predict_batch<false, 4, kLds>;
     if (k <= 16) return k_forest_predict_batch<false, 16, kLds>;
-    return k_forest_predict_batch<false, 64, kLds>;
+    if (k <= 64) return k_forest_predict_batch<false, 64, kLds>;
+    return k_forest_predict_batch<false, kMaxClasses, kLds>;
 }
 
 size_t forest_lds_bytes(int n_nodes, int n_trees) {
@@ -837,7 +847,8 @@ extern "C" int ddm_forest_predict(const float* X, int64_t ld, int32_t n_features
         ddm::set_error("ddm_forest_predict: invalid argument");
         return DDM_E_ARG;
     }
-    if (forest->n_classes > 64 || (forest->pure && forest->n_trees > 255) || (!forest->pure && !forest->leaf_value)) {
+    if (forest->n_classes > kMaxClasses || (forest->pure && forest->n_trees > 255) ||
+        (!forest->pure && !forest->leaf_value)) {
         ddm::set_error("ddm_forest_predict: unsupported forest (classes=%d trees=%d pure=%d)", forest->n_classes,
                        forest->n_trees, forest->pure);
         return DDM_E_FOREST;
@@ -888,12 +899,13 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
     hipStream_t s = ddm::as_hip(stream);
     // One launch per kernel variant; every launch walks the whole device table and only
     // the blocks assigned to its segments work.  Variants: 16 node-walk kinds (pure x
-    // classes x LDS-resident forest) and 6 compiled kinds (vote registers x rows/lane).
+    // classes <= 64 x LDS-resident forest), 9 compiled kinds (vote registers x rows/lane)
+    // and 4 wide node-walk kinds (pure x LDS, up to kMaxClasses classes).
     Seg* hs = reinterpret_cast<Seg*>(const_cast<ddm_predict_segment*>(segs_host));
     for (int i = 0; i < n_segs; ++i) {
         const Seg& g = hs[i];
         if (!g.X || !g.y || !g.perm || !g.err || !g.nodes || !g.roots || !g.classes || g.pos_end < g.pos_begin ||
-            g.pos_begin < 0 || g.n_classes <= 0 || g.n_classes > 64 || g.n_trees <= 0 ||
+            g.pos_begin < 0 || g.n_classes <= 0 || g.n_classes > kMaxClasses || g.n_trees <= 0 ||
             (g.pure && g.n_trees > 255) || (!g.pure && !g.leaf_value)) {
             ddm::set_error("ddm_forest_predict_batch: invalid segment %d", i);
             return DDM_E_ARG;
@@ -904,16 +916,21 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
     }
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
-    constexpr int kNV = 16 + 9;
+    constexpr int kCf0 = 16, kWide0 = 16 + 9, kNV = 16 + 9 + 4;
+    const auto is_cf = [](int v) { return v >= kCf0 && v < kWide0; };
     std::vector<int> variant(n_segs);
     for (int i = 0; i < n_segs; ++i) {
         const Seg& g = hs[i];
         if (cf_usable(g, per_batch)) {
-            variant[i] = 16 + 3 * cf_rows_idx(cf_rows(g, per_batch)) + cf_vkind(g.cf_vote_regs);
+            variant[i] = kCf0 + 3 * cf_rows_idx(cf_rows(g, per_batch)) + cf_vkind(g.cf_vote_regs);
         } else {
             const bool lds = forest_lds_bytes(g.n_nodes, g.n_trees) <= (size_t)kMaxLdsForest;
-            const int kc = g.n_classes <= 4 ? 0 : g.n_classes <= 8 ? 1 : g.n_classes <= 16 ? 2 : 3;
-            variant[i] = (g.pure ? 1 : 0) * 8 + (lds ? 4 : 0) + kc;
+            if (g.n_classes > 64) {
+                variant[i] = kWide0 + (g.pure ? 2 : 0) + (lds ? 1 : 0);
+            } else {
+                const int kc = g.n_classes <= 4 ? 0 : g.n_classes <= 8 ? 1 : g.n_classes <= 16 ? 2 : 3;
+                variant[i] = (g.pure ? 1 : 0) * 8 + (lds ? 4 : 0) + kc;
+            }
         }
     }
     int64_t vbase[kNV + 1] = {0};
@@ -921,13 +938,13 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
     int64_t b0 = 0;
     for (int v = 0; v < kNV; ++v) {
         vbase[v] = b0;
-        const int unit = v >= 16 ? cf_unit(cf_rows_of_idx((v - 16) / 3), per_batch) : kThreads;
+        const int unit = is_cf(v) ? cf_unit(cf_rows_of_idx((v - kCf0) / 3), per_batch) : kThreads;
         int64_t rows = 0;
         for (int i = 0; i < n_segs; ++i)
             if (variant[i] == v) {
                 rows += hs[i].pos_end - hs[i].pos_begin;
-                vlds[v] = std::max(vlds[v], v >= 16 ? cf_lds_bound(hs[i], per_batch)
-                                                    : forest_lds_bytes(hs[i].n_nodes, hs[i].n_trees));
+                vlds[v] = std::max(vlds[v], is_cf(v) ? cf_lds_bound(hs[i], per_batch)
+                                                     : forest_lds_bytes(hs[i].n_nodes, hs[i].n_trees));
             }
         const int64_t total_blocks = rows ? std::min<int64_t>(ddm::ceil_div(rows, unit), kMaxBlocks) : 0;
         for (int i = 0; i < n_segs; ++i) {
@@ -941,15 +958,15 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
     }
     vbase[kNV] = b0;
     bool all_cf = true;
-    for (int i = 0; i < n_segs; ++i) all_cf = all_cf && variant[i] >= 16;
+    for (int i = 0; i < n_segs; ++i) all_cf = all_cf && is_cf(variant[i]);
     if (all_cf && n_segs <= kArgSegs) {
         // compiled forests only: the table rides in the kernel arguments (no table copy)
         SegTab tab{};
         for (int i = 0; i < n_segs; ++i) tab.s[i] = hs[i];
-        for (int v = 16; v < kNV; ++v) {
+        for (int v = kCf0; v < kWide0; ++v) {
             const int64_t nb = vbase[v + 1] - vbase[v];
             if (nb == 0) continue;
-            hipLaunchKernelGGL(pick_cf_arg((v - 16) % 3, cf_rows_of_idx((v - 16) / 3)), dim3((unsigned)nb),
+            hipLaunchKernelGGL(pick_cf_arg((v - kCf0) % 3, cf_rows_of_idx((v - kCf0) / 3)), dim3((unsigned)nb),
                                dim3(kCfThreads), vlds[v],
                                s, tab, n_segs, vbase[v], (int)per_batch);
             if (int rc = ddm::launch_status("ddm_forest_predict_batch")) return rc;
@@ -966,14 +983,15 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
     for (int v = 0; v < kNV; ++v) {
         const int64_t nb = vbase[v + 1] - vbase[v];
         if (nb == 0) continue;
-        if (v >= 16) {
-            hipLaunchKernelGGL(pick_cf_batch((v - 16) % 3, cf_rows_of_idx((v - 16) / 3)), dim3((unsigned)nb),
+        if (is_cf(v)) {
+            hipLaunchKernelGGL(pick_cf_batch((v - kCf0) % 3, cf_rows_of_idx((v - kCf0) / 3)), dim3((unsigned)nb),
                                dim3(kCfThreads), vlds[v], s,
                                reinterpret_cast<const Seg*>(segs_dev), n_segs, vbase[v], (int)per_batch);
         } else {
-            const bool lds = (v & 4) != 0;
-            const bool pure = (v & 8) != 0;
-            const int kmax = (v & 3) == 0 ? 4 : (v & 3) == 1 ? 8 : (v & 3) == 2 ? 16 : 64;
+            const bool wide = v >= kWide0;
+            const bool lds = wide ? ((v - kWide0) & 1) != 0 : (v & 4) != 0;
+            const bool pure = wide ? ((v - kWide0) & 2) != 0 : (v & 8) != 0;
+            const int kmax = wide ? kMaxClasses : (v & 3) == 0 ? 4 : (v & 3) == 1 ? 8 : (v & 3) == 2 ? 16 : 64;
             const predict_batch_fn fn = lds ? pick_batch<true>(pure, kmax) : pick_batch<false>(pure, kmax);
             hipLaunchKernelGGL(fn, dim3((unsigned)nb), dim3(kThreads), lds ? vlds[v] : 0, s,
                                reinterpret_cast<const Seg*>(segs_dev), n_segs, vbase[v], (int64_t)per_batch);

@@ -99,7 +99,8 @@ struct Hdr {                   // per stream
     int32_t active;            // this round scans the stream
     int32_t cont;              // mode 1: another round from next_lo
     int32_t fb;                // exact fallback from lo
-    int32_t status;            // 0 certified, 1 uncertified decision, 2 rounds exhausted
+    int32_t status;            // 0 certified, 1 uncertified decision, 2 rounds exhausted,
+                               // 3 uncertified decision from an inexact incoming state (void)
 };
 
 __device__ __forceinline__ MinEl mcomb(const MinEl& L, const MinEl& R) {
@@ -783,6 +784,16 @@ __global__ __launch_bounds__(64) void k_cert_prep_fb(Hdr* __restrict__ hdr, int6
         H.fb = 1;
         H.status = 2;
         H.cont = 0;
+    }
+    // The exact kernel is the reference only from the reference's state.  A fallback from the
+    // stream's first row starts from the caller's state, which is pa's (not the reference's
+    // rounded p) when it came with a bound: the near-tie the rescan exists for could then be
+    // decided wrongly, and the bound zeroed after it would certify what follows.  Such a
+    // stream is left alone with status 3 (every output void); the caller redoes the run from
+    // its last exact carry (ddm_amd/longstream.py).  Later rounds (mode 1) start fresh.
+    if (H.fb && H.lo == H.lo0 && (H.B0 != 0.0 || H.Bmin != 0.0)) {
+        H.fb = 0;
+        H.status = 3;
     }
     fb_off[s] = H.lo;
     fb_end[s] = H.hi;

@@ -19,6 +19,8 @@ DDM_E_FOREST = 1002
 DDM_E_NAN = 1003
 DDM_E_IMPURE = 1004
 DDM_STOP_FAILED = -2      # ddm_scan_long: the stream's look-back gave up, its results are void
+DDM_CERT_INEXACT = 3      # ddm_scan_certified: a decision was uncertified and the incoming state was
+                          # inexact (a nonzero bound): every output void, redo from an exact carry
 
 
 class DdmParams(ctypes.Structure):

@@ -72,11 +72,19 @@ class Segments:
 _NO_BOUND = np.zeros(2)
 
 
-def _carried(scanner, row0, n_rows, state, bound):
+class InexactCarry(RuntimeError):
+    """A certified carried scan met a decision inside its bound while its incoming state was
+    itself inexact (ddm_scan_certified status 3): its results are void; the run must be
+    redone from an exact carry."""
+
+
+def _carried(scanner, row0, n_rows, state, bound, exact=False):
     """Mode-1 scan of rows [row0, row0 + n_rows) as one stream from `state` (whose p and
-    p_min are within `bound` of the reference's); (events, end state, its bound)."""
+    p_min are within `bound` of the reference's); (events, end state, its bound).  exact:
+    the exact kernel (the state must be the reference's)."""
     if hasattr(scanner, "carried"):
-        out = scanner.carried(row0, n_rows, state, bound)
+        out = scanner.carried(row0, n_rows, state, bound, exact=exact) if exact else \
+            scanner.carried(row0, n_rows, state, bound)
         return out if len(out) == 3 else (out[0], out[1], _NO_BOUND)
     st = np.empty(1, STATE_DTYPE)
     st[0] = state
@@ -95,15 +103,27 @@ def resolve(carry, spec_final, segs, ev, scanner, chain=4, bound=None):
     k, redone = 0, 0
     n = segs.n
     bd = _NO_BOUND if bound is None else np.asarray(bound, np.float64)
+    exact_at = (0, carry) if not np.any(bd) else None   # the last carry known to be the reference's
+    force_exact = False
     while k < n:
         if state_fresh(carry):
             carry = spec_final[k]
             bd = _NO_BOUND                              # ddm_scan_batches: exact from a fresh carry
             k += 1
+            exact_at = (k, carry)
             continue
         m = min(n, k + chain)
         rows = sum(segs.lens[k:m])
-        e, f, fb = _carried(scanner, segs.rows0[k], rows, carry, bd)
+        try:
+            e, f, fb = _carried(scanner, segs.rows0[k], rows, carry, bd, exact=force_exact)
+        except InexactCarry:
+            if exact_at is None:                        # inexact since this call's carry-in
+                raise
+            # back to the last exact carry, that run on the exact kernel
+            k, carry = exact_at
+            bd, force_exact = _NO_BOUND, True
+            continue
+        force_exact = False
         base = segs.ev_off[k]
         j_end = None
         for j in range(k, m - 1):                       # a change in segment j's last batch
@@ -116,11 +136,14 @@ def resolve(carry, spec_final, segs, ev, scanner, chain=4, bound=None):
             redone += m - k
             k = m
             chain *= 2
+            if not np.any(bd):
+                exact_at = (k, carry)
         else:
             ev[base:segs.ev_off[j_end + 1]] = e[:segs.ev_off[j_end + 1] - base]
             carry, bd = _FRESH, _NO_BOUND
             redone += j_end + 1 - k
             k = j_end + 1
+            exact_at = (k, carry)
     return carry, redone, bd
 
 
@@ -130,14 +153,15 @@ class DeviceScanner:
     the CPU tests inject a scanner with the same interface).  Scratch buffers are kept and
     reused across calls; `status` counts the certified calls by outcome: [certified, handed
     to the exact kernel for a decision inside its bound, (mode 1) handed over after four
-    changes in the run]."""
+    changes in the run, void (a decision inside the bound of an inexact carry-in: redone
+    from the last exact carry by resolve)]."""
 
     def __init__(self, err, params, stream=None, certified=True):
         import torch
         self.err, self.params, self.stream = err, params, stream
         self.torch = torch
         self.certified = certified
-        self.status = [0, 0, 0]
+        self.status = [0, 0, 0, 0]
         self._scratch = {}
 
     def _buf(self, key, nbytes):
@@ -162,11 +186,13 @@ class DeviceScanner:
         torch.cuda.synchronize(dev)
         return ev[:n_segments * nb].cpu().numpy(), st.cpu().numpy().view(STATE_DTYPE).copy()
 
-    def carried(self, row0, n_rows, state, bound=None):
+    def carried(self, row0, n_rows, state, bound=None, exact=False):
         """(ev int32 [nb, 2], end state, its bound) of rows [row0, row0 + n_rows) as ONE mode-1
-        stream from `state` (p and p_min within `bound` of the reference's)."""
+        stream from `state` (p and p_min within `bound` of the reference's); exact: on
+        ddm_scan_long whatever `certified` says.  Raises InexactCarry when the certified scan
+        reports status 3."""
         from . import kernels
-        from ._capi import DDM_STOP_FAILED
+        from ._capi import DDM_CERT_INEXACT, DDM_STOP_FAILED
         torch = self.torch
         dev = self.err.device
         pb = self.params.per_batch
@@ -177,7 +203,7 @@ class DeviceScanner:
         off = torch.tensor([row0], dtype=torch.int64, device=dev)
         end = torch.tensor([row0 + n_rows], dtype=torch.int64, device=dev)
         base = torch.zeros(1, dtype=torch.int64, device=dev)
-        if not self.certified:
+        if exact or not self.certified:
             if bound is not None and np.any(np.asarray(bound) != 0):
                 raise ValueError("ddm_scan_long needs the reference's exact state (bound 0)")
             scratch = self._buf("long", kernels.scan_long_scratch_size(1, n_rows, pb))
@@ -193,9 +219,12 @@ class DeviceScanner:
         kernels.scan_certified(self.err, off, self.params, st, base, ev, n_rows, scratch, ends=end, stop=stop, mode=1,
                                bound=bd, status=status, stream=self.stream)
         torch.cuda.synchronize(dev)
+        code = int(status.item())
+        self.status[code] += 1
+        if code == DDM_CERT_INEXACT:
+            raise InexactCarry(f"rows [{row0}, {row0 + n_rows}): uncertified decision from an inexact carry")
         if int(stop.item()) == DDM_STOP_FAILED:
             raise RuntimeError("ddm_scan_long gave up waiting for a carried state")
-        self.status[int(status.item())] += 1
         return ev[:nb].cpu().numpy(), st.cpu().numpy().view(STATE_DTYPE)[0].copy(), bd.cpu().numpy()
 
 
@@ -255,9 +284,17 @@ def scan_long_stream(scanner, n_rows, per_batch, seg_batches=64, state_in=None, 
     spec_final = np.concatenate(finals) if finals else np.empty(0, STATE_DTYPE)
     carry0 = (fresh_states(1) if state_in is None else np.asarray(state_in, STATE_DTYPE).reshape(1))[0]
 
+    failed = [False]
+
     def resolved(carry, bound):
         ev = spec_ev.copy()
-        end, _, bd = resolve(carry, spec_final, segs, ev, scanner, bound=bound)
+        try:
+            end, _, bd = resolve(carry, spec_final, segs, ev, scanner, bound=bound)
+        except InexactCarry:
+            # only a carry-in from another rank (with a bound) gets here: this rank's results
+            # are void, the ranks agree on it below and redo the stream on the exact kernel
+            failed[0] = True
+            return ev, carry, _NO_BOUND
         return ev, end, bd
 
     if not distributed:
@@ -293,6 +330,17 @@ def scan_long_stream(scanner, n_rows, per_batch, seg_batches=64, state_in=None, 
             ev, end, bd = ev_f, end_f, bd_f
         else:
             ev, end, bd = mine if mine is not None else resolved(*carry_in[rank])
+    if distributed:
+        t = torch.tensor([1 if failed[0] else 0], dtype=torch.int64, device=_coll_device())
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if int(t.item()):
+            cert = getattr(scanner, "certified", False)
+            scanner.certified = False
+            try:
+                return scan_long_stream(scanner, n_rows, per_batch, seg_batches, state_in, distributed, first_batch,
+                                        with_bound)
+            finally:
+                scanner.certified = cert
     hit = np.nonzero(ev[:, 1] >= 0)[0]
     first = int(first_batch + hit[0]) if len(hit) else -1
     if distributed:

@@ -5,15 +5,15 @@ The reference fits `RandomForestClassifier(n_jobs=CORES)` with random_state=None
 draws the 100 per-tree seeds from numpy's global RandomState; the controller reads them
 from the partition's MT19937 stream, then the trees are grown natively (the call releases
 the GIL, so partition threads refit in parallel) and come back already packed for
-ddm_forest_predict.  Inputs containing NaN (missing values) return None: the controller
-then refits with sklearn itself.
+ddm_forest_predict.  Inputs containing NaN (missing values) or more than FIT_MAX_CLASSES
+(64) classes return None: the controller then refits with sklearn itself.
 """
 import ctypes
 
 import numpy as np
 
 from ._capi import DDM_E_IMPURE, DDM_E_NAN, check, lib
-from .treepack import MAX_CLASSES, NODE_DTYPE, PackedForest
+from .treepack import FIT_MAX_CLASSES, NODE_DTYPE, PackedForest
 
 
 class NativeForestTrainer:
@@ -34,9 +34,8 @@ class NativeForestTrainer:
         X32 = np.ascontiguousarray(X32, dtype=np.float32)
         n, F = X32.shape
         classes, yi = np.unique(np.asarray(y), return_inverse=True)
-        if classes.size > MAX_CLASSES:
-            raise ValueError(f"a training batch holds {classes.size} classes; the device path supports at most "
-                                 f"{MAX_CLASSES} per batch (INTEGRATION.md, limits)")
+        if classes.size > FIT_MAX_CLASSES:
+            return None                          # more classes than the native trainer takes: sklearn
         if n > self.max_rows:
             self._alloc(n)
         yi = np.ascontiguousarray(yi, dtype=np.int32)
@@ -101,16 +100,16 @@ class BatchForestTrainer:
 
     def fit_many(self, batches):
         """batches: [(X32 [n, F], y, seeds)] -> [(PackedForest, blob or None, head dict or None) or None
-        (None: NaN in X, refit with sklearn)]."""
+        (None: NaN in X or more than FIT_MAX_CLASSES classes, refit with sklearn)]."""
         jobs = (FitJob * len(batches))()
         keep = []
         for k, (X32, y, seeds) in enumerate(batches):
             X32 = np.ascontiguousarray(X32, dtype=np.float32)
             n, F = X32.shape
             classes, yi = np.unique(np.asarray(y), return_inverse=True)
-            if classes.size > MAX_CLASSES:
-                raise ValueError(f"a training batch holds {classes.size} classes; the device path supports at most "
-                                 f"{MAX_CLASSES} per batch (INTEGRATION.md, limits)")
+            if classes.size > FIT_MAX_CLASSES:
+                keep.append(None)                # more classes than the native trainer takes: sklearn
+                continue
             yi = np.ascontiguousarray(yi, dtype=np.int32)
             seeds = np.ascontiguousarray(seeds, dtype=np.int64)
             cls32 = classes.astype(np.int32)
@@ -127,7 +126,7 @@ class BatchForestTrainer:
         rc = lib.ddm_rf_fit_many(jobs, len(batches), self.n_threads)
         out = []
         for k, j in enumerate(jobs):
-            if j.status == DDM_E_NAN:
+            if keep[k] is None or j.status == DDM_E_NAN:      # > FIT_MAX_CLASSES classes, or NaN
                 out.append(None)
                 continue
             check(j.status, "ddm_rf_fit_many")

@@ -16,7 +16,8 @@ import numpy as np
 
 NODE_DTYPE = np.dtype([("threshold", "<f8"), ("feature", "<i4"), ("child", "<i4")])
 MISSING_LEFT_BIT = 1 << 30
-MAX_CLASSES = 64
+MAX_CLASSES = 256          # ddm_forest_predict's limit (a batch of <= 256 rows holds at most 256)
+FIT_MAX_CLASSES = 64       # the native and device trainers' limit: more -> sklearn refit
 
 
 def tree_arrays(rf):

@@ -41,7 +41,7 @@ extern "C" {
 #define DDM_AMD_ABI_VERSION 20
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
-#define DDM_E_FOREST     1002   /* forest shape not supported (classes > 64) */
+#define DDM_E_FOREST     1002   /* forest shape not supported (classes > 256) */
 #define DDM_E_NAN        1003   /* ddm_rf_fit: NaN in X (use sklearn for missing values) */
 #define DDM_E_IMPURE     1004   /* ddm_rf_fit: impure forest needs a (larger) leaf_value buffer */
 

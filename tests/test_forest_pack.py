@@ -64,11 +64,23 @@ def test_trace_forests_pack_and_predict():
     assert np.array_equal(walk_packed(pf, X32), oforest.predict(trees, pf.classes, X32))
 
 
-def test_too_many_classes_rejected():
+def test_class_limits():
+    """ddm_forest_predict takes up to 256 classes (70 pack; a batch of <= 256 rows cannot
+    hold more); more is refused.  The native trainer hands > 64 classes to sklearn."""
+    from ddm_amd.trainer import BatchForestTrainer, NativeForestTrainer
     rs = np.random.RandomState(0)
-    X = rs.rand(200, 3)
-    y = np.arange(200) % 70
+    X = rs.rand(300, 3)
+    y = np.arange(300) % 70
     rf = RandomForestClassifier(n_estimators=3, random_state=0).fit(X, y)
+    pf = pack(tree_arrays(rf), rf.classes_)
+    assert len(pf.classes) == 70
+    y2 = np.arange(300) % 257
+    rf2 = RandomForestClassifier(n_estimators=3, random_state=0).fit(X, y2)
     with pytest.raises(ValueError):
-        pack(tree_arrays(rf), rf.classes_)
+        pack(tree_arrays(rf2), rf2.classes_)
+    X32 = X[:100].astype(np.float32)
+    assert NativeForestTrainer(n_estimators=3).fit(X32, y[:100], np.arange(3)) is None
+    out = BatchForestTrainer(n_estimators=3, n_threads=2).fit_many([(X32, y[:100], np.arange(3)),
+                                                                    (X32, y[:100] % 5, np.arange(3))])
+    assert out[0] is None and out[1] is not None
 

@@ -137,3 +137,31 @@ def test_lockstep_batch_of_unequal_partitions_vs_oracle(win, maxwin, refit):
         assert runner.stats.device_refits + len(parts) >= runner.stats.refits - 1
     else:
         assert runner.stats.device_refits == 0
+
+
+def test_batches_with_more_than_64_classes_vs_oracle():
+    """a training batch with more than 64 classes (the native / device
+    trainers' limit) is refit by sklearn on the host and its forest predicted on the device
+    by the wide node-walk variants (up to 256 classes), instead of raising; == the oracle,
+    RNG position included."""
+    from ddm_amd.controller import BatchRunner, DevicePartition
+    from ddm_amd.params import DDMSettings
+    from ddm_amd.rng import MTStream
+    from oracle.controller import run_partition
+    dev = torch.device("cuda", 0)
+    rs = np.random.RandomState(12)
+    n, F = 2_600, 5
+    y = np.concatenate([np.arange(n // 2) % 90, 90 + np.arange(n - n // 2) % 80]).astype(np.int64)
+    X = np.stack([y + 0.3 * rs.rand(n)] + [rs.rand(n) for _ in range(F - 1)], axis=1)
+    part = DevicePartition.from_columns(np.ascontiguousarray(X.T.astype(np.float32)), y, dev)
+    runner = BatchRunner([part], DDMSettings())
+    rng = MTStream.from_seed(77)
+    got = runner.run([rng])[0]
+    runner.close()
+    np.random.seed(77)
+    want = run_partition(X.astype(np.float32).astype(np.float64), y, np.arange(n), np.arange(n))
+    assert np.array_equal(got[:, 0], want[:, 0]) and np.array_equal(got[:, 1], want[:, 2])
+    after = np.random.get_state()
+    assert np.array_equal(rng.key, after[1]) and rng.pos.value == after[2]
+    assert runner.stats.sklearn_refits >= 1
+    assert (want[:, 2] >= 0).sum() + (want[:, 0] >= 0).sum() >= 1

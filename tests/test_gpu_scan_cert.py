@@ -201,6 +201,30 @@ def test_forced_exact_rescan_is_bit_exact(oracle_lib):
     assert _capi.lib.ddm_scan_certified_set_tol_scale(0.5) != 0      # < 1 is refused
 
 
+def test_inexact_carried_state_is_not_rescanned_exactly(oracle_lib):
+    """a carried call whose incoming state is pa's (a nonzero incoming bound)
+    and whose first round leaves a decision uncertified must not run the exact kernel from
+    that state (its p is not the reference's) nor zero the bound: status 3, state and bound
+    left as they came in, so the caller redoes the run from its last exact carry."""
+    from ddm_amd import _capi
+    n, cut = 1_000_000, 600_000
+    e = thinning_stream(n, 1.3, jitter_seed=3)
+    a = gpu_scan_cert(e[:cut], np.array([0, cut]), mode=0)
+    assert a["status"][0] == 0 and a["bound"][0, 0] > 0
+    try:
+        assert _capi.lib.ddm_scan_certified_set_tol_scale(1e300) == 0
+        for mode in (0, 1):
+            b = gpu_scan_cert(e[cut:], np.array([0, n - cut]), mode=mode, state=a["st"], bound=a["bound"])
+            assert b["status"][0] == 3, (mode, b["status"])
+            np.testing.assert_array_equal(b["bound"], a["bound"])
+            np.testing.assert_array_equal(_state_matrix(b["st"]), _state_matrix(a["st"]))
+            # an exact incoming state (no bound) still takes the exact kernel: status 1
+            c = gpu_scan_cert(e[cut:], np.array([0, n - cut]), mode=mode, state=a["st"])
+            assert c["status"][0] in (1, 2) and (c["bound"] == 0).all()
+    finally:
+        _capi.lib.ddm_scan_certified_set_tol_scale(1.0)
+
+
 def test_mode1_reset_heavy_long_stream(oracle_lib):
     """A change in almost every batch (20 % noise): four certified rounds, then the exact
     kernel from the fifth change on."""

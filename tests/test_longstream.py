@@ -87,7 +87,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, q):
+def _worker(rank, world, port, n, q, certifying=False):
     import sys
     from conftest import PKG_ROOT, ROOT
     for p in (ROOT, PKG_ROOT):
@@ -98,31 +98,91 @@ def _worker(rank, world, port, n, q):
     from ddm_amd.longstream import chunk_bounds, scan_long_stream
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    err = long_stream(7, n)
+    err = _two_rank_stream(n, certifying)
     lo, hi = chunk_bounds(n, world, 16 * 100)[rank]
-    ev, end, first = scan_long_stream(OracleScanner(err[lo:hi]), hi - lo, 100, seg_batches=16, distributed=True,
-                                      first_batch=lo // 100)
-    q.put((rank, ev.tolist(), end.tolist(), first))
+    from test_longstream import CertifyingScanner
+    sc = (CertifyingScanner if certifying else OracleScanner)(err[lo:hi])
+    ev, end, first = scan_long_stream(sc, hi - lo, 100, seg_batches=16, distributed=True, first_batch=lo // 100)
+    q.put((rank, ev.tolist(), end.tolist(), first, getattr(sc, "calls", None)))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_ranks_equal_sequential_scan():
+def _two_rank_stream(n, certifying):
+    if not certifying:
+        return long_stream(7, n)
+    # a detector carried across the rank boundary (all errors around row n / 2): rank 1's
+    # carry-in comes with a bound, its certified rescan is void, every rank redoes exactly
+    rs = np.random.RandomState(5)
+    a = n // 2 - 6_000
+    return np.concatenate([rs.binomial(1, 0.3, a), np.ones(12_000, np.int64),
+                           rs.binomial(1, 0.2, n - a - 12_000)]).astype(np.uint8)
+
+
+@pytest.mark.parametrize("certifying", [False, True])
+def test_two_ranks_equal_sequential_scan(certifying):
     from oracle.ddm import scan_stream
-    n = 30_000
+    n = 30_000 if not certifying else 32_000
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, q, certifying)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=240) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    ref, _, dref, _ = scan_stream(long_stream(7, n), per_batch=100, mode="restart")
+    ref, _, dref, _ = scan_stream(_two_rank_stream(n, certifying), per_batch=100, mode="restart")
     ev = np.concatenate([np.array(r[1], dtype=np.int32).reshape(-1, 2) for r in res])
     assert np.array_equal(ev, ref)
     assert tuple(res[-1][2]) == tuple(dref.state_tuple())
     hit = np.nonzero(ref[:, 1] >= 0)[0]
     assert res[0][3] == res[1][3] == (int(hit[0]) if len(hit) else -1)
+    if certifying:                # rank 1's bounded carry-in was void: both ranks redid exactly
+        assert res[1][4]["void"] >= 1 and res[0][4]["exact"] >= 1 and res[1][4]["exact"] >= 1, res
+
+
+class CertifyingScanner(OracleScanner):
+    """OracleScanner with the certified carried-scan interface: every carried call from a
+    state with a nonzero bound reports a void result (ddm_scan_certified status 3, the
+    near-tie case) unless it is asked for the exact kernel; a certified result's bound is
+    nonzero.  Counts the calls by kind."""
+
+    def __init__(self, err, per_batch=100):
+        super().__init__(err, per_batch)
+        self.certified = True
+        self.calls = {"certified": 0, "void": 0, "exact": 0}
+
+    def carried(self, row0, n_rows, state, bound=None, exact=False):
+        from ddm_amd.kernels import STATE_DTYPE
+        from ddm_amd.longstream import InexactCarry
+        if not exact and self.certified and bound is not None and np.any(np.asarray(bound) != 0):
+            self.calls["void"] += 1
+            raise InexactCarry("near tie from an inexact carry")
+        st = np.empty(1, STATE_DTYPE)
+        st[0] = state
+        ev, fin = self.scan(row0, 1, n_rows, st)
+        if exact or not self.certified:
+            self.calls["exact"] += 1
+            return ev, fin[0], np.zeros(2)
+        self.calls["certified"] += 1
+        return ev, fin[0], np.array([1e-15, 1e-15])
+
+
+def test_void_certified_rescan_redone_from_last_exact_carry():
+    """a carried run whose certified rescan comes back void (status 3) is redone
+    from the last exact carry on the exact kernel; the result is still the sequential scan."""
+    from ddm_amd.longstream import scan_long_stream
+    from oracle.ddm import scan_stream
+    n = 60_000
+    rs = np.random.RandomState(2)
+    # a long all-error stretch: a detector carried through many segments (chained rescans)
+    err = np.concatenate([rs.binomial(1, 0.3, 8_000), np.ones(30_000, np.int64), rs.binomial(1, 0.2, 22_000)])
+    err = err.astype(np.uint8)
+    sc = CertifyingScanner(err)
+    ev, end, first = scan_long_stream(sc, n, 100, seg_batches=16)
+    ref, _, dref, _ = scan_stream(err, per_batch=100, mode="restart")
+    assert np.array_equal(ev, ref)
+    assert tuple(end.tolist()) == tuple(dref.state_tuple())
+    assert sc.calls["void"] >= 1 and sc.calls["exact"] >= 1, sc.calls
