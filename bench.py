@@ -104,6 +104,13 @@ def parse():
     ap.add_argument("--c4-len", type=int, default=4096)
     ap.add_argument("--c5-rows", type=int, default=64_000_000, help="c5 rows (all partitions)")
     ap.add_argument("--c5-flip", type=float, default=0.0, help="c5 label-noise rate")
+    ap.add_argument("--drift-window", type=int, default=0,
+                    help="least speculative window after a drift, in batches (0: DDMSettings' default)")
+    ap.add_argument("--predict-timing", type=int, default=-1,
+                    help="HIP events around every predict launch of the timed steps (the roofline's in-step time); "
+                         "-1: on for c3/c3w (about 7 us of queue time per event, ~2%% of a C3 step), off for the "
+                         "latency-bound c2/c5 epochs (8%% of a C5 step), whose kernel times then come from an "
+                         "instrumented step after the timed ones")
     ap.add_argument("--predict-replays", type=int, default=0,
                     help="isolated back-to-back replays of the last timed step's predict tables (a side figure; "
                          "0 for PMC runs, whose rows must be the steps' own)")
@@ -413,12 +420,13 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     gather_s = [0.0]
     if not parts:
         raise RuntimeError(f"rank {rank} owns no partition ({instances} partitions over {world} GPUs)")
+    settings = DDMSettings() if args.drift_window <= 0 else DDMSettings(drift_window_batches=args.drift_window)
     if args.groups > 1 and len(parts) > 1:
         # partition groups pipelined on their own epoch streams and host threads
-        runner = GroupedRunner([p for _, p in parts], DDMSettings(), groups=args.groups, refit=args.refit,
+        runner = GroupedRunner([p for _, p in parts], settings, groups=args.groups, refit=args.refit,
                                timing=True, fit_threads=args.fit_threads)
     else:
-        runner = BatchRunner([p for _, p in parts], DDMSettings(), torch.cuda.Stream(dev, priority=-1),
+        runner = BatchRunner([p for _, p in parts], settings, torch.cuda.Stream(dev, priority=-1),
                              refit=args.refit, timing=True, fit_threads=args.fit_threads)
     torch.cuda.synchronize()
 
@@ -455,7 +463,8 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     runner.set_kernel_timing(False)
     # the predict launches of the timed steps are timed by HIP events on the epoch stream
     # (a pair per device epoch, read after each run)
-    runner.set_predict_timing(True)
+    timed_predicts = args.predict_timing if args.predict_timing >= 0 else int(kind in ("c3", "c3w"))
+    runner.set_predict_timing(bool(timed_predicts))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -516,7 +525,8 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
         rows_per_launch = agg["device_rows"] / launches
         avg_ms_step = agg["predict_dev_ms"] / launches
         dev_bytes = agg["device_predict_bytes"]
-    else:       # host-planned epochs only (DDM_DEVICE_CTL=0, host refits): the instrumented step's
+    else:       # no predict timing in the timed steps (c2 / c5 by default, or host-planned epochs only):
+        # the instrumented step's HIP events around each epoch's predict
         launches = max(1, agg["epochs"])
         rows_per_launch = agg["predicted_rows"] / launches
         avg_ms_step = agg["predict_ms"] / launches
@@ -584,10 +594,12 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
                                      "only; decoupled epochs leave the permutation to k_err_permute)",
                 "alg_bytes_per_launch": bytes_launch, "avg_launch_ms": avg_ms, "avg_rows_per_launch": rows_per_launch,
                 "launches": agg["predict_dev_launches"], "decoupled_row_fraction": dec_frac,
-                "launch_timing": "HIP events on the epoch stream around every device-epoch predict launch of the timed "
-                                 "steps (launches with no rows -- epochs enqueued after a run's last active one -- "
-                                 "included, as in a rocprofv3 average; the run's first, host-planned epoch is a "
-                                 "different kernel and excluded)",
+                "launch_timing": ("HIP events on the epoch stream around every device-epoch predict launch of the "
+                                  "timed steps (launches with no rows -- epochs enqueued after a run's last active "
+                                  "one -- included, as in a rocprofv3 average; the run's first, host-planned epoch "
+                                  "is a different kernel and excluded)" if agg["predict_dev_launches"] else
+                                  "HIP events around each epoch's predict in one instrumented step after the timed "
+                                  "ones (no events in the timed steps: --predict-timing 0)"),
                 "isolated_replay": {"avg_launch_ms": replay_ms if replay_n else None, "launches": replay_n,
                                     "achieved": replay_gbs,
                                     "frac": replay_gbs / PEAK_HBM_GBS if replay_gbs else None,

@@ -106,7 +106,63 @@ extern "C" int ddm_ctl_enter(const ddm_ctl_epoch* e) {
                                     nullptr, nullptr);
 }
 
-extern "C" int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs) {
+namespace {
+
+// The epochs' launch sequence.  graph: the sequence is being captured into a graph that is
+// replayed back to back on the stream, so the first epoch needs no join (the graph before
+// it ended with one) and the last one ends with a join (a capture must end joined).
+int ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs, bool graph);
+
+}  // namespace
+
+extern "C" int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs) { return ctl_epochs(e, n_epochs, false); }
+
+// Epoch groups as hipGraphs: the whole group (both streams, their fork / join edges) is
+// captured once and replayed; every decision it needs is in device memory (k_ctl), so the
+// same graph serves every group of a runner whose tables do not move.
+extern "C" int ddm_ctl_graph_create(const ddm_ctl_epoch* e, int32_t n_epochs, void** exec_out) {
+    if (!e || !exec_out || n_epochs <= 0 || e->predict_evs) {
+        ddm::set_error("ddm_ctl_graph_create: invalid argument");
+        return DDM_E_ARG;
+    }
+    for (int k = 0; k < 12; ++k)
+        if (e->ev[k]) {
+            ddm::set_error("ddm_ctl_graph_create: timing events are not captured");
+            return DDM_E_ARG;
+        }
+    hipStream_t s = ddm::as_hip(e->stream);
+    if (int rc = ddm::hip_status(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed), "graph capture")) return rc;
+    const int rc_epochs = ctl_epochs(e, n_epochs, true);
+    hipGraph_t g = nullptr;
+    const int rc_end = ddm::hip_status(hipStreamEndCapture(s, &g), "graph capture end");
+    if (rc_epochs || rc_end) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc_epochs ? rc_epochs : rc_end;
+    }
+    hipGraphExec_t x = nullptr;
+    const int rc = ddm::hip_status(hipGraphInstantiate(&x, g, nullptr, nullptr, 0), "graph instantiate");
+    (void)hipGraphDestroy(g);
+    if (rc) return rc;
+    *exec_out = x;
+    return 0;
+}
+
+extern "C" int ddm_ctl_graph_launch(void* exec, ddm_stream_t stream) {
+    if (!exec) {
+        ddm::set_error("ddm_ctl_graph_launch: invalid argument");
+        return DDM_E_ARG;
+    }
+    return ddm::hip_status(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(exec), ddm::as_hip(stream)),
+                           "graph launch");
+}
+
+extern "C" int ddm_ctl_graph_destroy(void* exec) {
+    return exec ? ddm::hip_status(hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(exec)), "graph destroy") : 0;
+}
+
+namespace {
+
+int ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs, bool graph) {
     if (!e || !e->ctl.parts || e->ctl.n <= 0 || n_epochs < 0 || !e->side_stream || !e->fork_ev || !e->join_ev) {
         ddm::set_error("ddm_ctl_epochs: invalid argument");
         return DDM_E_ARG;
@@ -122,7 +178,8 @@ extern "C" int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs) {
         return ddm::hip_status(hipStreamWaitEvent(s, reinterpret_cast<hipEvent_t>(e->join_ev), 0), "join");
     };
     for (int32_t k = 0; k < n_epochs; ++k) {
-        if (!dec)
+        const bool first_in_graph = graph && k == 0;   // the graph before ended with the join
+        if (!dec && !first_in_graph)
             if (int rc = join()) return rc;         // the last epoch's shuffles of this window
         const ddm_event_t pb0 = e->predict_evs ? e->predict_evs[2 * k] : e->ev[0];
         const ddm_event_t pb1 = e->predict_evs ? e->predict_evs[2 * k + 1] : e->ev[1];
@@ -137,7 +194,7 @@ extern "C" int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs) {
                 return rc;
         }
         if (int rc = rec(pb1, s)) return rc;
-        if (dec)
+        if (dec && !first_in_graph)
             if (int rc = join()) return rc;
         if (int rc = rec(e->ev[2], s)) return rc;
         if (dec)
@@ -193,6 +250,10 @@ extern "C" int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs) {
         }
     }
     // the next call's first epoch waits for the last shuffles (the caller synchronises the
-    // side stream before it reads anything they write)
+    // side stream before it reads anything they write); a captured group joins them itself
+    if (graph && n_epochs > 0)
+        if (int rc = join()) return rc;
     return 0;
 }
+
+}  // namespace

@@ -42,6 +42,13 @@ __device__ __forceinline__ int64_t window_draws(int64_t W, int64_t dpb_x1024) {
 
 __device__ __forceinline__ int64_t blen(const ddm_ctl_part& p, int64_t b) { return b == p.nb - 1 ? p.last_len : p.pb; }
 
+// The window after a change (BatchRunner._epoch_after): the next concept likely lasts about
+// as long as the one just closed (seg batches), so the window covers seg plus a margin of
+// max(seg >> shift, pad) batches (rule = shift | pad << 8); windows still double after a miss.
+__device__ __forceinline__ int64_t next_window(int64_t seg, int32_t rule) {
+    return seg + max(seg >> (rule & 255), (int64_t)(rule >> 8));
+}
+
 // _epoch for one partition: refit bookkeeping (_refit_prep, device branch), the window
 // (b_end, Wg) and everything the epoch's kernels read.  Leaves the partition idle (empty
 // tables) when it is done, parked, stalled, or its stream words are not tabulated yet.
@@ -80,6 +87,13 @@ __device__ void plan(const ddm_ctl& c, ddm_ctl_part& p, int i) {
                 b_end = g0 + Wg;
             }
         }
+    }
+    // a window for ddm_scan_long when no long scan is enqueued: the host takes the partition
+    // and enables the long scans for the rest of the run (their launch is skipped until then)
+    if (active && exact && !c.long_ok &&
+        p.base + (b_end - 1) * pb + blen(p, b_end - 1) - (p.base + p.j * pb) >= p.long_min_rows) {
+        p.stall = DDM_CTL_STALL_LONG;
+        active = false;
     }
     ddm_shuffle_job& jb = c.jobs[i];
     ddm_predict_segment& sg = c.segs[i];
@@ -211,7 +225,7 @@ __device__ void commit(const ddm_ctl& c, ddm_ctl_part& p, int i) {
         const int64_t P_at = info[0];               // the staging's: after batch d's shuffle
         p.P = P_at;
         const int64_t seg = d - p.seg_start + 1;
-        p.win = max(p.min_win, seg + seg / 8);      // the next concept: 9/8 of this one
+        p.win = max(p.min_win, next_window(seg, p.win_rule));   // the next concept, with a margin
         p.j = d + 1;
         if (p.j >= p.nb) {
             p.done = 1;

@@ -43,7 +43,7 @@ struct Job {
     int32_t* ev_out;
     uint8_t* perm_w;
     int64_t* seeds_out;
-    int32_t n_trees, pad;
+    int32_t n_trees, win_rule;
     int64_t p_now, win, max_win, seg_start, n_full, min_win, next_avail, dpb_x1024;
     int64_t* plan_out;
     ddm_shuffle_job* next_job;
@@ -67,8 +67,7 @@ __device__ void plan_next(const Job& jb, int32_t stop, bool drawn, int64_t p_see
         jn = d + 1;
         Pn = p_seeds;
         g0n = jn + 1;
-        const int64_t seg = d - jb.seg_start + 1;
-        winn = max(jb.min_win, seg + seg / 8);
+        winn = max(jb.min_win, next_window(d - jb.seg_start + 1, jb.win_rule));
         ok = drawn;
     } else {
         jn = jb.b_end;

@@ -70,7 +70,7 @@ class DdmCtl(ctypes.Structure):
                 ("stage", _vp), ("off", _vp), ("end", _vp), ("state", _vp), ("first", _vp), ("stop", _vp),
                 ("pick", _vp), ("loff", _vp), ("lend", _vp), ("pstall", _vp), ("predict_blocks", _i64),
                 ("status", _vp), ("logs", _vp), ("log_b0", _vp), ("sync", _vp), ("decoupled", _i32),
-                ("pad_c", _i32)]
+                ("long_ok", _i32)]
 
 
 class DdmCtlEpoch(ctypes.Structure):
@@ -119,6 +119,9 @@ SIGNATURES = {
     "ddm_ctl_epoch_bytes": (_i64, []),
     "ddm_ctl_enter": (ctypes.c_int, [_vp]),
     "ddm_ctl_epochs": (ctypes.c_int, [_vp, _i32]),
+    "ddm_ctl_graph_create": (ctypes.c_int, [_vp, _i32, ctypes.POINTER(ctypes.c_void_p)]),
+    "ddm_ctl_graph_launch": (ctypes.c_int, [_vp, _vp]),
+    "ddm_ctl_graph_destroy": (ctypes.c_int, [_vp]),
     "ddm_forest_predict_dev": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i64, _vp, _vp, _vp, _vp]),
     "ddm_epoch_struct_bytes": (_i64, []),
     "ddm_shuffle_window": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp,

@@ -41,7 +41,9 @@ from .trainer import BatchForestTrainer
 # (every row of it is exact arithmetic) and it spans at least this many rows.
 LONG_SCAN_MIN_ROWS = int(os.environ.get("DDM_LONG_SCAN_ROWS", 4 * 64 * 100))
 # Device-resident epochs (devctl.py) by default; DDM_DEVICE_CTL=0 keeps every epoch on the host path.
+# DDM_DEVICE_START=0: the first epoch (first fits on the host) stays host-planned.
 DEVICE_CTL = os.environ.get("DDM_DEVICE_CTL", "1") not in ("", "0")
+DEVICE_START = os.environ.get("DDM_DEVICE_START", "1") not in ("", "0")
 
 
 def carried_exact(st):
@@ -590,6 +592,9 @@ class BatchRunner:
         if ex is not None:
             ex.shutdown(wait=True)
             self._executor = None
+        if getattr(self, "devctl", None) is not None:
+            self.stream.synchronize()
+            self.devctl.close()
 
     # -- per-epoch tables: per-partition template records (the static fields), of which an
     #    epoch takes the live partitions' rows and sets the fields that move
@@ -612,6 +617,7 @@ class BatchRunner:
                 self._dptr(self.o_pick, i, 8)
             r["nb"], r["pb"], r["last_len"], r["n_features"] = self.nbs[i], pb, part.n - (self.nbs[i] - 1) * pb, F
             r["n_words"], r["max_events"], r["n_trees"] = self.n_words, self.max_events, T
+            r["win_rule"] = self.s.win_rule
             r["x_out"], r["y_out"], r["w_out"] = self._sptr("x", i), self._sptr("y", i), self._sptr("w", i)
             r["info_out"], r["ev_out"], r["perm_w"], r["seeds_out"] = self._sptr("info", i), self._sptr("ev", i), \
                 perm, self._sptr("seeds", i)
@@ -835,6 +841,9 @@ class BatchRunner:
             out_f = [pool.submit(np.full, (ps.nb - 1, 2), -1, np.int64) for ps in pss]
             self._mark("batch-0 shuffles")
             host_epochs = 0
+            if self.devctl is not None and DEVICE_START and self._device_start(pss):
+                host_epochs = 1                  # straight into device epochs
+                self._mark("device first fit enqueued")
             while True:
                 live = [ps for ps in pss if not ps.done]
                 if not live:
@@ -883,6 +892,59 @@ class BatchRunner:
             self.gen_stream.synchronize()
             self.tab_stream.synchronize()
             self._mark("side streams drained")
+
+    def _device_start(self, pss):
+        """The first fit of every partition on the device, so that the run starts in device
+        epochs instead of a host-planned first epoch with host fits.  The reference draws
+        batch 0's shuffle (DDM_Process.py:187, done on the host from the head words), batch
+        1's shuffle and the first fit's 100 seeds (:190, :194-196, :102): exactly what the
+        staging kernel draws after a change in a batch d, with d = 0 -- the training batch
+        is batch 0 in shuffled order, batch d + 1 = 1 is shuffled, the seeds follow it.  So
+        one ddm_epoch_stage launch with a change planted in batch 0 stages the rows, shuffle
+        and seeds, the gated device refit runs on them, and every partition enters device
+        mode with that refit pending (a refit that fails stalls to the host, which redoes it
+        from the staged batch, as after any change).  False (nothing enqueued) when the host
+        path must take the first epoch."""
+        if not self.dfit_rows or len(pss) > len(self.parts):
+            return False
+        s, pb, T = self.s, self.s.per_batch, self.s.n_estimators
+        plans = []
+        for ps in pss:
+            if ps.words0 is None or ps.nb < 2:
+                return False
+            r = perm_seeds_from_words(ps.words0, ps.blen(1), T)
+            if r is None:                        # rejections ran past the head read-back
+                return False
+            plans.append((ps, ps.P + r[2], ps.P + r[2] + r[3]))
+        n, stream = len(pss), self.stream
+        t = self._stream_ptrs(pss)
+        rec = t["stage"][[ps.i for ps in pss]]
+        rec["j"], rec["g0"], rec["b_end"] = 0, 1, 1
+        rec["p_after_first"] = [ps.P for ps in pss]          # the draw after batch 0's shuffle
+        rec["p_tail_after"], rec["tail"] = -1, 0
+        rec["p_now"] = [ps.P for ps in pss]
+        rec["win"] = [ps.win for ps in pss]
+        rec["seg_start"] = 0
+        rec["next_avail"] = [self.shuffles[ps.i].waited * CHUNK for ps in pss]
+        rec["max_events"], rec["log"], rec["plan_out"], rec["next_job"] = 0, 0, 0, 0
+        self.stage_jobs.rec[:n] = rec
+        self.dfit_jobs.rec[:n] = self._templates()["dfit"][[ps.i for ps in pss]]
+        for ps in pss:
+            self._upload_perm(ps.i, 0, np.asarray(ps.train_rows, dtype=np.uint8), 0)
+        with torch.cuda.stream(stream):
+            # the whole host half of the slab, as a host epoch uploads it: the device copy
+            # must hold every static table field (the next-window jobs' stream pointers,
+            # the batch bases, ...), since a device phase hands the slab back to the host
+            # (ctrl_d -> ctrl_h) when it ends
+            self.ctrl_d[:self.o_stage].copy_(self.ctrl_h[:self.o_stage], non_blocking=True)
+            self.ctrl_d[self.o_stop:self.o_stop + 4 * len(self.parts)].zero_()   # a change in batch 0
+        kernels.epoch_stage(self.stage_jobs, n, stream, upload=False)
+        dfit.fit_device(self.dfit_jobs.d, n, T, stream, self._E.dfit_max_lf)
+        for ps, P1, P2 in plans:
+            ps.j, ps.seg_start, ps.retrain = 1, 1, True
+            ps.staged = ("device", P1, P2, None)
+            ps.words0 = None
+        return True
 
     def _epoch_desc(self):
         """The ddm_epoch record of this runner (ddm_epoch_launch): the buffers never move, so
@@ -958,7 +1020,7 @@ class BatchRunner:
         s = self.s
         lo = max(1, min(s.window_batches, s.drift_window_batches))
         return max(0, min(ps.max_win, ps.nb - ps.j,
-                          max(lo, (ps.b_end - ps.seg_start) * 9 // 8 + 1, 2 * ps.win)))
+                          max(lo, s.next_window(ps.b_end - ps.seg_start) + 1, 2 * ps.win)))
 
     def _enqueue_rest(self):
         """The partitions' whole streams, in growing pieces on the side streams (the first
@@ -1284,10 +1346,10 @@ class BatchRunner:
                                  info[4], info[5])
                 ps.retrain = True
                 # adaptive speculation: the next concept likely lasts about as long as this
-                # one, so the next window covers it with 1/8 to spare (one epoch per drift
-                # when concepts repeat their length; windows still double after a miss)
+                # one, so the next window covers it with a margin (one epoch per drift when
+                # concepts repeat their length; windows still double after a miss)
                 seg = d - ps.seg_start + 1
-                ps.win = max(max(1, min(s.window_batches, s.drift_window_batches)), seg + seg // 8)
+                ps.win = max(max(1, min(s.window_batches, s.drift_window_batches)), s.next_window(seg))
                 ps.j = d + 1
             else:
                 if ps.tail:

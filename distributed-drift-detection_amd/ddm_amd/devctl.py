@@ -21,6 +21,7 @@ mode.  The decisions are the host's, line for line, so results do not depend on 
 (tests/test_gpu_devctl.py).
 """
 import ctypes
+import os
 import time
 
 import numpy as np
@@ -41,6 +42,9 @@ GROUP = 4                       # epochs per enqueued group
 # shuffles before the predict (they finish under the refit, and the permutation would be one
 # launch more per epoch).
 DECOUPLE_ROWS = 200_000
+# DDM_CTL_GRAPH=1: each group of epochs is one replayed hipGraph (ddm_ctl_graph_create) instead
+# of ~20 launches and event operations per epoch enqueued from the host
+CTL_GRAPH = os.environ.get("DDM_CTL_GRAPH", "0") not in ("", "0")
 
 
 class PredictTimer:
@@ -120,12 +124,17 @@ class DeviceController:
         self.avail_h = torch.zeros(64 * n, dtype=torch.int64, pin_memory=True)   # H2D sources (a ring)
         self._avail_k = 0
         self.long_min_rows, self.long_cap_rows = int(long_min_rows), int(long_cap_rows)
+        # ddm_scan_long is enqueued in the epochs only once a window needed it (a partition
+        # stalls with CTL_STALL_LONG the first time): until then every epoch is one launch
+        # shorter (C5: ~6 us of each ~150-us epoch)
+        self.long_ok = False
         # row-order errors of decoupled epochs: a buffer shaped like the runner's err
         self.err_rows = torch.empty_like(r.err_all)
         self.decouple_ok = True      # off after a decoupled predict found a forest it cannot take
         self.timers = []             # per-epoch HIP event pairs when the runner times kernels
         self.seg_log = None          # (segs, res) device copies per epoch when the runner logs predicts
         self.pred_timer = None       # a PredictTimer while the runner times the predict launches
+        self.graphs = {}             # (decouple, long_ok) -> captured group of GROUP epochs
         self._E = None
 
     # ---------------------------------------------------------------- eligibility
@@ -169,7 +178,7 @@ class DeviceController:
         E.err, E.params, E.batch_base = r.err_all.data_ptr(), ctypes.addressof(r.params), base + r.o_bbase
         E.n_batches_total, E.ev_out, E.nev, E.perm_map = r.ev_total, r.ev_d.data_ptr(), base + r.o_nev, \
             r.perm_all.data_ptr()
-        E.long_max_rows, E.long_scratch = self.long_cap_rows, r.long_scratch.data_ptr()
+        E.long_max_rows, E.long_scratch = 0, r.long_scratch.data_ptr()
         E.dfit_jobs, E.n_dfit, E.max_trees = r.dfit_jobs.d.data_ptr(), self.n, r.s.n_estimators
         mw = max(r.max_wins)
         E.max_W = mw
@@ -213,6 +222,7 @@ class DeviceController:
             q["dtrees"] = b.T
             q["nb"], q["n_full"], q["base"] = r.nbs[i], t["stage"][i]["n_full"], r.bases[i]
             q["max_win"], q["min_win"] = r.max_wins[i], lo
+            q["win_rule"] = r.s.win_rule
             q["long_min_rows"], q["long_cap_rows"] = self.long_min_rows, self.long_cap_rows
             q["dpb_x1024"] = int(np.ceil(expected_draws_per_batch(pb) * 1024))
             q["pb"], q["last_len"], q["n_words"] = pb, part.n - (r.nbs[i] - 1) * pb, r.n_words
@@ -295,6 +305,22 @@ class DeviceController:
         stream.synchronize()
         r._pending_sync = False
         r._pending_forests = []
+        E = self._epoch_struct()
+        E.long_max_rows = self.long_cap_rows if self.long_ok else 0
+        E.ctl.long_ok = 1 if self.long_ok else 0
+        timing = r.t_pred is not None
+        logging = r.predict_log is not None
+        pt = self.pred_timer
+        # HIP cannot time events that a graph records (hipEventElapsedTime: invalid resource
+        # handle), so timed predicts keep the launched form
+        use_graph = CTL_GRAPH and pt is None and not (timing or logging)
+        if use_graph:
+            # every launch sequence captured while both streams are idle (a capture joins the
+            # side stream through the fork event)
+            r.side_stream.synchronize()
+            for dec in (0, 1):
+                E.decouple = dec
+                self._graph(E)
         # the rest of the streams in growing pieces, two more at every poll (all of it up
         # front kept the side streams busy past the last epoch: the run waited ~14 ms for
         # generation no epoch needed, C3)
@@ -306,18 +332,16 @@ class DeviceController:
             r.dfit_jobs.d[:self.n * dfit.DFIT_DTYPE.itemsize].copy_(
                 r.dfit_jobs.h[:self.n * dfit.DFIT_DTYPE.itemsize], non_blocking=True)
         self._publish_avail()
-        E = self._epoch_struct()
         E.decouple = self._decouple([(ps.win, r.max_wins[ps.i]) for ps in live])
         check(lib.ddm_ctl_enter(ctypes.byref(E)), "ddm_ctl_enter")
         r._mark("device phase entered")
-        timing = r.t_pred is not None
-        logging = r.predict_log is not None
         pending, slot, epochs, group = None, 0, 0, 0
-        pt = self.pred_timer
         while True:
             if timing or logging:
                 for _ in range(GROUP):
                     self._one_epoch_instrumented(E, timing, logging)
+            elif use_graph:
+                check(lib.ddm_ctl_graph_launch(self._graph(E), stream.cuda_stream), "ddm_ctl_graph_launch")
             else:
                 E.predict_evs = pt.arm(GROUP, group) if pt is not None else None
                 check(lib.ddm_ctl_epochs(ctypes.byref(E), GROUP), "ddm_ctl_epochs")
@@ -365,6 +389,26 @@ class DeviceController:
         out = self._take_back(live)
         r._mark("records taken back")
         return out
+
+    def _graph(self, E):
+        """The captured group for the epochs' current launch sequence (decoupled or not, long
+        scans enqueued or not); captured on first use, kept for the runner's life."""
+        key = (int(E.decouple), int(E.ctl.long_ok), int(E.long_max_rows))
+        g = self.graphs.get(key)
+        if g is None:
+            g = ctypes.c_void_p()
+            E.predict_evs = None
+            check(lib.ddm_ctl_graph_create(ctypes.byref(E), GROUP, ctypes.byref(g)), "ddm_ctl_graph_create")
+            self.graphs[key] = g
+        return g
+
+    def close(self):
+        for g in self.graphs.values():
+            lib.ddm_ctl_graph_destroy(g)
+        self.graphs = {}
+        if self.pred_timer is not None:
+            self.pred_timer.close()
+            self.pred_timer = None
 
     def _decouple(self, wins):
         """1 when the active partitions' windows ((win, max_win) pairs) average at least
@@ -461,6 +505,8 @@ class DeviceController:
             if stall == kernels.CTL_STALL_REFIT and self._E is not None and self._E.decouple:
                 # the row-order predict's smaller LDS (csrc/forest_predict.hip) may be why
                 self.decouple_ok = False
+            if stall == kernels.CTL_STALL_LONG:          # the next phases enqueue the long scans
+                self.long_ok = True
             if stall == kernels.CTL_STALL_SCAN:
                 raise RuntimeError(f"ddm_scan_long gave up waiting for a carried state (partition {ps.i}): the "
                                    "epoch's results are void")

@@ -39,7 +39,7 @@ STAGE_DTYPE = np.dtype([("X", "<u8"), ("ld", "<i8"), ("y", "<u8"), ("perm", "<u8
                         ("last_len", "<i4"), ("n_features", "<i4"), ("n_words", "<i4"), ("tail", "<i4"),
                         ("max_events", "<i4"), ("x_out", "<u8"), ("y_out", "<u8"), ("w_out", "<u8"),
                         ("info_out", "<u8"), ("ev_out", "<u8"), ("perm_w", "<u8"), ("seeds_out", "<u8"),
-                        ("n_trees", "<i4"), ("pad", "<i4"), ("p_now", "<i8"), ("win", "<i8"), ("max_win", "<i8"),
+                        ("n_trees", "<i4"), ("win_rule", "<i4"), ("p_now", "<i8"), ("win", "<i8"), ("max_win", "<i8"),
                         ("seg_start", "<i8"), ("n_full", "<i8"), ("min_win", "<i8"), ("next_avail", "<i8"),
                         ("dpb_x1024", "<i8"), ("plan_out", "<u8"), ("next_job", "<u8")])
 STAGE_DTYPE = np.dtype(STAGE_DTYPE.descr + [("log", "<u8"), ("log_n", "<u8"), ("log_cap", "<i8"), ("stall", "<u8")])
@@ -50,7 +50,7 @@ CTL_PART_DTYPE = np.dtype([("job", JOB_DTYPE), ("seg", SEG_DTYPE), ("stage", STA
                            ("dblob", "<u8"), ("nb", "<i8"), ("n_full", "<i8"), ("base", "<i8"), ("max_win", "<i8"),
                            ("min_win", "<i8"), ("long_min_rows", "<i8"), ("long_cap_rows", "<i8"),
                            ("dpb_x1024", "<i8"), ("pb", "<i4"), ("last_len", "<i4"), ("n_words", "<i4"),
-                           ("dtrees", "<i4"), ("host_slots", "<i4"), ("pad0", "<i4"),
+                           ("dtrees", "<i4"), ("host_slots", "<i4"), ("win_rule", "<i4"),
                            ("j", "<i8"), ("P", "<i8"), ("win", "<i8"), ("seg_start", "<i8"), ("P1", "<i8"),
                            ("P2", "<i8"), ("avail", "<i8"), ("retrain", "<i4"), ("done", "<i4"), ("stall", "<i4"),
                            ("park", "<i4"), ("forest_dev", "<i4"), ("applied", "<i4"), ("idle", "<i4"),
@@ -59,7 +59,7 @@ CTL_PART_DTYPE = np.dtype([("job", JOB_DTYPE), ("seg", SEG_DTYPE), ("stage", STA
                            ("n_log", "<i8"), ("predicted_rows", "<i8"), ("predict_bytes", "<i8"), ("epochs", "<i8"),
                            ("refits", "<i8"), ("log_mark", "<i8"), ("long_scans", "<i8"),
                            ("permute_rows", "<i8"), ("pad2", "<i8")])
-CTL_STALL_REFIT, CTL_STALL_WORDS, CTL_STALL_SCAN = 1, 2, 3
+CTL_STALL_REFIT, CTL_STALL_WORDS, CTL_STALL_SCAN, CTL_STALL_LONG = 1, 2, 3, 4
 
 
 class PinnedTable:

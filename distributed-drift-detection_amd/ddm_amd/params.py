@@ -21,7 +21,21 @@ class DDMSettings:
     max_window_batches: int = 1 << 16
     drift_window_batches: int = 16       # least window after a drift (short concepts: an epoch costs more
                                          # than predicting a few batches past the next drift)
+    # the window after a drift covers the concept just closed (seg batches) plus
+    # max(seg >> drift_window_shift, drift_window_pad) batches: concepts that repeat their
+    # length are found in one epoch each, with little predicted past them (a miss doubles)
+    drift_window_shift: int = 5
+    drift_window_pad: int = 4
     extra: dict = field(default_factory=dict)
+
+    def next_window(self, seg):
+        """The window after a change that closed a concept of seg batches (before the
+        least-window floor; csrc/ctl_dev.h next_window)."""
+        return seg + max(seg >> self.drift_window_shift, self.drift_window_pad)
+
+    @property
+    def win_rule(self):
+        return int(self.drift_window_shift) | (int(self.drift_window_pad) << 8)
 
 
 SCHEMA = ("warning_flag_local int, warning_flag_global int, change_flag_local int, "

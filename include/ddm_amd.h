@@ -444,7 +444,8 @@ typedef struct ddm_stage_job {
     float* x_out; int32_t* y_out; uint32_t* w_out; int64_t* info_out; int32_t* ev_out;
     uint8_t* perm_w;        /* perm array to receive batch d+1's shuffle (may be NULL)   */
     int64_t* seeds_out;     /* [n_trees] refit seeds drawn after it (may be NULL)        */
-    int32_t n_trees, pad;
+    int32_t n_trees;
+    int32_t win_rule;       /* ABI 20: window after a change (ddm_ctl_part.win_rule)      */
     /* next-window plan (plan_out may be NULL): the controller's window policy applied on
      * the device, so the next window's shuffles can run before the host has seen this
      * epoch.  plan_out = {P, W (0: not planned), g0, b_end, j, planned}; next_job (may be
@@ -594,7 +595,10 @@ typedef struct ddm_ctl_part {
     const uint8_t* dblob;        /* the device refit's forest buffers */
     int64_t nb, n_full, base, max_win, min_win, long_min_rows, long_cap_rows, dpb_x1024;
     int32_t pb, last_len, n_words, dtrees;
-    int32_t host_slots, pad0;    /* feature slots the host forest reads (statistics) */
+    int32_t host_slots;          /* feature slots the host forest reads (statistics) */
+    int32_t win_rule;            /* ABI 20: the window after a change covers the concept just
+                                    closed plus max(concept >> (win_rule & 255), win_rule >> 8)
+                                    batches (DDMSettings drift_window_shift / _pad) */
     /* dynamic: the host controller's state at the start of an epoch */
     int64_t j, P, win, seg_start, P1, P2, avail;
     int32_t retrain, done, stall, park, forest_dev, applied, idle, pad1;
@@ -612,6 +616,7 @@ typedef struct ddm_ctl_part {
 #define DDM_CTL_STALL_REFIT 1    /* the device refit reported a status / did not compile     */
 #define DDM_CTL_STALL_WORDS 2    /* batch d+1's shuffle or the seeds ran past the staged words */
 #define DDM_CTL_STALL_SCAN  3    /* ddm_scan_long gave up (DDM_STOP_FAILED)                   */
+#define DDM_CTL_STALL_LONG  4    /* a carried window needs ddm_scan_long, not enqueued          */
 
 typedef struct ddm_ctl {
     ddm_ctl_part* parts; int32_t n, entry;       /* entry: plan the first window only     */
@@ -625,9 +630,14 @@ typedef struct ddm_ctl {
     uint32_t* sync;                                /* NULL or uint32[2], zeroed: [0] the fused
                                                       staging's block ticket (left 0), [1] set
                                                       when the next epoch has a long window    */
-    int32_t decoupled, pad_c;                      /* ABI 20: set by ddm_ctl_epochs for the
+    int32_t decoupled;                             /* ABI 20: set by ddm_ctl_epochs for the
                                                       decisions kernel: this epoch's predict
                                                       wrote row-order errors (statistics)      */
+    int32_t long_ok;                               /* ABI 20: ddm_scan_long runs in the epochs
+                                                      (long_max_rows > 0); 0: a window that
+                                                      needs it stalls (DDM_CTL_STALL_LONG)
+                                                      instead, and no long-scan launch is
+                                                      enqueued                                 */
 } ddm_ctl;
 
 typedef struct ddm_ctl_epoch {
@@ -664,6 +674,15 @@ int ddm_ctl_enter(const ddm_ctl_epoch* e);
  * ctl.sync, pick + staging + decisions are one kernel (the last workgroup splits the predict
  * grid) and the long scan's blocks return at once in epochs without a long window. */
 int ddm_ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs);
+/* ABI 20: n_epochs of ddm_ctl_epochs captured once into an executable hipGraph (both streams
+ * and their fork / join edges; no timing events: e->ev and e->predict_evs must be empty, HIP
+ * does not time events a graph records), replayed by ddm_ctl_graph_launch on
+ * e->stream.  Every decision is in device memory, so one graph serves every group of the
+ * same runner (the tables never move).  A replayed group starts without the join of the
+ * group before it and ends with its own. */
+int ddm_ctl_graph_create(const ddm_ctl_epoch* e, int32_t n_epochs, void** exec_out);
+int ddm_ctl_graph_launch(void* exec, ddm_stream_t stream);
+int ddm_ctl_graph_destroy(void* exec);
 
 /* Forest predict for the device-resident runner: one launch, fixed grid, segments and block
  * split from the device table; a segment with res[s] != NULL takes its compiled forest's shape

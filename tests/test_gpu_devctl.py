@@ -98,3 +98,44 @@ def test_device_epochs_vs_oracle():
         assert np.array_equal(rng[k][0], after[1]) and rng[k][1] == after[2], k
         drifts += int((want[:, 2] >= 0).sum())
     assert drifts >= 50
+
+
+@pytest.mark.parametrize("case,decouple,timed", [("jitter", False, False), ("blocks", True, True),
+                                                 ("tails", False, True), ("noise", True, False)])
+def test_graph_epochs_equal_host_epochs(case, decouple, timed, monkeypatch):
+    """Groups of device epochs captured once as hipGraphs and replayed (DDM_CTL_GRAPH,
+    ddm_ctl_graph_create; with predict timing the launched form runs instead): the same
+    events, RNG positions and refits as host epochs, over two runs of the same runner (the
+    cached graphs replayed again)."""
+    from ddm_amd import devctl
+    from ddm_amd.controller import BatchRunner
+    from ddm_amd.params import DDMSettings
+    from ddm_amd.rng import MTStream
+    monkeypatch.setattr(devctl, "CTL_GRAPH", True)
+    if decouple:
+        monkeypatch.setattr(devctl, "DECOUPLE_ROWS", 0)
+    if case == "blocks":
+        parts = _parts((60_000,) * 4, 27, 20_011, 3)
+    elif case == "jitter":
+        parts = _parts((24_000,) * 4, 27, 0, 5, jitter=True)
+    elif case == "noise":
+        parts = _parts((30_000, 30_000), 27, 0, 7, flip=0.01, jitter=True)
+    else:
+        parts = _parts((24_037, 17_055, 4_321, 9_999), 27, 6_007, 9)
+    seeds = [300 + k for k in range(len(parts))]
+    host_out, host_rng, st_h = _run(parts, False, seeds)
+    runner = BatchRunner(parts, DDMSettings(), device_ctl=True)
+    if timed:
+        runner.set_predict_timing(True)
+    for rep in range(2):
+        rngs = [MTStream.from_seed(s) for s in seeds]
+        out = runner.run(rngs)
+        for k in range(len(parts)):
+            assert np.array_equal(out[k], host_out[k]), (rep, k)
+            assert np.array_equal(rngs[k].key, host_rng[k][0]) and rngs[k].pos.value == host_rng[k][1], (rep, k)
+    st = runner.stats
+    assert st.device_epochs > 0 and (timed or len(runner.devctl.graphs) > 0)
+    if timed:
+        assert st.predict_dev_launches > 0 and st.predict_dev_ms > 0
+        runner.set_predict_timing(False)
+    runner.close()
