@@ -106,6 +106,8 @@ def parse():
     ap.add_argument("--c5-flip", type=float, default=0.0, help="c5 label-noise rate")
     ap.add_argument("--drift-window", type=int, default=0,
                     help="least speculative window after a drift, in batches (0: DDMSettings' default)")
+    ap.add_argument("--drift-short", type=int, default=-1,
+                    help="concepts of at most this many batches skip that floor (-1: DDMSettings' default)")
     ap.add_argument("--predict-timing", type=int, default=-1,
                     help="HIP events around every predict launch of the timed steps (the roofline's in-step time); "
                          "-1: on for c3/c3w (about 7 us of queue time per event, ~2%% of a C3 step), off for the "
@@ -420,7 +422,11 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     gather_s = [0.0]
     if not parts:
         raise RuntimeError(f"rank {rank} owns no partition ({instances} partitions over {world} GPUs)")
-    settings = DDMSettings() if args.drift_window <= 0 else DDMSettings(drift_window_batches=args.drift_window)
+    settings = DDMSettings()
+    if args.drift_window > 0:
+        settings.drift_window_batches = args.drift_window
+    if args.drift_short >= 0:
+        settings.drift_window_short = args.drift_short
     if args.groups > 1 and len(parts) > 1:
         # partition groups pipelined on their own epoch streams and host threads
         runner = GroupedRunner([p for _, p in parts], settings, groups=args.groups, refit=args.refit,

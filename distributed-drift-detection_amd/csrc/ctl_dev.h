@@ -42,11 +42,14 @@ __device__ __forceinline__ int64_t window_draws(int64_t W, int64_t dpb_x1024) {
 
 __device__ __forceinline__ int64_t blen(const ddm_ctl_part& p, int64_t b) { return b == p.nb - 1 ? p.last_len : p.pb; }
 
-// The window after a change (BatchRunner._epoch_after): the next concept likely lasts about
-// as long as the one just closed (seg batches), so the window covers seg plus a margin of
-// max(seg >> shift, pad) batches (rule = shift | pad << 8); windows still double after a miss.
-__device__ __forceinline__ int64_t next_window(int64_t seg, int32_t rule) {
-    return seg + max(seg >> (rule & 255), (int64_t)(rule >> 8));
+// The window after a change (BatchRunner._epoch_after, DDMSettings.drift_window): the next
+// concept likely lasts about as long as the one just closed (seg batches), so the window
+// covers seg plus a margin of max(seg >> shift, pad) batches, at least min_win batches unless
+// the concept was short (seg <= short: C5's concepts of 1.5-3 batches repeat, c2's short
+// ones do not) (rule = shift | pad << 8 | short << 16); windows still double after a miss.
+__device__ __forceinline__ int64_t drift_window(int64_t seg, int64_t min_win, int32_t rule) {
+    const int64_t w = seg + max(seg >> (rule & 255), (int64_t)((rule >> 8) & 255));
+    return seg <= (int64_t)(rule >> 16) ? w : max(min_win, w);
 }
 
 // _epoch for one partition: refit bookkeeping (_refit_prep, device branch), the window
@@ -225,7 +228,7 @@ __device__ void commit(const ddm_ctl& c, ddm_ctl_part& p, int i) {
         const int64_t P_at = info[0];               // the staging's: after batch d's shuffle
         p.P = P_at;
         const int64_t seg = d - p.seg_start + 1;
-        p.win = max(p.min_win, next_window(seg, p.win_rule));   // the next concept, with a margin
+        p.win = drift_window(seg, p.min_win, p.win_rule);   // the next concept, with a margin
         p.j = d + 1;
         if (p.j >= p.nb) {
             p.done = 1;

@@ -67,7 +67,7 @@ __device__ void plan_next(const Job& jb, int32_t stop, bool drawn, int64_t p_see
         jn = d + 1;
         Pn = p_seeds;
         g0n = jn + 1;
-        winn = max(jb.min_win, next_window(d - jb.seg_start + 1, jb.win_rule));
+        winn = drift_window(d - jb.seg_start + 1, jb.min_win, jb.win_rule);
         ok = drawn;
     } else {
         jn = jb.b_end;

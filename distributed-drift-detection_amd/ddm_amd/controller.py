@@ -622,7 +622,7 @@ class BatchRunner:
             r["info_out"], r["ev_out"], r["perm_w"], r["seeds_out"] = self._sptr("info", i), self._sptr("ev", i), \
                 perm, self._sptr("seeds", i)
             r["max_win"], r["n_full"], r["min_win"] = self.max_wins[i], self.nbs[i] - (1 if r["last_len"] != pb else 0), \
-                max(1, min(self.s.window_batches, self.s.drift_window_batches))
+                self.s.min_window
             r["dpb_x1024"] = int(np.ceil(expected_draws_per_batch(pb) * 1024))
             r["plan_out"], r["next_job"] = self._sptr("plan", i), self.njobs.d.data_ptr() + i * kernels.JOB_DTYPE.itemsize
             sh = self.shuffles[i]
@@ -781,8 +781,10 @@ class BatchRunner:
             s_.wait_event(ready)
         for s_ in (self.stream, self.gen_stream, self.tab_stream):   # nothing of the last run
             s_.synchronize()                                          # may still read the streams
+        self._mark("streams idle")
         for ps, rng in zip(pss, rngs):
             self.shuffles[ps.i].reset(rng, synced=True)
+        self._mark("MT states uploaded")
         started = []
         try:
             # each partition's whole stream up front (one batched generate + tables);
@@ -1018,7 +1020,7 @@ class BatchRunner:
         _epoch_after: 9/8 of the concept just closed after a change, twice the window
         otherwise)."""
         s = self.s
-        lo = max(1, min(s.window_batches, s.drift_window_batches))
+        lo = s.min_window
         return max(0, min(ps.max_win, ps.nb - ps.j,
                           max(lo, s.next_window(ps.b_end - ps.seg_start) + 1, 2 * ps.win)))
 
@@ -1349,7 +1351,7 @@ class BatchRunner:
                 # one, so the next window covers it with a margin (one epoch per drift when
                 # concepts repeat their length; windows still double after a miss)
                 seg = d - ps.seg_start + 1
-                ps.win = max(max(1, min(s.window_batches, s.drift_window_batches)), s.next_window(seg))
+                ps.win = s.drift_window(seg)
                 ps.j = d + 1
             else:
                 if ps.tail:

@@ -199,7 +199,7 @@ class DeviceController:
         rec[:] = np.zeros(1, CTL)
         base_d = self.parts_d.data_ptr()
         nlog = _OFF["n_log"]
-        lo = max(1, min(r.s.window_batches, r.s.drift_window_batches))
+        lo = r.s.min_window
         for i, part in enumerate(r.parts):
             q = rec[i]
             q["job"] = t["job"][i]
@@ -466,6 +466,7 @@ class DeviceController:
             self.parts_h.copy_(self.parts_d, non_blocking=True)
             r.ctrl_h.copy_(r.ctrl_d, non_blocking=True)        # staging slots and refit results
         r.stream.synchronize()
+        r._mark("records copied")
         rec = self.rec
         epochs = int(rec["epochs"].max()) if len(rec) else 0
         # every partition's event log in one read-back
@@ -476,6 +477,7 @@ class DeviceController:
                     o = int(self.log_off[ps.i])
                     self.logs_h[o:o + 3 * n_log].copy_(self.logs[ps.i][:3 * n_log], non_blocking=True)
         r.stream.synchronize()
+        r._mark("logs copied")
         logs_np = self.logs_h.numpy()
         for ps in live:
             q = rec[ps.i]

@@ -597,8 +597,10 @@ typedef struct ddm_ctl_part {
     int32_t pb, last_len, n_words, dtrees;
     int32_t host_slots;          /* feature slots the host forest reads (statistics) */
     int32_t win_rule;            /* ABI 20: the window after a change covers the concept just
-                                    closed plus max(concept >> (win_rule & 255), win_rule >> 8)
-                                    batches (DDMSettings drift_window_shift / _pad) */
+                                    closed plus max(concept >> (win_rule & 255),
+                                    (win_rule >> 8) & 255) batches, and at least min_win unless
+                                    the concept was at most win_rule >> 16 batches
+                                    (DDMSettings drift_window_shift / _pad / _short) */
     /* dynamic: the host controller's state at the start of an epoch */
     int64_t j, P, win, seg_start, P1, P2, avail;
     int32_t retrain, done, stall, park, forest_dev, applied, idle, pad1;
