@@ -53,6 +53,46 @@ int launch_ctl(const ddm_ctl& c, int entry, hipStream_t s) {
 constexpr int64_t kShufW = 64 * 256, kShufPieces = 256;
 constexpr int32_t kPermBlocks = 256;            // ddm_err_permute_dev blocks per partition
 
+// Cross-stream order without HIP events (ddm_ctl_epoch.sync_flags): the producing stream
+// runs a one-wave kernel that stores a sequence number (agent-scope release, then an sc1
+// store), the consuming stream a one-wave kernel that polls it (sc1 loads, s_sleep between
+// polls) and ends; the data itself is ordered by the kernel boundaries on both sides (the
+// producer's kernels have ended before the store, the consumer's start after the poll).
+// One fork + join this way costs ~12 us against ~30 us with two events
+// (profiles/r04/gap_bench.log).  Every wait is enqueued after the store it waits for, so
+// even streams sharing one hardware queue cannot deadlock; the poll still gives up after
+// ~0.1 s and counts it in flags[2], which voids the phase (ddm_amd/devctl.py raises).
+__global__ __launch_bounds__(64) void k_flag_pub(uint32_t* flag, uint32_t v) {
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+__global__ __launch_bounds__(64) void k_flag_wait(const uint32_t* flag, uint32_t v, uint32_t* timeouts) {
+    if (threadIdx.x == 0) {
+        const uint64_t t0 = wall_clock64();
+        while ((int32_t)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - v) < 0) {
+            __builtin_amdgcn_s_sleep(1);
+            if (wall_clock64() - t0 > 10000000ull) {          // 0.1 s at 100 MHz
+                atomicAdd(timeouts, 1u);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+}
+
+int flag_pub(uint32_t* flags, int k, uint32_t v, hipStream_t s) {
+    hipLaunchKernelGGL(k_flag_pub, dim3(1), dim3(64), 0, s, flags + k, v);
+    return ddm::launch_status("ddm_ctl_epochs/flag");
+}
+
+int flag_wait(uint32_t* flags, int k, uint32_t v, hipStream_t s) {
+    hipLaunchKernelGGL(k_flag_wait, dim3(1), dim3(64), 0, s, flags + k, v, flags + 2);
+    return ddm::launch_status("ddm_ctl_epochs/flag wait");
+}
+
 }  // namespace
 
 extern "C" int ddm_scan_long_reuse(const uint8_t* err, const int64_t* stream_off, const int64_t* stream_end,
@@ -174,7 +214,15 @@ int ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs, bool graph) {
     // the window's shuffle) and waits for the shuffles only before the permutation into DDM
     // order, so the side stream's window shuffles overlap the refit AND the predict
     const bool dec = e->decouple && e->row_order_delta != 0 && c.sync;
+    // fork / join by flags (not inside a graph: a replay would reuse the captured numbers)
+    uint32_t* const flags = graph ? nullptr : e->sync_flags;
+    uint32_t* const seq = e->sync_seq;
+    if (flags && !seq) {
+        ddm::set_error("ddm_ctl_epochs: sync_flags without sync_seq");
+        return DDM_E_ARG;
+    }
     auto join = [&]() {
+        if (flags) return flag_wait(flags, 1, seq[1], s);
         return ddm::hip_status(hipStreamWaitEvent(s, reinterpret_cast<hipEvent_t>(e->join_ev), 0), "join");
     };
     for (int32_t k = 0; k < n_epochs; ++k) {
@@ -232,17 +280,28 @@ int ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs, bool graph) {
         }
         if (int rc = rec(e->ev[5], s)) return rc;
         // the next windows' shuffles beside the refits
-        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(e->fork_ev), s), "fork")) return rc;
-        if (int rc = ddm::hip_status(hipStreamWaitEvent(side, reinterpret_cast<hipEvent_t>(e->fork_ev), 0), "fork"))
-            return rc;
+        if (flags) {
+            ++seq[0];
+            if (int rc = flag_pub(flags, 0, seq[0], s)) return rc;
+            if (int rc = flag_wait(flags, 0, seq[0], side)) return rc;
+        } else {
+            if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(e->fork_ev), s), "fork"))
+                return rc;
+            if (int rc = ddm::hip_status(hipStreamWaitEvent(side, reinterpret_cast<hipEvent_t>(e->fork_ev), 0), "fork"))
+                return rc;
+        }
         if (int rc = rec(e->ev[10], side)) return rc;
         if (int rc = ddm_shuffle_window_batch(c.jobs, c.n, std::min(e->max_W, kShufW),
                                               std::min(e->max_pieces, kShufPieces), e->per_batch, e->side_stream,
                                               nullptr, nullptr))
             return rc;
         if (int rc = rec(e->ev[11], side)) return rc;
-        if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(e->join_ev), side), "join"))
+        if (flags) {
+            ++seq[1];
+            if (int rc = flag_pub(flags, 1, seq[1], side)) return rc;
+        } else if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(e->join_ev), side), "join")) {
             return rc;
+        }
         if (e->n_dfit > 0) {
             if (int rc = rec(e->ev[6], s)) return rc;
             if (int rc = ddm_rf_fit_device_lf(e->dfit_jobs, e->n_dfit, e->max_trees, e->dfit_max_lf, e->stream)) return rc;

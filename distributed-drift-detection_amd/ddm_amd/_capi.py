@@ -12,7 +12,7 @@ import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 # DDM_AMD_LIB: an alternative build of the same library (e.g. an instrumented one)
 LIB_PATH = os.environ.get("DDM_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
@@ -81,7 +81,7 @@ class DdmCtlEpoch(ctypes.Structure):
                 ("long_max_rows", _i64), ("long_scratch", _vp), ("dfit_jobs", _vp), ("n_dfit", _i32),
                 ("max_trees", _i32), ("max_W", _i64), ("max_pieces", _i64), ("dfit_max_lf", _i64),
                 ("ev", _vp * 12), ("row_order_delta", _i64), ("decouple", _i32), ("pad_dc", _i32),
-                ("predict_evs", _vp)]
+                ("predict_evs", _vp), ("sync_flags", _vp), ("sync_seq", _vp)]
 
 # name -> (restype, argtypes); every symbol include/ddm_amd.h declares.
 SIGNATURES = {

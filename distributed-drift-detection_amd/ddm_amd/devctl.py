@@ -45,6 +45,10 @@ DECOUPLE_ROWS = 200_000
 # DDM_CTL_GRAPH=1: each group of epochs is one replayed hipGraph (ddm_ctl_graph_create) instead
 # of ~20 launches and event operations per epoch enqueued from the host
 CTL_GRAPH = os.environ.get("DDM_CTL_GRAPH", "0") not in ("", "0")
+# the epochs' fork (main -> side stream) and join (side -> main) by flags in device memory
+# (ddm_ctl_epoch.sync_flags: a one-wave store / poll kernel pair, ~12 us per epoch) instead
+# of HIP events (~30 us); DDM_CTL_FLAGS=0: events
+CTL_FLAGS = os.environ.get("DDM_CTL_FLAGS", "1") not in ("", "0")
 
 
 class PredictTimer:
@@ -135,6 +139,11 @@ class DeviceController:
         self.seg_log = None          # (segs, res) device copies per epoch when the runner logs predicts
         self.pred_timer = None       # a PredictTimer while the runner times the predict launches
         self.graphs = {}             # (decouple, long_ok) -> captured group of GROUP epochs
+        # fork / join numbers: published on the device, enqueued so far on the host (both
+        # monotonic for the runner's life), and the device's count of waits that gave up
+        self.sync_flags = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.sync_seq = (ctypes.c_uint32 * 2)()
+        self.sync_h = torch.zeros(4, dtype=torch.int32, pin_memory=True)
         self._E = None
 
     # ---------------------------------------------------------------- eligibility
@@ -314,6 +323,9 @@ class DeviceController:
         # HIP cannot time events that a graph records (hipEventElapsedTime: invalid resource
         # handle), so timed predicts keep the launched form
         use_graph = CTL_GRAPH and pt is None and not (timing or logging)
+        flags = CTL_FLAGS and not use_graph
+        E.sync_flags = self.sync_flags.data_ptr() if flags else None
+        E.sync_seq = ctypes.addressof(self.sync_seq) if flags else None
         if use_graph:
             # every launch sequence captured while both streams are idle (a capture joins the
             # side stream through the fork event)
@@ -465,8 +477,13 @@ class DeviceController:
         with torch.cuda.stream(r.stream):
             self.parts_h.copy_(self.parts_d, non_blocking=True)
             r.ctrl_h.copy_(r.ctrl_d, non_blocking=True)        # staging slots and refit results
+            self.sync_h.copy_(self.sync_flags, non_blocking=True)
         r.stream.synchronize()
         r._mark("records copied")
+        if int(self.sync_h[2]):
+            raise RuntimeError(f"{int(self.sync_h[2])} cross-stream flag waits of the device epochs gave up "
+                               "(ddm_ctl_epoch.sync_flags): the epochs' results are void (DDM_CTL_FLAGS=0 "
+                               "orders the streams by events)")
         rec = self.rec
         epochs = int(rec["epochs"].max()) if len(rec) else 0
         # every partition's event log in one read-back

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 20
+#define DDM_AMD_ABI_VERSION 21
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 256) */
@@ -665,6 +665,14 @@ typedef struct ddm_ctl_epoch {
                                                       events recorded right before / after each
                                                       epoch's predict launch (ev[0] / ev[1] are
                                                       used when NULL)                          */
+    uint32_t* sync_flags;                          /* ABI 21: NULL (fork / join by fork_ev /
+                                                      join_ev) or device words [4], zeroed once
+                                                      for the streams' life: [0] / [1] the last
+                                                      fork / join number published, [2] waits
+                                                      that gave up (nonzero voids the results) */
+    uint32_t* sync_seq;                            /* ABI 21: host words [2], the fork / join
+                                                      numbers enqueued so far (advanced by
+                                                      ddm_ctl_epochs; zero with the flags)     */
 } ddm_ctl_epoch;
 int64_t ddm_ctl_part_bytes(void);
 int64_t ddm_ctl_epoch_bytes(void);
