@@ -799,7 +799,9 @@ class BatchRunner:
             # and batch 1's shuffle) come back in ONE copy queued on the generation stream
             # right behind the first piece, ahead of the jumps and the later pieces
             n0 = max(64, 3 * pb) + 3 * pb + s.n_estimators + 64
-            head_h = torch.empty((len(pss), n0), dtype=torch.int32, pin_memory=True)
+            if getattr(self, "_head_h", None) is None or self._head_h.shape != (len(pss), n0):
+                self._head_h = torch.empty((len(pss), n0), dtype=torch.int32, pin_memory=True)
+            head_h = self._head_h            # free: the last run's copy into it has completed
             head_ev = None
             self._mark("head buffer")
             self._ensure_all([(ps.i, min(upto, int(ps.nb * expected_draws_per_batch(pb) * 1.02))) for ps in pss],

@@ -335,8 +335,9 @@ class DeviceController:
                 self._graph(E)
         # the rest of the streams in growing pieces, two more at every poll (all of it up
         # front kept the side streams busy past the last epoch: the run waited ~14 ms for
-        # generation no epoch needed, C3)
-        r._enqueue_rest()
+        # generation no epoch needed, C3); the first two only once the first group is
+        # enqueued (~0.9 ms of host time the first epochs no longer wait for: their windows
+        # are planned within the words already tabulated)
         self._write_records(live)
         with torch.cuda.stream(stream):
             self.pstall.zero_()
@@ -360,6 +361,8 @@ class DeviceController:
                 E.predict_evs = None
             epochs += GROUP
             group += 1
+            if group == 1:
+                r._enqueue_rest()
             with torch.cuda.stream(stream):
                 self.poll_h[slot].copy_(self.parts_d, non_blocking=True)
             ev = torch.cuda.Event()
