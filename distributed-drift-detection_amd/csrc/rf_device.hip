@@ -367,8 +367,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_dfit_prep(const Job* __restric
 }
 
 // ---- k_dfit_trees -------------------------------------------------------------------
-struct WaveLds {
-    uint32_t mt[624];      // raw MT state
+struct TreeLds {            // one tree's build state
     int32_t cnt[kMaxL];    // bootstrap multiplicity
     int16_t key[kMaxL];    // node key of each in-bag row (-1: out of bag)
     uint8_t crow[kMaxL];   // the node's rows in the current feature's order
@@ -382,6 +381,10 @@ struct WaveLds {
     double st_imp[kMaxL];
 };
 
+struct WaveLds : TreeLds {
+    uint32_t mt[624];      // raw MT state (RandomState drawn in the tree kernel itself)
+};
+
 struct Best {
     double proxy, thr, il, ir;
     int feature, pos, ml;
@@ -392,18 +395,19 @@ __device__ __forceinline__ int node_key(int parent, int is_left) {
 }
 
 // The node's rows (key == nk) in ascending order of feature f: crow/cfv[0..n).
-__device__ __forceinline__ int sort_feature(WaveLds& S, const float* __restrict__ X, const uint8_t* __restrict__ order, int L, int F,
-                            int f, int nk, int lane) {
+__device__ __forceinline__ int sort_feature(const int16_t* key, uint8_t* crow, float* cfv,
+                                            const float* __restrict__ X, const uint8_t* __restrict__ order, int L,
+                                            int F, int f, int nk, int lane) {
     int n = 0;
     for (int q0 = 0; q0 < L; q0 += 64) {
         const int q = q0 + lane;
         const int r = q < L ? order[(int64_t)f * L + q] : 0;
-        const bool in = q < L && S.key[r] == nk;
+        const bool in = q < L && key[r] == nk;
         const uint64_t m = __ballot(in);
         if (in) {
             const int p = n + __popcll(m & lanemask_lt(lane));
-            S.crow[p] = (uint8_t)r;
-            S.cfv[p] = X[(int64_t)r * F + f];
+            crow[p] = (uint8_t)r;
+            cfv[p] = X[(int64_t)r * F + f];
         }
         n += __popcll(m);
     }
@@ -411,7 +415,7 @@ __device__ __forceinline__ int sort_feature(WaveLds& S, const float* __restrict_
     return n;
 }
 
-__device__ void swap_feats(WaveLds& S, int a, int b) {
+__device__ void swap_feats(TreeLds& S, int a, int b) {
     const int16_t fa = S.feats[a], fb = S.feats[b];
     wave_sync();
     S.feats[a] = fb;
@@ -419,8 +423,94 @@ __device__ void swap_feats(WaveLds& S, int a, int b) {
     wave_sync();
 }
 
+// The best split position of one feature (rf_fit.cpp Builder::node_split, the body for one
+// feature that is not constant): the node's n rows in the feature's order in crow / cfv.
+// Every split position p in [1, n): left = positions [0, p).  Lane owns positions
+// lane + 64k; the class weights left of every position come from one wave prefix sum per
+// class present in the node (exact integers; an absent class adds 0 to every sum), summed
+// into sum-of-squares per position.  pos < 0: no split position.
+struct FeatBest {
+    double mx, thr, il, ir;
+    int pos, ml;
+};
+
+__device__ __forceinline__ FeatBest eval_feature(const uint8_t* crow, const float* cfv, const int32_t* cnt,
+                                                 const int32_t* ccnt, const uint8_t* __restrict__ yidx, int n, int K,
+                                                 double wn_node, int lane) {
+    constexpr int kR = kMaxL / 64;
+    int wq[kR], cq[kR], wl[kR], sql[kR], sqr[kR];
+    int carry = 0;
+#pragma unroll
+    for (int k = 0; k < kR; ++k) {
+        const int q = 64 * k + lane;
+        const bool inq = q < n;
+        const int r = inq ? crow[q] : 0;
+        wq[k] = inq ? cnt[r] : 0;
+        cq[k] = inq ? (int)yidx[r] : -1;
+        const int incl = wave_scan_i(wq[k], lane);
+        wl[k] = carry + incl - wq[k];
+        carry += __shfl(incl, 63, 64);
+        sql[k] = 0;
+        sqr[k] = 0;
+    }
+    for (int c = 0; c < K; ++c) {
+        const int tot = ccnt[c];
+        if (tot == 0) continue;
+        int cc = 0;
+#pragma unroll
+        for (int k = 0; k < kR; ++k) {
+            if (64 * k >= n) break;
+            const int v = cq[k] == c ? wq[k] : 0;
+            const int incl = wave_scan_i(v, lane);
+            const int sl = cc + incl - v;
+            const int sr = tot - sl;
+            sql[k] += sl * sl;
+            sqr[k] += sr * sr;
+            cc += __shfl(incl, 63, 64);
+        }
+    }
+    double bp = -INFINITY, bil = 0.0, bir = 0.0;
+    int bpos = -1;
+#pragma unroll
+    for (int k = 0; k < kR; ++k) {
+        const int q = 64 * k + lane;
+        const bool cand = q < n && q >= 1 && !(cfv[q] <= cfv[q - 1] + kFeatureThreshold);
+        if (cand) {
+            const double dwl = (double)wl[k], dwr = wn_node - dwl;
+            const double il = 1.0 - (double)sql[k] / (dwl * dwl);
+            const double ir = 1.0 - (double)sqr[k] / (dwr * dwr);
+            const double proxy = (-dwr * ir) - dwl * il;
+            if (proxy > bp) {                   // positions ascend within a lane
+                bp = proxy;
+                bpos = q;
+                bil = il;
+                bir = ir;
+            }
+        }
+    }
+    // first maximum over the wave: the largest proxy, then the smallest position
+    double mx = bp;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    int mpos = (bpos >= 0 && bp == mx) ? bpos : 0x7fffffff;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mpos = min(mpos, __shfl_xor(mpos, o, 64));
+    FeatBest r{mx, 0.0, 0.0, 0.0, -1, 0};
+    if (mpos != 0x7fffffff) {
+        const int src = mpos & 63;                // the lane that owns position mpos
+        r.pos = mpos;
+        r.il = __shfl(bil, src, 64);
+        r.ir = __shfl(bir, src, 64);
+        double thr = (double)cfv[mpos - 1] / 2.0 + (double)cfv[mpos] / 2.0;
+        if (thr == (double)cfv[mpos] || thr == INFINITY || thr == -INFINITY) thr = (double)cfv[mpos - 1];
+        r.thr = thr;
+        r.ml = mpos > n - mpos ? 1 : 0;
+    }
+    return r;
+}
+
 // node_split_best without missing values (rf_fit.cpp Builder::node_split).
-__device__ __forceinline__ Best node_split(WaveLds& S, const float* __restrict__ X, const uint8_t* __restrict__ order,
+__device__ __forceinline__ Best node_split(TreeLds& S, const float* __restrict__ X, const uint8_t* __restrict__ order,
                            const uint8_t* __restrict__ yidx, int L, int F, int K, int max_features, int nk,
                            int n_node, double wn_node, uint32_t& rstate, int& n_const, int lane) {
     Best best{-INFINITY, 0.0, INFINITY, INFINITY, 0, -1, 0};
@@ -438,7 +528,7 @@ __device__ __forceinline__ Best node_split(WaveLds& S, const float* __restrict__
         }
         f_j += n_found_c;
         const int feature = S.feats[f_j];
-        const int n = sort_feature(S, X, order, L, F, feature, nk, lane);
+        const int n = sort_feature(S.key, S.crow, S.cfv, X, order, L, F, feature, nk, lane);
         if (n == 0 || S.cfv[n - 1] <= S.cfv[0] + kFeatureThreshold) {
             swap_feats(S, f_j, n_total_c);
             ++n_found_c;
@@ -447,77 +537,15 @@ __device__ __forceinline__ Best node_split(WaveLds& S, const float* __restrict__
         }
         --f_i;
         swap_feats(S, f_i, f_j);
-        // every split position p in [1, n): left = positions [0, p).  Lane owns positions
-        // lane + 64k; the class weights left of every position come from one wave prefix
-        // sum per class (exact integers), accumulated into sum-of-squares per position.
-        constexpr int kR = kMaxL / 64;
-        int wq[kR], cq[kR], wl[kR], sql[kR], sqr[kR];
-        int carry = 0;
-#pragma unroll
-        for (int k = 0; k < kR; ++k) {
-            const int q = 64 * k + lane;
-            const bool inq = q < n;
-            const int r = inq ? S.crow[q] : 0;
-            wq[k] = inq ? S.cnt[r] : 0;
-            cq[k] = inq ? (int)yidx[r] : -1;
-            const int incl = wave_scan_i(wq[k], lane);
-            wl[k] = carry + incl - wq[k];
-            carry += __shfl(incl, 63, 64);
-            sql[k] = 0;
-            sqr[k] = 0;
-        }
-        for (int c = 0; c < K; ++c) {
-            int cc = 0;
-            const int tot = S.ccnt[c];
-#pragma unroll
-            for (int k = 0; k < kR; ++k) {
-                if (64 * k >= n) break;
-                const int v = cq[k] == c ? wq[k] : 0;
-                const int incl = wave_scan_i(v, lane);
-                const int sl = cc + incl - v;
-                const int sr = tot - sl;
-                sql[k] += sl * sl;
-                sqr[k] += sr * sr;
-                cc += __shfl(incl, 63, 64);
-            }
-        }
-        double bp = -INFINITY, bil = 0.0, bir = 0.0;
-        int bpos = -1;
-#pragma unroll
-        for (int k = 0; k < kR; ++k) {
-            const int q = 64 * k + lane;
-            const bool cand = q < n && q >= 1 && !(S.cfv[q] <= S.cfv[q - 1] + kFeatureThreshold);
-            if (cand) {
-                const double dwl = (double)wl[k], dwr = wn_node - dwl;
-                const double il = 1.0 - (double)sql[k] / (dwl * dwl);
-                const double ir = 1.0 - (double)sqr[k] / (dwr * dwr);
-                const double proxy = (-dwr * ir) - dwl * il;
-                if (proxy > bp) {                   // positions ascend within a lane
-                    bp = proxy;
-                    bpos = q;
-                    bil = il;
-                    bir = ir;
-                }
-            }
-        }
-        // first maximum over the wave: the largest proxy, then the smallest position
-        double mx = bp;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
-        int mpos = (bpos >= 0 && bp == mx) ? bpos : 0x7fffffff;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) mpos = min(mpos, __shfl_xor(mpos, o, 64));
-        if (mpos != 0x7fffffff && mx > best.proxy) {
-            const int src = mpos & 63;                // the lane that owns position mpos
-            best.proxy = mx;
-            best.pos = mpos;
+        const FeatBest fb = eval_feature(S.crow, S.cfv, S.cnt, S.ccnt, yidx, n, K, wn_node, lane);
+        if (fb.pos >= 0 && fb.mx > best.proxy) {
+            best.proxy = fb.mx;
+            best.pos = fb.pos;
             best.feature = feature;
-            best.il = __shfl(bil, src, 64);
-            best.ir = __shfl(bir, src, 64);
-            double thr = (double)S.cfv[mpos - 1] / 2.0 + (double)S.cfv[mpos] / 2.0;
-            if (thr == (double)S.cfv[mpos] || thr == INFINITY || thr == -INFINITY) thr = (double)S.cfv[mpos - 1];
-            best.thr = thr;
-            best.ml = mpos > n - mpos ? 1 : 0;
+            best.il = fb.il;
+            best.ir = fb.ir;
+            best.thr = fb.thr;
+            best.ml = fb.ml;
         }
     }
     // features[0:n_known_c] = constant[0:n_known_c];
@@ -530,9 +558,11 @@ __device__ __forceinline__ Best node_split(WaveLds& S, const float* __restrict__
     return best;
 }
 
-__device__ __forceinline__ void build_tree(const Job& jb, const Layout& lo, int tree, int K, WaveLds& S, int lane,
+// One tree, one wave; mt: RandomState drawn here (boot == nullptr, the fused kernel).
+__device__ __forceinline__ void build_tree(const Job& jb, const Layout& lo, int tree, int K, TreeLds& S, int lane,
                                            const float* __restrict__ X, const uint8_t* __restrict__ order,
-                                           const uint8_t* __restrict__ yidx, const int32_t* __restrict__ boot) {
+                                           const uint8_t* __restrict__ yidx, const int32_t* __restrict__ boot,
+                                           uint32_t* mt) {
     const int L = jb.L, F = jb.F;
     const int64_t M = 2 * (int64_t)L - 1;
     TNode* nodes = reinterpret_cast<TNode*>(jb.scratch + lo.tnodes) + tree * M;
@@ -551,7 +581,7 @@ __device__ __forceinline__ void build_tree(const Job& jb, const Layout& lo, int 
         rstate = (uint32_t)bt[0];
         wave_sync();
     } else {
-        rstate = tree_boot((uint32_t)jb.seeds[tree], L, S.mt, S.cnt, lane);
+        rstate = tree_boot((uint32_t)jb.seeds[tree], L, mt, S.cnt, lane);
     }
 #ifdef DDM_DFIT_PROFILE
     const uint64_t t_a1 = wall_clock64();
@@ -774,7 +804,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfit_trees(const Job* __restric
         int K = 0;
         if (!fused_prep<true>(jb, s_X, s_ord, s_yi, K)) return;
         const Layout lo = layout(jb.L, jb.F, jb.n_trees, jb.k_cap);
-        if (tree < jb.n_trees) build_tree(jb, lo, tree, K, lds[w], lane, s_X, s_ord, s_yi, nullptr);
+        if (tree < jb.n_trees) build_tree(jb, lo, tree, K, lds[w], lane, s_X, s_ord, s_yi, nullptr, lds[w].mt);
         return;
     }
     if (gated_off(jb) || jb.result[DDM_DFIT_STATUS] != 0) return;
@@ -791,9 +821,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfit_trees(const Job* __restric
         }
         for (int e = threadIdx.x; e < jb.L; e += 64 * kWaves) s_yi[e] = yidx[e];
         __syncthreads();
-        if (tree < jb.n_trees) build_tree(jb, lo, tree, K, lds[w], lane, s_X, s_ord, s_yi, boot);
+        if (tree < jb.n_trees) build_tree(jb, lo, tree, K, lds[w], lane, s_X, s_ord, s_yi, boot, nullptr);
     } else if (tree < jb.n_trees) {
-        build_tree(jb, lo, tree, K, lds[w], lane, jb.X, order, yidx, boot);
+        build_tree(jb, lo, tree, K, lds[w], lane, jb.X, order, yidx, boot, nullptr);
     }
 }
 

@@ -13,11 +13,21 @@ from ddm_amd.dfit import DeviceTrainer  # noqa: E402
 
 rng = np.random.default_rng(3)
 batches = []
-for k in range(8):
-    y = np.where(np.arange(100) < 60, 3, 4)
-    X = rng.random((100, 27), dtype=np.float32) + (y[:, None] == 4) * (10.0 if "stumps" in sys.argv else 0.5)
-    batches.append((X.astype(np.float32), y, rng.integers(0, 2**31 - 1, 100)))
-tr = DeviceTrainer(100, 16, torch.device("cuda", 0))
+if "outdoor" in sys.argv:
+    # c2-like: 16 partitions (row % 16) of the reference's outdoorStream rows, one 100-row
+    # batch each (shuffled), ~9 classes per batch
+    d = np.load("tests/golden/outdoor.npz", allow_pickle=False)
+    Xo, yo = d["X"].astype(np.float32), d["target"].astype(np.int64)
+    for k in range(16):
+        rows = np.arange(k, len(yo), 16)[:100]
+        rows = rows[rng.permutation(len(rows))]
+        batches.append((Xo[rows], yo[rows], rng.integers(0, 2**31 - 1, 100)))
+else:
+    for k in range(8):
+        y = np.where(np.arange(100) < 60, 3, 4)
+        X = rng.random((100, 27), dtype=np.float32) + (y[:, None] == 4) * (10.0 if "stumps" in sys.argv else 0.5)
+        batches.append((X.astype(np.float32), y, rng.integers(0, 2**31 - 1, 100)))
+tr = DeviceTrainer(100, 64, torch.device("cuda", 0), fused="fused" in sys.argv)
 for rep in range(3):
     t = time.perf_counter()
     out = tr.fit_many(batches)
