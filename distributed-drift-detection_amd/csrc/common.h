@@ -22,4 +22,25 @@ inline hipStream_t as_hip(ddm_stream_t s) { return reinterpret_cast<hipStream_t>
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Cross-stream order by a sequence number in device memory (ddm_ctl_epoch.sync_flags):
+// the producer's data are released (agent scope) before the number is stored; a poll ends
+// when the number reaches v, or gives up after ~0.1 s and counts that in *timeouts.  One
+// thread each.
+__device__ inline void flag_publish(uint32_t* flag, uint32_t v) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ inline void flag_poll(const uint32_t* flag, uint32_t v, uint32_t* timeouts) {
+    const uint64_t t0 = wall_clock64();
+    while ((int32_t)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - v) < 0) {
+        __builtin_amdgcn_s_sleep(1);
+        if (wall_clock64() - t0 > 10000000ull) {            // 0.1 s at 100 MHz
+            atomicAdd(timeouts, 1u);
+            break;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
 }  // namespace ddm

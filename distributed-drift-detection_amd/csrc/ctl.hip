@@ -53,34 +53,25 @@ int launch_ctl(const ddm_ctl& c, int entry, hipStream_t s) {
 constexpr int64_t kShufW = 64 * 256, kShufPieces = 256;
 constexpr int32_t kPermBlocks = 256;            // ddm_err_permute_dev blocks per partition
 
-// Cross-stream order without HIP events (ddm_ctl_epoch.sync_flags): the producing stream
-// runs a one-wave kernel that stores a sequence number (agent-scope release, then an sc1
-// store), the consuming stream a one-wave kernel that polls it (sc1 loads, s_sleep between
-// polls) and ends; the data itself is ordered by the kernel boundaries on both sides (the
-// producer's kernels have ended before the store, the consumer's start after the poll).
-// One fork + join this way costs ~12 us against ~30 us with two events
-// (profiles/r04/gap_bench.log).  Every wait is enqueued after the store it waits for, so
-// even streams sharing one hardware queue cannot deadlock; the poll still gives up after
+// Cross-stream order without HIP events (ddm_ctl_epoch.sync_flags, common.h flag_publish /
+// flag_poll): the producing stream stores a sequence number after its data (agent-scope
+// release, then an sc1 store), the consuming stream polls it (sc1 loads, s_sleep between
+// polls); the data are ordered by kernel boundaries (the consumer's kernels start after
+// the poll).  The fork is stored by the last workgroup of k_stage_ctl itself and polled by
+// a one-wave kernel at the head of the side stream; the side stream stores the join after
+// its shuffles (a one-wave kernel), and in coupled epochs the refit's pack kernel polls it
+// (one thread of workgroup 0, after its job), so the next predict starts right after the
+// pack; decoupled epochs poll it by a one-wave kernel before the permutation.  A fork +
+// join by one-wave kernels costs ~12 us against ~30 us with two events
+// (profiles/r04/gap_bench.log).  Every poll is enqueued after the store it waits for, so
+// even streams sharing one hardware queue cannot deadlock; a poll still gives up after
 // ~0.1 s and counts it in flags[2], which voids the phase (ddm_amd/devctl.py raises).
 __global__ __launch_bounds__(64) void k_flag_pub(uint32_t* flag, uint32_t v) {
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (threadIdx.x == 0) ddm::flag_publish(flag, v);
 }
 
 __global__ __launch_bounds__(64) void k_flag_wait(const uint32_t* flag, uint32_t v, uint32_t* timeouts) {
-    if (threadIdx.x == 0) {
-        const uint64_t t0 = wall_clock64();
-        while ((int32_t)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - v) < 0) {
-            __builtin_amdgcn_s_sleep(1);
-            if (wall_clock64() - t0 > 10000000ull) {          // 0.1 s at 100 MHz
-                atomicAdd(timeouts, 1u);
-                break;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
+    if (threadIdx.x == 0) ddm::flag_poll(flag, v, timeouts);
 }
 
 int flag_pub(uint32_t* flags, int k, uint32_t v, hipStream_t s) {
@@ -108,6 +99,11 @@ extern "C" int ddm_err_permute_dev(const ddm_predict_segment* segs_dev, int32_t 
 extern "C" int ddm_epoch_stage_ctl(const ddm_stage_job* jobs_dev, const ddm_shuffle_job* shuffle_jobs,
                                    const ddm_ctl* ctl, const uint8_t* err, const ddm_params* prm,
                                    const uint8_t* perm_map, ddm_stream_t stream);
+int epoch_stage_ctl_pub(const ddm_stage_job* jobs_dev, const ddm_shuffle_job* shuffle_jobs, const ddm_ctl* ctl,
+                        const uint8_t* err, const ddm_params* prm, const uint8_t* perm_map, uint32_t* pub_flag,
+                        uint32_t pub_v, ddm_stream_t stream);
+int rf_fit_device_join(const ddm_dfit_job* jobs_dev, int32_t n_jobs, int32_t max_trees, int64_t max_lf,
+                       const uint32_t* join_flag, uint32_t join_v, uint32_t* timeouts, ddm_stream_t stream);
 
 namespace {
 
@@ -222,7 +218,11 @@ int ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs, bool graph) {
         return DDM_E_ARG;
     }
     auto join = [&]() {
-        if (flags) return flag_wait(flags, 1, seq[1], s);
+        if (flags) {
+            if (seq[2] == seq[1]) return 0;           // a pack kernel held the last one already
+            seq[2] = seq[1];
+            return flag_wait(flags, 1, seq[1], s);
+        }
         return ddm::hip_status(hipStreamWaitEvent(s, reinterpret_cast<hipEvent_t>(e->join_ev), 0), "join");
     };
     for (int32_t k = 0; k < n_epochs; ++k) {
@@ -269,7 +269,8 @@ int ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs, bool graph) {
             if (int rc = rec(e->ev[4], s)) return rc;
             ddm_ctl cd = c;
             cd.decoupled = dec ? 1 : 0;
-            if (int rc = ddm_epoch_stage_ctl(c.stage, c.jobs, &cd, e->err, e->params, e->perm_map, e->stream))
+            if (int rc = epoch_stage_ctl_pub(c.stage, c.jobs, &cd, e->err, e->params, e->perm_map,
+                                             flags ? flags : nullptr, flags ? seq[0] + 1 : 0, e->stream))
                 return rc;
         } else {
             if (int rc = ddm_shuffle_pick_batch(c.jobs, c.n, e->stream)) return rc;
@@ -282,7 +283,8 @@ int ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs, bool graph) {
         // the next windows' shuffles beside the refits
         if (flags) {
             ++seq[0];
-            if (int rc = flag_pub(flags, 0, seq[0], s)) return rc;
+            if (!c.sync)                            // k_stage_ctl stores it itself
+                if (int rc = flag_pub(flags, 0, seq[0], s)) return rc;
             if (int rc = flag_wait(flags, 0, seq[0], side)) return rc;
         } else {
             if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(e->fork_ev), s), "fork"))
@@ -304,7 +306,13 @@ int ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs, bool graph) {
         }
         if (e->n_dfit > 0) {
             if (int rc = rec(e->ev[6], s)) return rc;
-            if (int rc = ddm_rf_fit_device_lf(e->dfit_jobs, e->n_dfit, e->max_trees, e->dfit_max_lf, e->stream)) return rc;
+            // coupled epochs: the pack kernel holds the join, the next predict needs no poll
+            const bool hold = flags && !dec;
+            if (int rc = rf_fit_device_join(e->dfit_jobs, e->n_dfit, e->max_trees, e->dfit_max_lf,
+                                            hold ? flags + 1 : nullptr, hold ? seq[1] : 0, flags ? flags + 2 : nullptr,
+                                            e->stream))
+                return rc;
+            if (hold) seq[2] = seq[1];
             if (int rc = rec(e->ev[7], s)) return rc;
         }
     }

@@ -1249,9 +1249,7 @@ __device__ void pack_tree(const TNode* tn, int m, int16_t* new_id, int16_t* queu
     }
 }
 
-__global__ __launch_bounds__(kPackThreads) void k_dfit_pack(const Job* __restrict__ jobs) {
-    refit_priority();
-    const Job jb = jobs[blockIdx.x];
+__device__ __forceinline__ void pack_job(const Job& jb) {
 #ifdef DDM_DFIT_PROFILE
     const uint64_t t_pack0 = wall_clock64();
 #endif
@@ -1318,7 +1316,20 @@ __global__ __launch_bounds__(kPackThreads) void k_dfit_pack(const Job* __restric
     }
 }
 
+// join_flag: one thread of workgroup 0 polls it after its job (ctl.hip: the side stream's
+// shuffles of the next window, which the next predict reads), so the kernel ends only once
+// they are done.
+__global__ __launch_bounds__(kPackThreads) void k_dfit_pack(const Job* __restrict__ jobs, const uint32_t* join_flag,
+                                                            uint32_t join_v, uint32_t* timeouts) {
+    refit_priority();
+    pack_job(jobs[blockIdx.x]);
+    if (join_flag && blockIdx.x == 0 && threadIdx.x == 0) ddm::flag_poll(join_flag, join_v, timeouts);
+}
+
 }  // namespace
+
+int rf_fit_device_join(const ddm_dfit_job* jobs_dev, int32_t n_jobs, int32_t max_trees, int64_t max_lf,
+                       const uint32_t* join_flag, uint32_t join_v, uint32_t* timeouts, ddm_stream_t stream);
 
 extern "C" int64_t ddm_rf_device_scratch_bytes(int32_t L, int32_t F, int32_t n_trees, int32_t k_cap) {
     if (L < 1 || F < 1 || n_trees < 1 || k_cap < 1) return 0;
@@ -1327,7 +1338,14 @@ extern "C" int64_t ddm_rf_device_scratch_bytes(int32_t L, int32_t F, int32_t n_t
 
 extern "C" int ddm_rf_fit_device_lf(const ddm_dfit_job* jobs_dev, int32_t n_jobs, int32_t max_trees, int64_t max_lf,
                                     ddm_stream_t stream) {
-    if (!jobs_dev || n_jobs < 0 || max_trees < 1 || max_trees > 256) {
+    return rf_fit_device_join(jobs_dev, n_jobs, max_trees, max_lf, nullptr, 0, nullptr, stream);
+}
+
+// The same; join_flag != NULL: the pack kernel ends only once *join_flag reaches join_v
+// (ctl.hip), n_jobs >= 1.
+int rf_fit_device_join(const ddm_dfit_job* jobs_dev, int32_t n_jobs, int32_t max_trees, int64_t max_lf,
+                       const uint32_t* join_flag, uint32_t join_v, uint32_t* timeouts, ddm_stream_t stream) {
+    if (!jobs_dev || n_jobs < 0 || max_trees < 1 || max_trees > 256 || (join_flag && (!timeouts || n_jobs < 1))) {
         ddm::set_error("ddm_rf_fit_device: invalid argument");
         return DDM_E_ARG;
     }
@@ -1344,7 +1362,7 @@ extern "C" int ddm_rf_fit_device_lf(const ddm_dfit_job* jobs_dev, int32_t n_jobs
                        dim3((unsigned)ddm::ceil_div(max_trees, kWaves), (unsigned)n_jobs), dim3(64 * kWaves), 0, s,
                        jobs);
     if (int rc = ddm::launch_status("ddm_rf_fit_device/trees")) return rc;
-    hipLaunchKernelGGL(k_dfit_pack, dim3((unsigned)n_jobs), dim3(kPackThreads), 0, s, jobs);
+    hipLaunchKernelGGL(k_dfit_pack, dim3((unsigned)n_jobs), dim3(kPackThreads), 0, s, jobs, join_flag, join_v, timeouts);
     return ddm::launch_status("ddm_rf_fit_device/pack");
 }
 

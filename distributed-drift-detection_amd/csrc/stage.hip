@@ -385,6 +385,8 @@ struct FoldScan {
     const uint8_t* err;
     const uint8_t* perm_map;
     ddm_params P;
+    uint32_t* pub;           // non-null: the last workgroup stores pub_v there (ctl.hip's fork)
+    uint32_t pub_v;
 };
 
 // The device-resident runner's epoch tail in one launch, a workgroup per partition: the
@@ -441,10 +443,15 @@ __global__ __launch_bounds__(kStageThreads) void k_stage_ctl(const Job* __restri
         __threadfence();
         ctl_split(c);
         c.sync[0] = 0;                              // the ticket, for the next epoch
-    }
+        if (fs.pub) ddm::flag_publish(fs.pub, fs.pub_v);   // the fork (ctl.hip): every block's
+    }                                                       // records are released before its ticket
 }
 
 }  // namespace
+
+int epoch_stage_ctl_pub(const ddm_stage_job* jobs_dev, const ddm_shuffle_job* shuffle_jobs, const ddm_ctl* ctl,
+                        const uint8_t* err, const ddm_params* prm, const uint8_t* perm_map, uint32_t* pub_flag,
+                        uint32_t pub_v, ddm_stream_t stream);
 
 // err != NULL: the kernel also runs the epoch's one-lane DDM scan (mode 0) on err with the
 // params and perm_map given.
@@ -455,7 +462,18 @@ extern "C" int ddm_epoch_stage_ctl(const ddm_stage_job* jobs_dev, const ddm_shuf
         ddm::set_error("ddm_epoch_stage_ctl: invalid argument");
         return DDM_E_ARG;
     }
-    FoldScan fs{err, perm_map, {}};
+    return epoch_stage_ctl_pub(jobs_dev, shuffle_jobs, ctl, err, prm, perm_map, nullptr, 0, stream);
+}
+
+// The same, storing pub_v into *pub_flag once every record is written (ctl.hip's fork).
+int epoch_stage_ctl_pub(const ddm_stage_job* jobs_dev, const ddm_shuffle_job* shuffle_jobs, const ddm_ctl* ctl,
+                        const uint8_t* err, const ddm_params* prm, const uint8_t* perm_map, uint32_t* pub_flag,
+                        uint32_t pub_v, ddm_stream_t stream) {
+    if (!jobs_dev || !shuffle_jobs || !ctl || !ctl->sync || ctl->n <= 0 || (err && (!prm || prm->per_batch <= 0))) {
+        ddm::set_error("ddm_epoch_stage_ctl: invalid argument");
+        return DDM_E_ARG;
+    }
+    FoldScan fs{err, perm_map, {}, pub_flag, pub_v};
     if (err) fs.P = *prm;
     hipLaunchKernelGGL(k_stage_ctl, dim3((unsigned)ctl->n), dim3(kStageThreads), 0, ddm::as_hip(stream),
                        reinterpret_cast<const Job*>(jobs_dev), shuffle_jobs, *ctl, fs);

@@ -142,7 +142,7 @@ class DeviceController:
         # fork / join numbers: published on the device, enqueued so far on the host (both
         # monotonic for the runner's life), and the device's count of waits that gave up
         self.sync_flags = torch.zeros(4, dtype=torch.int32, device=dev)
-        self.sync_seq = (ctypes.c_uint32 * 2)()
+        self.sync_seq = (ctypes.c_uint32 * 3)()
         self.sync_h = torch.zeros(4, dtype=torch.int32, pin_memory=True)
         self._E = None
 

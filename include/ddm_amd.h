@@ -670,9 +670,10 @@ typedef struct ddm_ctl_epoch {
                                                       for the streams' life: [0] / [1] the last
                                                       fork / join number published, [2] waits
                                                       that gave up (nonzero voids the results) */
-    uint32_t* sync_seq;                            /* ABI 21: host words [2], the fork / join
-                                                      numbers enqueued so far (advanced by
-                                                      ddm_ctl_epochs; zero with the flags)     */
+    uint32_t* sync_seq;                            /* ABI 21: host words [3], the fork / join
+                                                      numbers enqueued so far and the last
+                                                      join the epoch stream polled (advanced
+                                                      by ddm_ctl_epochs; zero with the flags)  */
 } ddm_ctl_epoch;
 int64_t ddm_ctl_part_bytes(void);
 int64_t ddm_ctl_epoch_bytes(void);
