@@ -62,6 +62,10 @@ def carried_exact(st):
 # waits only for the piece holding the draws it reads, so the generator (one sequential
 # recurrence per partition) runs ahead of the epochs instead of holding them to its end.
 GEN_PIECE_MAX = int(os.environ.get("DDM_GEN_PIECE", 1 << 25))
+# the smallest piece after the first: a piece's latency (jumps, one <= 2^20-draw segment per
+# workgroup, its tables) hardly depends on its size, so the doubling starts at 8M draws
+# (C3: the first ~25 epochs waited for pieces of 1M, 2M, 4M ... one after the other)
+GEN_PIECE_MIN = int(os.environ.get("DDM_GEN_PIECE_MIN", 1 << 23))
 
 
 def _round_up(n, m):
@@ -1039,7 +1043,7 @@ class BatchRunner:
         for _ in range(2):
             if upto >= total:
                 break
-            upto = min(total, upto + min(upto, GEN_PIECE_MAX))
+            upto = min(total, upto + min(max(upto, GEN_PIECE_MIN), GEN_PIECE_MAX))
             self._ensure_all([(ps.i, min(upto, int(ps.nb * expected_draws_per_batch(pb) * 1.02))) for ps in pss],
                              wait=False)
             self._mark(f"piece to {upto}")

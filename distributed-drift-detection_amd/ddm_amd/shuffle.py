@@ -250,8 +250,11 @@ class GpuShuffle:
         reqs = np.empty(0, dtype=kernels.GEN_DTYPE)
         if target > self.gen:
             s_last = self._segments_for(target - 1) - 1
-            if s_last >= 1:                 # every segment of the expected stream at once
-                self._jump_to(max(s_last + 1, self.n_seg), jumps)
+            if s_last >= 1:
+                # the segments this piece reaches (all of the expected stream at once was one
+                # ~4 ms launch of 1,952 jumps for C3 that held up the first pieces and the
+                # first epochs beside it)
+                self._jump_to(s_last + 1, jumps)
             s0 = self._segments_for(self.gen) - 1 if self.gen else 0
             seg = np.arange(s0, s_last + 1, dtype=np.int64)
             starts = np.where(seg == 0, 0, (624 - self.init_pos) + seg * JUMP)
