@@ -109,9 +109,10 @@ def parse():
     ap.add_argument("--drift-short", type=int, default=-1,
                     help="concepts of at most this many batches skip that floor (-1: DDMSettings' default)")
     ap.add_argument("--predict-timing", type=int, default=-1,
-                    help="HIP events around every predict launch of the timed steps (the roofline's in-step time); "
-                         "-1: on for c3/c3w (about 7 us of queue time per event, ~2%% of a C3 step), off for the "
-                         "latency-bound c2/c5 epochs (8%% of a C5 step), whose kernel times then come from an "
+                    help="device-clock stamps of every predict launch of the timed steps (the roofline's in-step "
+                         "time: each launch's span from its first workgroup's start to its last one's end, folded "
+                         "by the staging kernel after it); -1: on for c3/c3w, off for the latency-bound c2/c5 "
+                         "epochs (a few us of each ~120-us C5 epoch), whose kernel times then come from an "
                          "instrumented step after the timed ones")
     ap.add_argument("--predict-replays", type=int, default=0,
                     help="isolated back-to-back replays of the last timed step's predict tables (a side figure; "
@@ -600,10 +601,12 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
                                      "only; decoupled epochs leave the permutation to k_err_permute)",
                 "alg_bytes_per_launch": bytes_launch, "avg_launch_ms": avg_ms, "avg_rows_per_launch": rows_per_launch,
                 "launches": agg["predict_dev_launches"], "decoupled_row_fraction": dec_frac,
-                "launch_timing": ("HIP events on the epoch stream around every device-epoch predict launch of the "
-                                  "timed steps (launches with no rows -- epochs enqueued after a run's last active "
-                                  "one -- included, as in a rocprofv3 average; the run's first, host-planned epoch "
-                                  "is a different kernel and excluded)" if agg["predict_dev_launches"] else
+                "launch_timing": ("the device clock (100 MHz) over every device-epoch predict launch of the timed "
+                                  "steps, from the launch's first workgroup start to its last workgroup end "
+                                  "(ddm_ctl.predict_clock; launches with no rows -- epochs enqueued after a run's "
+                                  "last active one -- included, as in a rocprofv3 average; the run's first, "
+                                  "host-planned epoch is a different kernel and excluded)"
+                                  if agg["predict_dev_launches"] else
                                   "HIP events around each epoch's predict in one instrumented step after the timed "
                                   "ones (no events in the timed steps: --predict-timing 0)"),
                 "isolated_replay": {"avg_launch_ms": replay_ms if replay_n else None, "launches": replay_n,

@@ -93,7 +93,9 @@ extern "C" int ddm_scan_long_reuse(const uint8_t* err, const int64_t* stream_off
                                    ddm_stream_t stream);
 extern "C" int ddm_forest_predict_dev_orig(const ddm_predict_segment* segs_dev, const int64_t* const* res_dev,
                                            int32_t n_segs, int32_t per_batch, int64_t grid, int32_t* stall,
-                                           int64_t delta, ddm_stream_t stream);
+                                           int64_t delta, uint64_t* clk, ddm_stream_t stream);
+int forest_predict_dev_clk(const ddm_predict_segment* segs_dev, const int64_t* const* res_dev, int32_t n_segs,
+                           int32_t per_batch, int64_t grid, int32_t* stall, uint64_t* clk, ddm_stream_t stream);
 extern "C" int ddm_err_permute_dev(const ddm_predict_segment* segs_dev, int32_t n_segs, int32_t per_batch,
                                    int64_t delta, int32_t blocks_per_seg, ddm_stream_t stream);
 extern "C" int ddm_epoch_stage_ctl(const ddm_stage_job* jobs_dev, const ddm_shuffle_job* shuffle_jobs,
@@ -217,6 +219,8 @@ int ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs, bool graph) {
         ddm::set_error("ddm_ctl_epochs: sync_flags without sync_seq");
         return DDM_E_ARG;
     }
+    // the predict's device-clock stamps are folded by k_stage_ctl: only with the fused tail
+    uint64_t* const clk = c.sync ? c.predict_clock : nullptr;
     auto join = [&]() {
         if (flags) {
             if (seq[2] == seq[1]) return 0;           // a pack kernel held the last one already
@@ -234,11 +238,11 @@ int ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs, bool graph) {
         if (int rc = rec(pb0, s)) return rc;
         if (dec) {
             if (int rc = ddm_forest_predict_dev_orig(c.segs, c.seg_res, c.n, e->per_batch, c.predict_blocks, c.pstall,
-                                                     e->row_order_delta, e->stream))
+                                                     e->row_order_delta, clk, e->stream))
                 return rc;
         } else {
-            if (int rc = ddm_forest_predict_dev(c.segs, c.seg_res, c.n, e->per_batch, c.predict_blocks, c.pstall,
-                                                e->stream, nullptr, nullptr))
+            if (int rc = forest_predict_dev_clk(c.segs, c.seg_res, c.n, e->per_batch, c.predict_blocks, c.pstall, clk,
+                                                e->stream))
                 return rc;
         }
         if (int rc = rec(pb1, s)) return rc;

@@ -740,10 +740,9 @@ __device__ __forceinline__ int cf_rows_dev(const Seg& g, int pb) {
     return aligned ? kVecRows : 2;
 }
 
-__global__ __launch_bounds__(kCfThreads) void k_cforest_predict_dev(const Seg* __restrict__ segs,
-                                                                    const int64_t* const* __restrict__ res,
-                                                                    int n_segs, int pb, int32_t* __restrict__ stall,
-                                                                    int64_t row_order_delta, int lds_cap) {
+__device__ __forceinline__ void predict_dev_body(const Seg* __restrict__ segs, const int64_t* const* __restrict__ res,
+                                                 int n_segs, int pb, int32_t* __restrict__ stall,
+                                                 int64_t row_order_delta, int lds_cap) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int64_t gb = blockIdx.x;
     int s = 0;
@@ -786,6 +785,23 @@ __global__ __launch_bounds__(kCfThreads) void k_cforest_predict_dev(const Seg* _
         case 6: cf_dispatch<1, kVecRows>(sg, blk, nblk, pb, smem); break;
         case 7: cf_dispatch<2, kVecRows>(sg, blk, nblk, pb, smem); break;
         default: cf_dispatch<4, kVecRows>(sg, blk, nblk, pb, smem); break;
+    }
+}
+
+// clk (ddm_ctl.predict_clock): the launch's span on the 100 MHz device clock, as the
+// kernel's own time (a rocprofv3 kernel record's, without the queue time HIP events add):
+// workgroups 0-7 (one per XCD) stamp their start, every workgroup its end, into 8 shards
+// (block b -> shard b & 7) so that no one word takes 2,048 atomics; k_stage_ctl folds them.
+__global__ __launch_bounds__(kCfThreads) void k_cforest_predict_dev(const Seg* __restrict__ segs,
+                                                                    const int64_t* const* __restrict__ res,
+                                                                    int n_segs, int pb, int32_t* __restrict__ stall,
+                                                                    int64_t row_order_delta, int lds_cap,
+                                                                    unsigned long long* clk) {
+    if (clk && blockIdx.x < 8 && threadIdx.x == 0) atomicMin(clk + blockIdx.x, (unsigned long long)wall_clock64());
+    predict_dev_body(segs, res, n_segs, pb, stall, row_order_delta, lds_cap);
+    if (clk) {
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(clk + 8 + (blockIdx.x & 7), (unsigned long long)wall_clock64());
     }
 }
 
@@ -1003,6 +1019,9 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
     return 0;
 }
 
+int forest_predict_dev_clk(const ddm_predict_segment* segs_dev, const int64_t* const* res_dev, int32_t n_segs,
+                           int32_t per_batch, int64_t grid, int32_t* stall, uint64_t* clk, ddm_stream_t stream);
+
 extern "C" int ddm_forest_predict_dev(const ddm_predict_segment* segs_dev, const int64_t* const* res_dev,
                                       int32_t n_segs, int32_t per_batch, int64_t grid, int32_t* stall,
                                       ddm_stream_t stream, ddm_event_t ev_begin, ddm_event_t ev_end) {
@@ -1014,13 +1033,19 @@ extern "C" int ddm_forest_predict_dev(const ddm_predict_segment* segs_dev, const
     hipStream_t s = ddm::as_hip(stream);
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
-    hipLaunchKernelGGL(k_cforest_predict_dev, dim3((unsigned)grid), dim3(kCfThreads), kDevLds, s,
-                       reinterpret_cast<const Seg*>(segs_dev), res_dev, (int)n_segs, (int)per_batch, stall,
-                       (int64_t)0, (int)kDevLds);
-    if (int rc = ddm::launch_status("ddm_forest_predict_dev")) return rc;
+    if (int rc = forest_predict_dev_clk(segs_dev, res_dev, n_segs, per_batch, grid, stall, nullptr, stream)) return rc;
     if (ev_end)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
     return 0;
+}
+
+// The same launch, stamping clk (ddm_ctl.predict_clock) when non-null (csrc/ctl.hip).
+int forest_predict_dev_clk(const ddm_predict_segment* segs_dev, const int64_t* const* res_dev, int32_t n_segs,
+                           int32_t per_batch, int64_t grid, int32_t* stall, uint64_t* clk, ddm_stream_t stream) {
+    hipLaunchKernelGGL(k_cforest_predict_dev, dim3((unsigned)grid), dim3(kCfThreads), kDevLds, ddm::as_hip(stream),
+                       reinterpret_cast<const Seg*>(segs_dev), res_dev, (int)n_segs, (int)per_batch, stall,
+                       (int64_t)0, (int)kDevLds, reinterpret_cast<unsigned long long*>(clk));
+    return ddm::launch_status("ddm_forest_predict_dev");
 }
 
 // ---- row-order predict + the permutation into DDM order (device-resident epochs) --------
@@ -1082,7 +1107,7 @@ __global__ __launch_bounds__(kPermThreads) void k_err_permute(const Seg* __restr
 // Internal (csrc/ctl.hip): the device-table predict writing err + delta in row order.
 extern "C" int ddm_forest_predict_dev_orig(const ddm_predict_segment* segs_dev, const int64_t* const* res_dev,
                                            int32_t n_segs, int32_t per_batch, int64_t grid, int32_t* stall,
-                                           int64_t delta, ddm_stream_t stream) {
+                                           int64_t delta, uint64_t* clk, ddm_stream_t stream) {
     if (!segs_dev || !res_dev || !stall || n_segs <= 0 || per_batch <= 0 || per_batch > 256 || grid <= 0 ||
         grid >= ((int64_t)1 << 31) || delta == 0) {
         ddm::set_error("ddm_forest_predict_dev_orig: invalid argument");
@@ -1095,7 +1120,7 @@ extern "C" int ddm_forest_predict_dev_orig(const ddm_predict_segment* segs_dev, 
     // unusable forest, and the runner stops decoupling (ddm_amd/devctl.py).
     hipLaunchKernelGGL(k_cforest_predict_dev, dim3((unsigned)grid), dim3(kCfThreads), kDevLdsRowOrder,
                        ddm::as_hip(stream), reinterpret_cast<const Seg*>(segs_dev), res_dev, (int)n_segs,
-                       (int)per_batch, stall, delta, (int)kDevLdsRowOrder);
+                       (int)per_batch, stall, delta, (int)kDevLdsRowOrder, reinterpret_cast<unsigned long long*>(clk));
     return ddm::launch_status("ddm_forest_predict_dev_orig");
 }
 

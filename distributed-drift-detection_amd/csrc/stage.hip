@@ -404,6 +404,22 @@ __global__ __launch_bounds__(kStageThreads) void k_stage_ctl(const Job* __restri
     const int t = threadIdx.x;
     const int i = (int)blockIdx.x;
     const Job jb = jobs[i];
+    if (c.predict_clock && i == 0 && t < 64) {
+        // the epoch's predict launch: its span on the device clock into the running sum (the
+        // 16 shards read and reset by 16 lanes at once, then reduced over the wave)
+        unsigned long long* clk = reinterpret_cast<unsigned long long*>(c.predict_clock);
+        unsigned long long lo = ~0ull, hi = 0;
+        if (t < 8) lo = atomicExch(clk + t, ~0ull);
+        else if (t < 16) hi = atomicExch(clk + t, 0ull);
+        for (int o = 32; o > 0; o >>= 1) {
+            lo = min(lo, (unsigned long long)__shfl_xor(lo, o, 64));
+            hi = max(hi, (unsigned long long)__shfl_xor(hi, o, 64));
+        }
+        if (t == 0 && lo != ~0ull && hi > lo) {
+            atomicAdd(clk + 16, hi - lo);
+            atomicAdd(clk + 17, 1ull);
+        }
+    }
     if (fs.err) {
         for (int k = t; k < kRcpN; k += kStageThreads) s_rcp[k] = 1.0 / (double)(k > 0 ? k : 1);
         __syncthreads();

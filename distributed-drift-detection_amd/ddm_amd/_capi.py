@@ -70,7 +70,7 @@ class DdmCtl(ctypes.Structure):
                 ("stage", _vp), ("off", _vp), ("end", _vp), ("state", _vp), ("first", _vp), ("stop", _vp),
                 ("pick", _vp), ("loff", _vp), ("lend", _vp), ("pstall", _vp), ("predict_blocks", _i64),
                 ("status", _vp), ("logs", _vp), ("log_b0", _vp), ("sync", _vp), ("decoupled", _i32),
-                ("long_ok", _i32)]
+                ("long_ok", _i32), ("predict_clock", _vp)]
 
 
 class DdmCtlEpoch(ctypes.Structure):

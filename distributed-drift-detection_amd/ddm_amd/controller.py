@@ -1009,14 +1009,14 @@ class BatchRunner:
             self._E.ev[2 * k + 1] = t.ev[1].value if t is not None else None
 
     def set_predict_timing(self, on):
-        """HIP events around every device-epoch predict launch (devctl.PredictTimer), read
-        after each run into stats.predict_dev_ms / predict_dev_launches: the bench's
-        in-step predict timing inside its timed region."""
+        """The device-clock span of every device-epoch predict launch (devctl.PredictTimer),
+        read after each device phase into stats.predict_dev_ms / predict_dev_launches: the
+        bench's in-step predict timing inside its timed region."""
         if self.devctl is None:
             return
         if on and self.devctl.pred_timer is None:
             from .devctl import PredictTimer
-            self.devctl.pred_timer = PredictTimer()
+            self.devctl.pred_timer = PredictTimer(self.device)
         elif not on and self.devctl.pred_timer is not None:
             self.devctl.pred_timer.close()
             self.devctl.pred_timer = None

@@ -52,54 +52,33 @@ CTL_FLAGS = os.environ.get("DDM_CTL_FLAGS", "1") not in ("", "0")
 
 
 class PredictTimer:
-    """HIP timing events around every device-epoch predict launch of the timed runs (passed
-    to ddm_ctl_epochs as predict_evs, a fresh pair per epoch of a group), harvested once
-    their group has completed: the launches, their summed duration and the launches that
-    had rows (the trailing epochs of a phase, enqueued before the host saw every partition
-    done, predict nothing)."""
+    """The span of every device-epoch predict launch of the timed runs on the 100 MHz device
+    clock (ddm_ctl.predict_clock): the kernel stamps its workgroups' starts and ends into 8
+    shards and the staging kernel after it adds max(end) - min(start) to word 16 and 1 to word
+    17.  The kernel's own time, as a rocprofv3 kernel record measures it (HIP events around
+    the launch added ~20 us of queue time to each, and ~7 us per event to the epoch), launches
+    with no rows (the trailing epochs of a phase) included."""
 
-    def __init__(self):
-        self.free = []
-        self.inflight = []           # (group index, ctypes array of 2*GROUP events)
-        self.ms = 0.0
-        self.launches = 0
+    TICK_MS = 1e-5                   # 10-ns ticks
 
-    def arm(self, n, group):
-        evs = (ctypes.c_void_p * (2 * n))()
-        for k in range(2 * n):
-            if self.free:
-                evs[k] = self.free.pop()
-            else:
-                e = ctypes.c_void_p()
-                check(lib.ddm_event_create(ctypes.byref(e)), "ddm_event_create")
-                evs[k] = e.value
-        self.inflight.append((group, evs))
-        return ctypes.cast(evs, ctypes.c_void_p)
+    def __init__(self, device):
+        self.d = torch.zeros(18, dtype=torch.int64, device=device)
+        self.d[:8] = -1              # min(start) shards: ~0
+        self.h = torch.zeros(2, dtype=torch.int64, pin_memory=True)
 
-    def harvest(self, upto=None):
-        """Read (and recycle) the pairs of every group <= upto (None: all, after a sync)."""
-        ms = ctypes.c_float()
-        keep = []
-        for g, evs in self.inflight:
-            if upto is not None and g > upto:
-                keep.append((g, evs))
-                continue
-            for k in range(0, len(evs), 2):
-                check(lib.ddm_event_elapsed_ms(evs[k], evs[k + 1], ctypes.byref(ms)), "ddm_event_elapsed_ms")
-                self.ms += ms.value
-                self.launches += 1
-            self.free.extend(evs)
-        self.inflight = keep
+    def ptr(self):
+        return self.d.data_ptr()
 
-    def take(self):
-        out = (self.ms, self.launches)
-        self.ms, self.launches = 0.0, 0
-        return out
+    def take(self, stream):
+        """(ms, launches) since the last take; the stream is synchronised."""
+        with torch.cuda.stream(stream):
+            self.h.copy_(self.d[16:18], non_blocking=True)
+            self.d[16:18].zero_()
+        stream.synchronize()
+        return float(self.h[0]) * self.TICK_MS, int(self.h[1])
 
     def close(self):
-        for e in self.free:
-            lib.ddm_event_destroy(e)
-        self.free = []
+        pass
 
 
 class DeviceController:
@@ -320,6 +299,7 @@ class DeviceController:
         timing = r.t_pred is not None
         logging = r.predict_log is not None
         pt = self.pred_timer
+        E.ctl.predict_clock = pt.ptr() if pt is not None else None
         # HIP cannot time events that a graph records (hipEventElapsedTime: invalid resource
         # handle), so timed predicts keep the launched form
         use_graph = CTL_GRAPH and pt is None and not (timing or logging)
@@ -356,9 +336,7 @@ class DeviceController:
             elif use_graph:
                 check(lib.ddm_ctl_graph_launch(self._graph(E), stream.cuda_stream), "ddm_ctl_graph_launch")
             else:
-                E.predict_evs = pt.arm(GROUP, group) if pt is not None else None
                 check(lib.ddm_ctl_epochs(ctypes.byref(E), GROUP), "ddm_ctl_epochs")
-                E.predict_evs = None
             epochs += GROUP
             group += 1
             if group == 1:
@@ -370,8 +348,6 @@ class DeviceController:
             if pending is not None:
                 pev, pslot = pending
                 pev.synchronize()
-                if pt is not None:
-                    pt.harvest(upto=group - 2)     # every group up to the polled one is complete
                 rec = self.poll_h[pslot].numpy().view(CTL)
                 active = (rec["done"] == 0) & (rec["stall"] == 0) & (rec["park"] == 0)
                 if not active.any() or (rec["stall"] != 0).any():
@@ -389,8 +365,7 @@ class DeviceController:
         stream.synchronize()
         r.side_stream.synchronize()
         if pt is not None:
-            pt.harvest()
-            ms, n = pt.take()
+            ms, n = pt.take(stream)
             st.predict_dev_ms += ms
             st.predict_dev_launches += n
         r._mark("device epochs drained")

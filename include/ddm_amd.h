@@ -640,6 +640,14 @@ typedef struct ddm_ctl {
                                                       needs it stalls (DDM_CTL_STALL_LONG)
                                                       instead, and no long-scan launch is
                                                       enqueued                                 */
+    uint64_t* predict_clock;                       /* ABI 21: NULL or device words [18], set
+                                                      once to 8 x ~0, 8 x 0, 0, 0: every
+                                                      epoch's predict stamps its first
+                                                      workgroups' starts and every workgroup's
+                                                      end on the 100 MHz device clock (8
+                                                      shards), the staging kernel after it adds
+                                                      max(end) - min(start) to [16] and 1 to
+                                                      [17] and resets the shards              */
 } ddm_ctl;
 
 typedef struct ddm_ctl_epoch {
