@@ -187,15 +187,22 @@ __device__ __forceinline__ int wave_sum_i(int v) {
     return v;
 }
 
-// inclusive prefix sum over the wave
+// inclusive prefix sum over the wave by DPP (rows of 16 by row_shr 1/2/4/8, then across
+// rows by row_bcast 15/31; a lane without a source adds 0): six VALU operations instead of
+// six LDS-crossbar shuffles (the split search's per-class scans are its inner loop)
 __device__ __forceinline__ int wave_scan_i(int v, int lane) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(v, o, 64);
-        if (lane >= o) v += u;
-    }
+    (void)lane;
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
     return v;
 }
+
+// the last lane's value (uniform)
+__device__ __forceinline__ int wave_last_i(int v) { return __builtin_amdgcn_readlane(v, 63); }
 
 // RandomState(seed) of one tree (init_genrand on lane 0: a serial recurrence, on the
 // scalar unit it made the trees kernel slower, 46 -> 54 us with 800 waves sharing one
@@ -426,9 +433,9 @@ __device__ void swap_feats(TreeLds& S, int a, int b) {
 // The best split position of one feature (rf_fit.cpp Builder::node_split, the body for one
 // feature that is not constant): the node's n rows in the feature's order in crow / cfv.
 // Every split position p in [1, n): left = positions [0, p).  Lane owns positions
-// lane + 64k; the class weights left of every position come from one wave prefix sum per
-// class present in the node (exact integers; an absent class adds 0 to every sum), summed
-// into sum-of-squares per position.  pos < 0: no split position.
+// lane + 64k; the class weights left of every position come from wave prefix sums, three
+// classes per sum (exact integers; absent classes add 0 to every sum), summed into
+// sum-of-squares per position.  pos < 0: no split position.
 struct FeatBest {
     double mx, thr, il, ir;
     int pos, ml;
@@ -449,24 +456,28 @@ __device__ __forceinline__ FeatBest eval_feature(const uint8_t* crow, const floa
         cq[k] = inq ? (int)yidx[r] : -1;
         const int incl = wave_scan_i(wq[k], lane);
         wl[k] = carry + incl - wq[k];
-        carry += __shfl(incl, 63, 64);
+        carry += wave_last_i(incl);
         sql[k] = 0;
         sqr[k] = 0;
     }
-    for (int c = 0; c < K; ++c) {
-        const int tot = ccnt[c];
-        if (tot == 0) continue;
+    // three classes per scan: 10-bit fields of one int (a field's running sum is at most the
+    // node's weight <= L <= 256, so fields never carry into each other)
+    for (int c0 = 0; c0 < K; c0 += 3) {
+        const int t0 = ccnt[c0], t1 = c0 + 1 < K ? ccnt[c0 + 1] : 0, t2 = c0 + 2 < K ? ccnt[c0 + 2] : 0;
+        if ((t0 | t1 | t2) == 0) continue;
         int cc = 0;
 #pragma unroll
         for (int k = 0; k < kR; ++k) {
             if (64 * k >= n) break;
-            const int v = cq[k] == c ? wq[k] : 0;
+            const int d = cq[k] - c0;
+            const int v = (d >= 0 && d < 3) ? wq[k] << (10 * d) : 0;
             const int incl = wave_scan_i(v, lane);
-            const int sl = cc + incl - v;
-            const int sr = tot - sl;
-            sql[k] += sl * sl;
-            sqr[k] += sr * sr;
-            cc += __shfl(incl, 63, 64);
+            const int slp = cc + incl - v;
+            const int sl0 = slp & 1023, sl1 = (slp >> 10) & 1023, sl2 = (slp >> 20) & 1023;
+            const int sr0 = t0 - sl0, sr1 = t1 - sl1, sr2 = t2 - sl2;
+            sql[k] += sl0 * sl0 + sl1 * sl1 + sl2 * sl2;
+            sqr[k] += sr0 * sr0 + sr1 * sr1 + sr2 * sr2;
+            cc += wave_last_i(incl);
         }
     }
     double bp = -INFINITY, bil = 0.0, bir = 0.0;
@@ -841,15 +852,10 @@ constexpr int kPackThreads = 256;
 constexpr int kPackLdsNodes = 1024;          // forests up to this many nodes are packed in LDS
 
 // Block-wide exclusive prefix sum of one int per thread (kPackThreads threads): a wave
-// scan by shuffles, then the wave totals through LDS (two barriers).
+// scan (DPP), then the wave totals through LDS (two barriers).
 __device__ int block_scan_excl(int v, int* tmp, int& total) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    int inc = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += u;
-    }
+    const int inc = wave_scan_i(v, lane);
     if (lane == 63) tmp[wv] = inc;
     __syncthreads();
     int base = 0, all = 0;
