@@ -181,10 +181,59 @@ __device__ __forceinline__ uint32_t our_rand_r(uint32_t& s) {
     return s % (kRandRMax + 1u);
 }
 
+// One step of a wave scan / reduction by DPP: the value from the lane kCtrl names
+// (row_shr:n, or row_bcast:15/31 into the rows of kRowMask), `ident` where there is none.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ int dpp_i(int v, int ident) {
+    return __builtin_amdgcn_update_dpp(ident, v, kCtrl, kRowMask, 0xF, false);
+}
+
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ double dpp_d(double v, double ident) {
+    const long long b = __double_as_longlong(v), e = __double_as_longlong(ident);
+    const int lo = __builtin_amdgcn_update_dpp((int)e, (int)b, kCtrl, kRowMask, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(e >> 32), (int)(b >> 32), kCtrl, kRowMask, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+__device__ __forceinline__ double readlane_d(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, src);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// Wave reductions, uniform results: the inclusive DPP scan's last lane, read by readlane.
 __device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v += dpp_i<0x111, 0xF>(v, 0);
+    v += dpp_i<0x112, 0xF>(v, 0);
+    v += dpp_i<0x114, 0xF>(v, 0);
+    v += dpp_i<0x118, 0xF>(v, 0);
+    v += dpp_i<0x142, 0xA>(v, 0);
+    v += dpp_i<0x143, 0xC>(v, 0);
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+__device__ __forceinline__ int wave_min_i(int v) {
+    constexpr int kId = 0x7fffffff;
+    v = min(v, dpp_i<0x111, 0xF>(v, kId));
+    v = min(v, dpp_i<0x112, 0xF>(v, kId));
+    v = min(v, dpp_i<0x114, 0xF>(v, kId));
+    v = min(v, dpp_i<0x118, 0xF>(v, kId));
+    v = min(v, dpp_i<0x142, 0xA>(v, kId));
+    v = min(v, dpp_i<0x143, 0xC>(v, kId));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+__device__ __forceinline__ double wave_max_d(double v) {
+    const double kId = -__builtin_huge_val();
+    v = fmax(v, dpp_d<0x111, 0xF>(v, kId));
+    v = fmax(v, dpp_d<0x112, 0xF>(v, kId));
+    v = fmax(v, dpp_d<0x114, 0xF>(v, kId));
+    v = fmax(v, dpp_d<0x118, 0xF>(v, kId));
+    v = fmax(v, dpp_d<0x142, 0xA>(v, kId));
+    v = fmax(v, dpp_d<0x143, 0xC>(v, kId));
+    return readlane_d(v, 63);
 }
 
 // inclusive prefix sum over the wave by DPP (rows of 16 by row_shr 1/2/4/8, then across
@@ -500,18 +549,14 @@ __device__ __forceinline__ FeatBest eval_feature(const uint8_t* crow, const floa
         }
     }
     // first maximum over the wave: the largest proxy, then the smallest position
-    double mx = bp;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
-    int mpos = (bpos >= 0 && bp == mx) ? bpos : 0x7fffffff;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mpos = min(mpos, __shfl_xor(mpos, o, 64));
+    const double mx = wave_max_d(bp);
+    const int mpos = wave_min_i((bpos >= 0 && bp == mx) ? bpos : 0x7fffffff);
     FeatBest r{mx, 0.0, 0.0, 0.0, -1, 0};
     if (mpos != 0x7fffffff) {
-        const int src = mpos & 63;                // the lane that owns position mpos
+        const int src = mpos & 63;                // the lane that owns position mpos (uniform)
         r.pos = mpos;
-        r.il = __shfl(bil, src, 64);
-        r.ir = __shfl(bir, src, 64);
+        r.il = readlane_d(bil, src);
+        r.ir = readlane_d(bir, src);
         double thr = (double)cfv[mpos - 1] / 2.0 + (double)cfv[mpos] / 2.0;
         if (thr == (double)cfv[mpos] || thr == INFINITY || thr == -INFINITY) thr = (double)cfv[mpos - 1];
         r.thr = thr;
