@@ -259,19 +259,46 @@ __device__ __forceinline__ int wave_last_i(int v) { return __builtin_amdgcn_read
 // randint(0, 2**31 - 1) of that stream (peeked, not consumed) and the bootstrap =
 // randint(0, L, L) from the same start, as multiplicities in cnt[0..L).  One wave; returns
 // the splitter seed.
-__device__ uint32_t tree_boot(uint32_t seed, int L, uint32_t* mt, int32_t* cnt, int lane) {
-    if (lane == 0) {
-        uint32_t v = seed;
-        mt[0] = v;
-        for (int i = 1; i < 624; ++i) {
-            v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
-            mt[i] = v;
-        }
+#ifdef DDM_PREP_PROFILE
+__device__ uint64_t g_boot_prof[3];   // the last boot's stamps: init done, twist done, end
+#endif
+
+// init_genrand words base + k0 .. base + k1 - 1 (v holds word base + k0 - 1), each written
+// into lane k of buf
+template <int k0, int k1>
+__device__ __forceinline__ void init_block(uint32_t& v, uint32_t& buf, uint32_t base) {
+#pragma unroll
+    for (int k = k0; k < k1; ++k) {
+        v = 1812433253u * (v ^ (v >> 30)) + (base + (uint32_t)k);
+        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(buf) : "s"(v), "i"(k));
     }
+}
+
+__device__ uint32_t tree_boot(uint32_t seed, int L, uint32_t* mt, int32_t* cnt, int lane) {
+    // init_genrand: the recurrence on the scalar unit (a uniform value: s_mul_i32 and
+    // friends, instead of quarter-rate wave64 VALU operations on one lane), each word put
+    // into its lane of a VGPR by v_writelane (off the chain; 64 steps unrolled, so no branch
+    // or compare per step) and stored 64 words at a time
+    uint32_t v = __builtin_amdgcn_readfirstlane(seed);
+    uint32_t buf = v;                               // word 0 in every lane, lane 0 kept
+    init_block<1, 64>(v, buf, 0u);
+    mt[lane] = buf;
+    for (uint32_t base = 64; base < 576; base += 64) {
+        init_block<0, 64>(v, buf, base);
+        mt[base + lane] = buf;
+    }
+    init_block<0, 48>(v, buf, 576u);
+    if (lane < 48) mt[576 + lane] = buf;            // words 576..623
     wave_sync();
+#ifdef DDM_PREP_PROFILE
+    const uint64_t tq1 = wall_clock64();
+#endif
     twist(mt, lane);
     for (int k = lane; k < L; k += 64) cnt[k] = 0;
     wave_sync();
+#ifdef DDM_PREP_PROFILE
+    const uint64_t tq2 = wall_clock64();
+#endif
     uint32_t rstate = 0;
     for (int j0 = 0; j0 < 624; j0 += 64) {
         const int j = j0 + lane;
@@ -302,10 +329,15 @@ __device__ uint32_t tree_boot(uint32_t seed, int L, uint32_t* mt, int32_t* cnt, 
         cnt[0] = 1;                                 // interval(0) draws nothing
     }
     wave_sync();
+#ifdef DDM_PREP_PROFILE
+    g_boot_prof[0] = tq1;
+    g_boot_prof[1] = tq2;
+    g_boot_prof[2] = wall_clock64();
+#endif
     return rstate;
 }
 
-// k_dfit_prep's boot workgroups (blockIdx.y > 0): one tree per wave, the draws tree_boot
+// k_dfit_prep's boot workgroups (blockIdx.y >= kSortBlocks): one tree per wave, the draws tree_boot
 // makes, stored for k_dfit_trees (rstate, then the L bootstrap counts).  They run beside
 // the presort instead of at the head of every tree wave (init_genrand alone is ~15 us).
 // Only the first wave of each SIMD works: the init recurrence runs on one lane, but every
@@ -313,6 +345,10 @@ __device__ uint32_t tree_boot(uint32_t seed, int L, uint32_t* mt, int32_t* cnt, 
 // SIMD) took 58 us instead of ~20 and slowed the window shuffles beside them.
 constexpr int kPrepThreads = 1024;         // presort tasks: every (feature, row) pair
 constexpr int kBootWaves = 4;              // working waves (trees) per boot workgroup
+// presort workgroups per job: the (feature, row) rank tasks are ALU work (100 comparisons
+// each, 2,700 for a 100 x 27 batch), ~10 us on one CU; each workgroup also redoes the
+// label pass (~1 us) so that all agree on NaN / class-count exits
+constexpr int kSortBlocks = 4;
 
 __device__ void dfit_boot(const Job& jb, int bblk) {
     __shared__ uint32_t s_mt[kBootWaves][624];
@@ -325,9 +361,20 @@ __device__ void dfit_boot(const Job& jb, int bblk) {
         return;
     const Layout lo = layout(L, jb.F, jb.n_trees, jb.k_cap);
     int32_t* bt = reinterpret_cast<int32_t*>(jb.scratch + lo.boot) + (int64_t)tree * (L + 1);
+#ifdef DDM_PREP_PROFILE
+    const uint64_t tb0 = wall_clock64();
+#endif
     const uint32_t rs = tree_boot((uint32_t)jb.seeds[tree], L, s_mt[w], s_cnt[w], lane);
     if (lane == 0) bt[0] = (int32_t)rs;
     for (int k = lane; k < L; k += 64) bt[1 + k] = s_cnt[w][k];
+#ifdef DDM_PREP_PROFILE
+    if (tree == 0 && lane == 0) {   // boot of tree 0: start (vs the presort's start), duration
+        __threadfence();
+        // init done / twist done / draws done / end: 16-bit fields of 10-ns ticks from tb0
+        jb.result[11] = (int64_t)((g_boot_prof[0] - tb0) | ((g_boot_prof[1] - tb0) << 16) |
+                                  ((g_boot_prof[2] - tb0) << 32) | ((wall_clock64() - tb0) << 48));
+    }
+#endif
 }
 
 // ---- k_dfit_prep --------------------------------------------------------------------
@@ -338,36 +385,58 @@ __device__ __forceinline__ void refit_priority() { __builtin_amdgcn_s_setprio(2)
 __global__ __launch_bounds__(kPrepThreads) void k_dfit_prep(const Job* __restrict__ jobs) {
     refit_priority();
     const Job jb = jobs[blockIdx.x];
-    if (blockIdx.y > 0) {
-        dfit_boot(jb, (int)blockIdx.y - 1);
+    if (blockIdx.y >= kSortBlocks) {
+        dfit_boot(jb, (int)blockIdx.y - kSortBlocks);
         return;
     }
     const int t = threadIdx.x;
+    const int part = (int)blockIdx.y;            // this workgroup's share of the rank tasks
+    const bool lead = part == 0;                 // writes classes_, yidx and the status
+#ifdef DDM_PREP_PROFILE
+    const uint64_t tp0 = wall_clock64();
+#endif
     __shared__ int32_t s_y[kMaxL];
     __shared__ float s_tile[kPrepTile];
     __shared__ uint8_t s_first[kMaxL];
     __shared__ int s_nan, s_K, s_skip;
+    const int L = jb.L, F = jb.F;
+    const bool args_ok = !(L < 1 || L > kMaxL || F < 1 || F > kMaxF || jb.n_trees < 1 || jb.n_trees > 256 ||
+                           jb.k_cap < 1 || jb.k_cap > kMaxK || jb.max_features < 1);
+    // the labels and (when every feature fits one tile, the controller's batches) X itself
+    // are loaded beside the gate words instead of after them: one round trip to HBM, not
+    // three; the NaN check reads the tile
+    const int G = args_ok ? max(1, min(F, kPrepTile / L)) : 1;
+    const bool one_tile = args_ok && G == F;
     if (t == 0) {
         s_skip = gated_off(jb);
         s_nan = 0;
         s_K = 0;
     }
+    if (args_ok) {
+        if (t < L) s_y[t] = jb.y[t];
+        if (one_tile) {
+            for (int e = t; e < L * F; e += kPrepThreads) {
+                const float x = jb.X[e];
+                const int r = e / F, k = e % F;
+                s_tile[k * L + r] = x;
+                if (x != x) s_nan = 1;
+            }
+        }
+    }
     __syncthreads();
     if (s_skip) return;                          // the result words keep the last refit's
-    const int L = jb.L, F = jb.F;
-    if (L < 1 || L > kMaxL || F < 1 || F > kMaxF || jb.n_trees < 1 || jb.n_trees > 256 || jb.k_cap < 1 ||
-        jb.k_cap > kMaxK ||
-        jb.max_features < 1) {
-        if (t == 0) jb.result[DDM_DFIT_STATUS] = DDM_E_ARG;
+    if (!args_ok) {
+        if (lead && t == 0) jb.result[DDM_DFIT_STATUS] = DDM_E_ARG;
         return;
     }
     const Layout lo = layout(L, F, jb.n_trees, jb.k_cap);
     uint8_t* yidx = jb.scratch + lo.yidx;
     uint8_t* order = jb.scratch + lo.order;
-    if (t < L) s_y[t] = jb.y[t];
-    for (int e = t; e < L * F; e += kPrepThreads)
-        if (jb.X[e] != jb.X[e]) s_nan = 1;
-    __syncthreads();
+    if (!one_tile) {
+        for (int e = t; e < L * F; e += kPrepThreads)
+            if (jb.X[e] != jb.X[e]) s_nan = 1;
+        __syncthreads();
+    }
     // classes_ = np.unique(y): first occurrences ranked by value
     if (t < L) {
         int first = 1;
@@ -382,28 +451,34 @@ __global__ __launch_bounds__(kPrepThreads) void k_dfit_prep(const Job* __restric
         int rank = 0;
 #pragma unroll 16
         for (int j = 0; j < L; ++j) rank += (s_first[j] && s_y[j] < s_y[t]) ? 1 : 0;
-        yidx[t] = (uint8_t)min(rank, 255);
-        if (s_first[t] && rank < jb.k_cap) jb.classes[rank] = s_y[t];
+        if (lead) {
+            yidx[t] = (uint8_t)min(rank, 255);
+            if (s_first[t] && rank < jb.k_cap) jb.classes[rank] = s_y[t];
+        }
     }
     if (s_nan || K > jb.k_cap) {
-        if (t == 0) {
+        if (lead && t == 0) {
             jb.result[DDM_DFIT_STATUS] = s_nan ? DDM_E_NAN : DDM_E_FOREST;
             jb.result[DDM_DFIT_CLASSES] = K;
         }
         return;
     }
+#ifdef DDM_PREP_PROFILE
+    const uint64_t tp1 = wall_clock64();
+#endif
     // presorted orders: the stable rank of every row in every feature, for as many
     // features at once as fit the LDS tile (every (feature, row) pair is one task)
-    const int G = max(1, min(F, kPrepTile / L));
     for (int f0 = 0; f0 < F; f0 += G) {
         const int g = min(G, F - f0);
-        __syncthreads();
-        for (int e = t; e < L * g; e += kPrepThreads) {
-            const int r = e / g, k = e % g;
-            s_tile[k * L + r] = jb.X[(int64_t)r * F + f0 + k];
+        if (!one_tile) {
+            __syncthreads();
+            for (int e = t; e < L * g; e += kPrepThreads) {
+                const int r = e / g, k = e % g;
+                s_tile[k * L + r] = jb.X[(int64_t)r * F + f0 + k];
+            }
         }
         __syncthreads();
-        for (int e = t; e < L * g; e += kPrepThreads) {
+        for (int e = part * kPrepThreads + t; e < L * g; e += kSortBlocks * kPrepThreads) {
             const int k = e / L, i = e % L;
             const float* col = s_tile + k * L;
             const float x = col[i];
@@ -416,10 +491,15 @@ __global__ __launch_bounds__(kPrepThreads) void k_dfit_prep(const Job* __restric
             order[(int64_t)(f0 + k) * L + r] = (uint8_t)i;
         }
     }
-    if (t == 0) {
+    if (lead && t == 0) {
         jb.result[DDM_DFIT_STATUS] = 0;
         jb.result[DDM_DFIT_CLASSES] = K;
     }
+#ifdef DDM_PREP_PROFILE
+    __syncthreads();
+    if (lead && t == 0)   // presort: start, classes done, end (10-ns ticks from the start)
+        jb.result[10] = (int64_t)(tp0 | ((tp1 - tp0) << 40) | ((wall_clock64() - tp0) << 52));
+#endif
 }
 
 // ---- k_dfit_trees -------------------------------------------------------------------
@@ -1405,7 +1485,7 @@ int rf_fit_device_join(const ddm_dfit_job* jobs_dev, int32_t n_jobs, int32_t max
     const Job* jobs = reinterpret_cast<const Job*>(jobs_dev);
     const bool fused = max_lf > 0 && max_lf <= kTreeTile;
     if (!fused) {
-        hipLaunchKernelGGL(k_dfit_prep, dim3((unsigned)n_jobs, 1u + (unsigned)ddm::ceil_div(max_trees, kBootWaves)),
+        hipLaunchKernelGGL(k_dfit_prep, dim3((unsigned)n_jobs, kSortBlocks + (unsigned)ddm::ceil_div(max_trees, kBootWaves)),
                            dim3(kPrepThreads), 0, s, jobs);
         if (int rc = ddm::launch_status("ddm_rf_fit_device/prep")) return rc;
     }

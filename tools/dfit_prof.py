@@ -38,3 +38,8 @@ for rep in range(3):
           f"build {((a >> 32) & 0xffff)/100:.1f} us, init_genrand {(a >> 48)/100:.1f} us; pack: bfs {(p & 0xffff)/100:.1f} us, compile {((p >> 16) & 0xffff)/100:.1f} us "
           f"(A/B-C/zero/D {', '.join(str(((p >> (32 + 8 * i)) & 255) * 0.08)[:4] for i in range(4))} us); "
           f"nodes {int(r[2])}, blob {int(r[5])}")
+    if "prep" in sys.argv:    # a DDM_PREP_PROFILE build: presort / boot timings of job 0
+        a, b = int(r[10]) & ((1 << 64) - 1), int(r[11]) & ((1 << 64) - 1)
+        f = [((b >> (16 * i)) & 0xffff) / 100 for i in range(4)]
+        print(f"  presort: classes {((a >> 40) & 0xfff) / 100:.1f} us, end {(a >> 52) / 100:.1f} us; "
+              f"boot tree 0: init done {f[0]:.1f}, twist done {f[1]:.1f}, draws done {f[2]:.1f}, end {f[3]:.1f} us")
