@@ -380,7 +380,10 @@ __device__ void dfit_boot(const Job& jb, int bblk) {
 // ---- k_dfit_prep --------------------------------------------------------------------
 // The refit kernels are the epoch's critical path while the next windows' shuffles run on
 // the side stream on the same CUs: their waves take issue priority over the shuffles'.
-__device__ __forceinline__ void refit_priority() { __builtin_amdgcn_s_setprio(2); }
+#ifndef DDM_REFIT_PRIO
+#define DDM_REFIT_PRIO 2
+#endif
+__device__ __forceinline__ void refit_priority() { __builtin_amdgcn_s_setprio(DDM_REFIT_PRIO); }
 
 __global__ __launch_bounds__(kPrepThreads) void k_dfit_prep(const Job* __restrict__ jobs) {
     refit_priority();

@@ -19,6 +19,7 @@ from ddm_amd.rng import MTStream  # noqa: E402
 from ddm_amd.shuffle import GpuShuffle  # noqa: E402
 
 W = int(sys.argv[1]) if len(sys.argv) > 1 else 12_500
+CAP = int(os.environ.get("SHUF_PIECE_CAP", 256))     # the replay grid's cap (ctl.hip kShufPieces)
 L, n = 100, 8
 dev = torch.device("cuda", 0)
 stream = torch.cuda.current_stream(dev)
@@ -39,7 +40,7 @@ for it in range(3):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(10):
-        check(lib.ddm_shuffle_window_batch(jobs.data_ptr(), n, W, min(max_pieces, 256), L,
+        check(lib.ddm_shuffle_window_batch(jobs.data_ptr(), n, W, min(max_pieces, CAP), L,
                                            torch.cuda.current_stream(dev).cuda_stream, None, None),
               "ddm_shuffle_window_batch")
     e1.record()
