@@ -93,7 +93,8 @@ extern "C" int ddm_scan_long_reuse(const uint8_t* err, const int64_t* stream_off
                                    ddm_stream_t stream);
 extern "C" int ddm_forest_predict_dev_orig(const ddm_predict_segment* segs_dev, const int64_t* const* res_dev,
                                            int32_t n_segs, int32_t per_batch, int64_t grid, int32_t* stall,
-                                           int64_t delta, uint64_t* clk, ddm_stream_t stream);
+                                           int64_t delta, uint64_t* clk, const uint32_t* join_flag,
+                                           uint32_t join_v, uint32_t* timeouts, ddm_stream_t stream);
 int forest_predict_dev_clk(const ddm_predict_segment* segs_dev, const int64_t* const* res_dev, int32_t n_segs,
                            int32_t per_batch, int64_t grid, int32_t* stall, uint64_t* clk, ddm_stream_t stream);
 extern "C" int ddm_err_permute_dev(const ddm_predict_segment* segs_dev, int32_t n_segs, int32_t per_batch,
@@ -237,9 +238,14 @@ int ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs, bool graph) {
         const ddm_event_t pb1 = e->predict_evs ? e->predict_evs[2 * k + 1] : e->ev[1];
         if (int rc = rec(pb0, s)) return rc;
         if (dec) {
+            // the predict's first workgroup holds the join of this window's shuffles (the
+            // permutation's input), unless it was held already
+            const bool hold = flags && !first_in_graph && seq[2] != seq[1];
             if (int rc = ddm_forest_predict_dev_orig(c.segs, c.seg_res, c.n, e->per_batch, c.predict_blocks, c.pstall,
-                                                     e->row_order_delta, clk, e->stream))
+                                                     e->row_order_delta, clk, hold ? flags + 1 : nullptr,
+                                                     hold ? seq[1] : 0u, flags ? flags + 2 : nullptr, e->stream))
                 return rc;
+            if (hold) seq[2] = seq[1];
         } else {
             if (int rc = forest_predict_dev_clk(c.segs, c.seg_res, c.n, e->per_batch, c.predict_blocks, c.pstall, clk,
                                                 e->stream))

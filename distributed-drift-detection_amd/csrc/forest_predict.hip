@@ -796,13 +796,18 @@ __global__ __launch_bounds__(kCfThreads) void k_cforest_predict_dev(const Seg* _
                                                                     const int64_t* const* __restrict__ res,
                                                                     int n_segs, int pb, int32_t* __restrict__ stall,
                                                                     int64_t row_order_delta, int lds_cap,
-                                                                    unsigned long long* clk) {
+                                                                    unsigned long long* clk, const uint32_t* join_flag,
+                                                                    uint32_t join_v, uint32_t* timeouts) {
     if (clk && blockIdx.x < 8 && threadIdx.x == 0) atomicMin(clk + blockIdx.x, (unsigned long long)wall_clock64());
     predict_dev_body(segs, res, n_segs, pb, stall, row_order_delta, lds_cap);
     if (clk) {
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(clk + 8 + (blockIdx.x & 7), (unsigned long long)wall_clock64());
     }
+    // join_flag (decoupled epochs, ctl.hip): workgroup 0 -- the first to finish -- holds the
+    // kernel's end until the side stream's shuffles of this window are done, so the
+    // permutation after it needs no poll of its own (the other workgroups never wait)
+    if (join_flag && blockIdx.x == 0 && threadIdx.x == 0) ddm::flag_poll(join_flag, join_v, timeouts);
 }
 
 using predict_fn = void (*)(Seg, int64_t);
@@ -1044,7 +1049,7 @@ int forest_predict_dev_clk(const ddm_predict_segment* segs_dev, const int64_t* c
                            int32_t per_batch, int64_t grid, int32_t* stall, uint64_t* clk, ddm_stream_t stream) {
     hipLaunchKernelGGL(k_cforest_predict_dev, dim3((unsigned)grid), dim3(kCfThreads), kDevLds, ddm::as_hip(stream),
                        reinterpret_cast<const Seg*>(segs_dev), res_dev, (int)n_segs, (int)per_batch, stall,
-                       (int64_t)0, (int)kDevLds, reinterpret_cast<unsigned long long*>(clk));
+                       (int64_t)0, (int)kDevLds, reinterpret_cast<unsigned long long*>(clk), nullptr, 0u, nullptr);
     return ddm::launch_status("ddm_forest_predict_dev");
 }
 
@@ -1107,7 +1112,8 @@ __global__ __launch_bounds__(kPermThreads) void k_err_permute(const Seg* __restr
 // Internal (csrc/ctl.hip): the device-table predict writing err + delta in row order.
 extern "C" int ddm_forest_predict_dev_orig(const ddm_predict_segment* segs_dev, const int64_t* const* res_dev,
                                            int32_t n_segs, int32_t per_batch, int64_t grid, int32_t* stall,
-                                           int64_t delta, uint64_t* clk, ddm_stream_t stream) {
+                                           int64_t delta, uint64_t* clk, const uint32_t* join_flag, uint32_t join_v,
+                                           uint32_t* timeouts, ddm_stream_t stream) {
     if (!segs_dev || !res_dev || !stall || n_segs <= 0 || per_batch <= 0 || per_batch > 256 || grid <= 0 ||
         grid >= ((int64_t)1 << 31) || delta == 0) {
         ddm::set_error("ddm_forest_predict_dev_orig: invalid argument");
@@ -1120,7 +1126,8 @@ extern "C" int ddm_forest_predict_dev_orig(const ddm_predict_segment* segs_dev, 
     // unusable forest, and the runner stops decoupling (ddm_amd/devctl.py).
     hipLaunchKernelGGL(k_cforest_predict_dev, dim3((unsigned)grid), dim3(kCfThreads), kDevLdsRowOrder,
                        ddm::as_hip(stream), reinterpret_cast<const Seg*>(segs_dev), res_dev, (int)n_segs,
-                       (int)per_batch, stall, delta, (int)kDevLdsRowOrder, reinterpret_cast<unsigned long long*>(clk));
+                       (int)per_batch, stall, delta, (int)kDevLdsRowOrder, reinterpret_cast<unsigned long long*>(clk),
+                       join_flag, join_v, timeouts);
     return ddm::launch_status("ddm_forest_predict_dev_orig");
 }
 
