@@ -22,6 +22,19 @@ inline hipStream_t as_hip(ddm_stream_t s) { return reinterpret_cast<hipStream_t>
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// A pointer into device (global) memory as the global address space: loads and stores
+// through it are global_* instructions.  A pointer loaded from a job table is generic, so
+// its accesses are flat_* instructions, which count on both vmcnt and lgkmcnt: every LDS
+// wait of a kernel then also waits for its outstanding memory operations (and the other
+// way round).  Keep the result typed as such down to the accesses (a cast back to generic
+// is folded away).
+template <typename T>
+using gptr = __attribute__((address_space(1))) T*;
+template <typename T>
+__device__ __forceinline__ gptr<T> as_global(T* p) {
+    return (gptr<T>)p;
+}
+
 // Cross-stream order by a sequence number in device memory (ddm_ctl_epoch.sync_flags):
 // the producer's data are released (agent scope) before the number is stored; a poll ends
 // when the number reaches v, or gives up after ~0.1 s and counts that in *timeouts.  One

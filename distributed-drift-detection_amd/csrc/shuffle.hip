@@ -25,6 +25,9 @@
 // recovers the exact numpy (key, pos) state at any draw from R.
 #include "common.h"
 
+using ddm::as_global;
+using ddm::gptr;
+
 namespace {
 
 constexpr int kN = 624;
@@ -372,6 +375,18 @@ struct ChunkStart {
     int32_t batch;    // batches completed (relative to the window) before pos
 };
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void put_piece(gptr<ChunkStart> out, int64_t k, int64_t pos, int32_t state, int32_t batch) {
+    out[k].pos = pos;
+    out[k].state = state;
+    out[k].batch = batch;
+}
+
+__device__ __forceinline__ ChunkStart get_piece(gptr<const ChunkStart> in, int64_t k) {
+    return ChunkStart{in[k].pos, in[k].state, in[k].batch};
+}
+
 // The prefix tables only describe chunks entered at their first draw.  A window starts at
 // a batch boundary P anywhere in a chunk (the refit seeds before it are not shuffle draws),
 // so the rest of that one chunk gets classic per-sub-chunk tables, every start state
@@ -389,7 +404,7 @@ __device__ void fsm_first(const Job& j, int L) {
     const int64_t d0 = cstart + (int64_t)q * kSub;
     if (d0 + kSub > j.avail) return;
     if (threadIdx.x < kSub / 4)
-        reinterpret_cast<uint4*>(dr)[threadIdx.x] = reinterpret_cast<const uint4*>(j.R + d0)[threadIdx.x];
+        reinterpret_cast<u32x4*>(dr)[threadIdx.x] = ((gptr<const u32x4>)as_global(j.R + d0))[threadIdx.x];
     __syncthreads();
     for (int s0 = threadIdx.x + 1; s0 <= S; s0 += blockDim.x) {
         uint32_t s = (uint32_t)s0, d = 0;
@@ -401,7 +416,7 @@ __device__ void fsm_first(const Job& j, int L) {
             fsm_step(v.z, s, d, (uint32_t)S);
             fsm_step(v.w, s, d, (uint32_t)S);
         }
-        j.first[q * S + (s0 - 1)] = (uint16_t)(s | (d << 8));
+        as_global(j.first)[q * S + (s0 - 1)] = (uint16_t)(s | (d << 8));
     }
 }
 
@@ -420,9 +435,9 @@ constexpr int kWalkThreads = 256;    // stage the table rows; lane 0 walks them
 // so the serial walk does LDS lookups, not dependent HBM loads.
 // Pieces: out[0] = [P, next sub-chunk boundary); then every sub-chunk of P's chunk; then
 // chunk starts.  info = {pieces, end draw, batches reached}.
-__device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restrict__ first,
-                         const uint32_t* __restrict__ Tchunk, int64_t P, int64_t W, int L, int64_t avail,
-                         ChunkStart* __restrict__ out, int64_t* __restrict__ info) {
+__device__ void fsm_walk(gptr<const uint32_t> __restrict__ R, gptr<const uint16_t> __restrict__ first,
+                         gptr<const uint32_t> __restrict__ Tchunk, int64_t P, int64_t W, int L, int64_t avail,
+                         gptr<ChunkStart> __restrict__ out, gptr<int64_t> __restrict__ info) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab[];   // [64][S] chunk rows; phase A: draws + first-chunk rows
 #ifdef DDM_WALK_PROFILE
     const uint64_t t_start = wall_clock64();
@@ -441,9 +456,9 @@ __device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restr
     for (int k = threadIdx.x; k < n_draws; k += kWalkThreads) a_draws[k] = R[P + k];
     const int of = (q0 * S) & 7;                      // 16-byte loads from the aligned element before
     {
-        const uint4* src = reinterpret_cast<const uint4*>(first + q0 * S - of);
+        const gptr<const u32x4> src = (gptr<const u32x4>)(first + q0 * S - of);
         const int n8 = n_subrows > 0 ? (n_subrows * S + of + 7) / 8 : 0;
-        for (int e = threadIdx.x; e < n8; e += kWalkThreads) reinterpret_cast<uint4*>(a_first)[e] = src[e];
+        for (int e = threadIdx.x; e < n8; e += kWalkThreads) reinterpret_cast<u32x4*>(a_first)[e] = src[e];
     }
     __syncthreads();
     if (threadIdx.x < 64) {
@@ -480,9 +495,9 @@ __device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restr
 #endif
         if (lane == 0) {                      // the rest of the walk is serial
             int64_t k = 0;
-            out[k++] = ChunkStart{P, (int32_t)S, 0};
+            put_piece(out, k++, P, S, 0);
             while (batch < W && pos % kChunk != 0 && pos + kSub <= avail) {
-                out[k++] = ChunkStart{pos, (int32_t)s, (int32_t)batch};
+                put_piece(out, k++, pos, (int32_t)s, (int32_t)batch);
                 const uint32_t e = a_first[of + ((pos - sub_end) / kSub) * S + (s - 1)];
                 s = e & 0xffu;
                 batch += e >> 8;
@@ -505,9 +520,9 @@ __device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restr
         // 16-byte loads from the aligned word at or before row c0 (Tchunk is 16-byte aligned
         // and padded by 4 words)
         const int o = (int)((c0 * S) & 3);
-        const uint4* src = reinterpret_cast<const uint4*>(Tchunk + c0 * S - o);
+        const gptr<const u32x4> src = (gptr<const u32x4>)(Tchunk + c0 * S - o);
         const int n4 = (n * S + o + 3) / 4;
-        for (int e = (int)threadIdx.x - t0; e < n4; e += kWalkThreads - t0) reinterpret_cast<uint4*>(buf)[e] = src[e];
+        for (int e = (int)threadIdx.x - t0; e < n4; e += kWalkThreads - t0) reinterpret_cast<u32x4*>(buf)[e] = src[e];
     };
     const int64_t covered = avail / kChunk;
     int64_t c_load = sh_pos / kChunk;
@@ -525,7 +540,7 @@ __device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restr
             int64_t pos = sh_pos, batch = sh_batch, k = sh_k;
             uint32_t s = sh_s;
             for (int c = 0; c < nload && batch < W; ++c) {
-                out[k++] = ChunkStart{pos, (int32_t)s, (int32_t)batch};
+                put_piece(out, k++, pos, (int32_t)s, (int32_t)batch);
                 const uint32_t e = now[o + c * S + (s - 1)];
                 s = e & 0xffu;
                 batch += e >> 8;
@@ -557,13 +572,15 @@ __device__ void fsm_walk(const uint32_t* __restrict__ R, const uint16_t* __restr
 }
 
 __global__ __launch_bounds__(kWalkThreads) void k_fsm_walk(Job j, int L) {
-    fsm_walk(j.R, j.first, j.Tchunk, j.P, j.W, L, j.avail, reinterpret_cast<ChunkStart*>(j.pieces), j.info);
+    fsm_walk(as_global(j.R), as_global((const uint16_t*)j.first), as_global(j.Tchunk), j.P, j.W, L, j.avail,
+             as_global(reinterpret_cast<ChunkStart*>(j.pieces)), as_global(j.info));
 }
 
 __global__ __launch_bounds__(kWalkThreads) void k_fsm_walk_batch(const Job* __restrict__ jobs, int L) {
     const Job j = jobs[blockIdx.x];
     if (j.W <= 0) return;
-    fsm_walk(j.R, j.first, j.Tchunk, j.P, j.W, L, j.avail, reinterpret_cast<ChunkStart*>(j.pieces), j.info);
+    fsm_walk(as_global(j.R), as_global((const uint16_t*)j.first), as_global(j.Tchunk), j.P, j.W, L, j.avail,
+             as_global(reinterpret_cast<ChunkStart*>(j.pieces)), as_global(j.info));
 }
 
 // One wave per window piece.  A piece of at most one sub-chunk (the start of the window's
@@ -580,8 +597,8 @@ __global__ __launch_bounds__(kWalkThreads) void k_fsm_walk_batch(const Job* __re
 constexpr int kReplayBatch = 16;
 
 struct ReplaySink {
-    uint8_t* J;
-    int64_t* E;
+    gptr<uint8_t> J;
+    gptr<int64_t> E;
     uint8_t* Jl;          // LDS rows of batches [b_lo, b_hi)
     int64_t b_lo, b_hi;
     int L;
@@ -611,14 +628,14 @@ __device__ __forceinline__ void replay_step(uint32_t v, int64_t q, uint32_t& s, 
     }
 }
 
-__device__ __forceinline__ void replay_range(const uint32_t* __restrict__ R, int64_t beg, int64_t fin, uint32_t s,
+__device__ __forceinline__ void replay_range(gptr<const uint32_t> __restrict__ R, int64_t beg, int64_t fin, uint32_t s,
                                              int64_t b, int64_t W, int L, const ReplaySink& k) {
     const uint32_t S = (uint32_t)(L - 1);
     if (fin - beg == kSub && (beg & 3) == 0) {
         // a whole sub-chunk: 64 words at a time in flight (sixteen 16-byte loads)
-        const uint4* src = reinterpret_cast<const uint4*>(R + beg);
+        const gptr<const u32x4> src = (gptr<const u32x4>)(R + beg);
         for (int h = 0; h < kSub / 64 && b < W; ++h) {
-            uint4 v[16];
+            u32x4 v[16];
 #pragma unroll
             for (int q = 0; q < 16; ++q) v[q] = src[16 * h + q];
 #pragma unroll
@@ -648,17 +665,17 @@ __host__ __device__ inline int replay_local_batches(int L) { return (int)(kChunk
 size_t replay_lds_bytes(int L) { return ((size_t)2 * replay_local_batches(L) * L + 15) & ~(size_t)15; }
 
 template <bool kFused>
-__device__ void fsm_replay(const uint32_t* __restrict__ R, const uint32_t* __restrict__ Tpre,
-                           const ChunkStart* __restrict__ pieces, const int64_t* __restrict__ info, int64_t W, int L,
-                           uint8_t* __restrict__ J, int64_t* __restrict__ E, uint8_t* __restrict__ perm_out,
-                           int64_t blk, int64_t nblk) {
+__device__ void fsm_replay(gptr<const uint32_t> __restrict__ R, gptr<const uint32_t> __restrict__ Tpre,
+                           gptr<const ChunkStart> __restrict__ pieces, gptr<const int64_t> __restrict__ info, int64_t W,
+                           int L, gptr<uint8_t> __restrict__ J, gptr<int64_t> __restrict__ E,
+                           gptr<uint8_t> __restrict__ perm_out, int64_t blk, int64_t nblk) {
     extern __shared__ __attribute__((aligned(16))) uint8_t rlds[];
     const int64_t npieces = info[0], end = info[1];
     const int S = L - 1;
     const int lane = threadIdx.x;
     const int cap = replay_local_batches(L);
     for (int64_t pc = blk; pc < npieces; pc += nblk) {
-        const ChunkStart c = pieces[pc];
+        const ChunkStart c = get_piece(pieces, pc);
         const int64_t stop = (pc + 1 < npieces) ? pieces[pc + 1].pos : end;
         if (stop <= c.pos) continue;
         if (stop - c.pos <= kSub) {
@@ -711,12 +728,12 @@ __device__ void fsm_replay(const uint32_t* __restrict__ R, const uint32_t* __res
         }
         __syncthreads();
         // their perm bytes, contiguous in the window
-        uint8_t* dst = perm_out + b_lo * L;
+        const gptr<uint8_t> dst = perm_out + b_lo * L;
         const int nbytes = nloc * L;
-        if ((reinterpret_cast<uintptr_t>(dst) & 3) == 0) {
+        if (((uintptr_t)dst & 3) == 0) {
             const int nw = nbytes >> 2;
             for (int e = lane; e < nw; e += 64)
-                reinterpret_cast<uint32_t*>(dst)[e] = reinterpret_cast<const uint32_t*>(Pl)[e];
+                ((gptr<uint32_t>)dst)[e] = reinterpret_cast<const uint32_t*>(Pl)[e];
             for (int e = 4 * nw + lane; e < nbytes; e += 64) dst[e] = Pl[e];
         } else {
             for (int e = lane; e < nbytes; e += 64) dst[e] = Pl[e];
@@ -726,23 +743,26 @@ __device__ void fsm_replay(const uint32_t* __restrict__ R, const uint32_t* __res
 }
 
 __global__ __launch_bounds__(64) void k_fsm_replay(Job j, int L) {
-    fsm_replay<false>(j.R, j.Tpre, reinterpret_cast<const ChunkStart*>(j.pieces), j.info, j.W, L, j.J, j.E, nullptr,
-                      blockIdx.x, gridDim.x);
+    fsm_replay<false>(as_global(j.R), as_global(j.Tpre), as_global(reinterpret_cast<const ChunkStart*>(j.pieces)),
+                      as_global((const int64_t*)j.info), j.W, L, as_global(j.J), as_global(j.E), nullptr, blockIdx.x,
+                      gridDim.x);
 }
 
 __global__ __launch_bounds__(64) void k_fsm_replay_batch(const Job* __restrict__ jobs, int L) {
     const Job j = jobs[blockIdx.y];
     if (j.W <= 0) return;
-    fsm_replay<true>(j.R, j.Tpre, reinterpret_cast<const ChunkStart*>(j.pieces), j.info, j.W, L, j.J, j.E,
-                     j.perm_out, blockIdx.x, gridDim.x);
+    fsm_replay<true>(as_global(j.R), as_global(j.Tpre), as_global(reinterpret_cast<const ChunkStart*>(j.pieces)),
+                     as_global((const int64_t*)j.info), j.W, L, as_global(j.J), as_global(j.E), as_global(j.perm_out),
+                     blockIdx.x, gridDim.x);
 }
 
 // One lane per batch: Fisher-Yates swaps i = L-1..1 with the recorded j's.
-__device__ void fsm_perms(const uint8_t* __restrict__ J, int64_t W, int L, uint8_t* __restrict__ perm, int64_t b0) {
+__device__ void fsm_perms(gptr<const uint8_t> __restrict__ J, int64_t W, int L, gptr<uint8_t> __restrict__ perm,
+                          int64_t b0) {
     extern __shared__ uint8_t buf[];
     const int64_t b = b0 + threadIdx.x;
     if (b >= W) return;
-    const uint8_t* j = J + b * L;
+    const gptr<const uint8_t> j = J + b * L;
     if (j[0]) return;                    // shuffled by the replay itself (fsm_replay<true>)
     uint8_t* p = buf + threadIdx.x * L;
     for (int k = 0; k < L; ++k) p[k] = (uint8_t)k;
@@ -756,13 +776,13 @@ __device__ void fsm_perms(const uint8_t* __restrict__ J, int64_t W, int L, uint8
 }
 
 __global__ __launch_bounds__(256) void k_fsm_perms(Job j, int L) {
-    fsm_perms(j.J, j.W, L, j.perm_out, (int64_t)blockIdx.x * 256);
+    fsm_perms(as_global((const uint8_t*)j.J), j.W, L, as_global(j.perm_out), (int64_t)blockIdx.x * 256);
 }
 
 __global__ __launch_bounds__(256) void k_fsm_perms_batch(const Job* __restrict__ jobs, int L) {
     const Job j = jobs[blockIdx.y];
     for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < j.W; b0 += (int64_t)gridDim.x * 256)
-        fsm_perms(j.J, j.W, L, j.perm_out, b0);
+        fsm_perms(as_global((const uint8_t*)j.J), j.W, L, as_global(j.perm_out), b0);
 }
 
 __global__ void k_pick(const int32_t* stop, const int64_t* E, int64_t W, int64_t offset, int64_t last, int64_t* out) {
