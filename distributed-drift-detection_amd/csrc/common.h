@@ -30,9 +30,37 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // is folded away).
 template <typename T>
 using gptr = __attribute__((address_space(1))) T*;
+// ... and into LDS (ds_* instructions, counting on lgkmcnt only)
+template <typename T>
+using lptr = __attribute__((address_space(3))) T*;
 template <typename T>
 __device__ __forceinline__ gptr<T> as_global(T* p) {
     return (gptr<T>)p;
+}
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ int4 ld_int4(gptr<const int32_t> p) {   // 16-byte aligned
+    const i32x4 v = *(gptr<const i32x4>)p;
+    return make_int4(v.x, v.y, v.z, v.w);
+}
+// Whole-struct copies to / from the global address space (no implicit operator= across
+// address spaces): word-wise in the struct's own alignment, which the compiler merges.
+template <typename T>
+__device__ __forceinline__ void gput(gptr<T> p, const T& v) {
+    static_assert(sizeof(T) % 4 == 0, "word-sized structs only");
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(&v);
+    gptr<uint32_t> d = (gptr<uint32_t>)p;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); ++i) d[i] = s[i];
+}
+template <typename T>
+__device__ __forceinline__ T gget(gptr<const T> p) {
+    static_assert(sizeof(T) % 4 == 0, "word-sized structs only");
+    T v;
+    uint32_t* d = reinterpret_cast<uint32_t*>(&v);
+    gptr<const uint32_t> s = (gptr<const uint32_t>)p;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); ++i) d[i] = s[i];
+    return v;
 }
 
 // Cross-stream order by a sequence number in device memory (ddm_ctl_epoch.sync_flags):

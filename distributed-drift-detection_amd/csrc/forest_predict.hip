@@ -30,14 +30,14 @@ constexpr int kThreads = 256;
 constexpr int kMaxLdsForest = 64 * 1024;
 
 // first_err reduction: at most one atomicMin per wave (see the file comment).
-__device__ __forceinline__ void note_first_error(unsigned long long* first_err, int e, int64_t g, int lane,
+__device__ __forceinline__ void note_first_error(ddm::gptr<unsigned long long> first_err, int e, int64_t g, int lane,
                                                  bool& wave_done) {
     const unsigned long long m = __ballot(e);
     if (m && !wave_done) {
         wave_done = true;
         if (lane == __ffsll((long long)m) - 1 &&
             (unsigned long long)g < __hip_atomic_load(first_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-            atomicMin(first_err, (unsigned long long)g);
+            __hip_atomic_fetch_min(first_err, (unsigned long long)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -56,14 +56,20 @@ __device__ __forceinline__ int leaf_of(const ddm_node* __restrict__ nodes, int n
 
 // One segment of predict work: DDM positions [pos_begin, pos_end) of one partition with
 // its forest.  The batch entry point takes a device array of these (one per partition).
+// The row / position pointers as the global address space: their loads and stores are
+// global_* instructions, not flat_* (a flat load also counts on lgkmcnt, so every LDS wait
+// of the row phase -- rank tables, labels -- would wait for the next rows' prefetched labels)
+using ddm::gptr;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+using ddm::ld_int4;
 struct Seg {
     const float* X;
     int64_t ld;
-    const int32_t* y;
-    const uint8_t* perm;
-    uint8_t* err;
-    int32_t* pred;
-    unsigned long long* first_err;
+    gptr<const int32_t> y;
+    gptr<const uint8_t> perm;
+    gptr<uint8_t> err;
+    gptr<int32_t> pred;
+    gptr<unsigned long long> first_err;
     int64_t pos_begin, pos_end;
     const ddm_node* nodes;
     const int32_t* roots;
@@ -287,11 +293,11 @@ __device__ __forceinline__ void cf_segment(const Seg& sg, int64_t blk, int64_t n
     uint8_t* s_leaf = s_e + kRows * kCfThreads;
     float* s_x = reinterpret_cast<float*>(s_leaf + ((n_leaves + 15) & ~15));
     {
-        const uint32_t* gt = reinterpret_cast<const uint32_t*>(blob + ldu(&H->rank_tab_off));
+        gptr<const uint32_t> gt = (gptr<const uint32_t>)(blob + ldu(&H->rank_tab_off));
         for (int k = tid; k < tab_words; k += kCfThreads) s_tab[k] = gt[k];
     }
-    for (int k = tid; k < n_leaves; k += kCfThreads) s_leaf[k] = leafcls[k];
-    if (tid < 16) s_cls[tid] = H->classes[tid];
+    for (int k = tid; k < n_leaves; k += kCfThreads) s_leaf[k] = ((gptr<const uint8_t>)leafcls)[k];
+    if (tid < 16) s_cls[tid] = ((gptr<const int32_t>)H->classes)[tid];
     if (tid < 32) s_colp[tid] = sg.X + (int64_t)H->cols[tid] * sg.ld;
     uint32_t base_votes[kVR];
 #pragma unroll
@@ -472,10 +478,10 @@ __device__ __forceinline__ void cf_segment_vec(const Seg& sg, int64_t blk, int64
     int32_t* s_cls = s_pred + kVecRows * kCfThreads;
     uint8_t* s_e = reinterpret_cast<uint8_t*>(s_cls + 16);
     {
-        const uint32_t* gt = reinterpret_cast<const uint32_t*>(blob + ldu(&H->rank_tab_off));
+        gptr<const uint32_t> gt = (gptr<const uint32_t>)(blob + ldu(&H->rank_tab_off));
         for (int k = tid; k < tab_words; k += kCfThreads) s_tab[k] = gt[k];
     }
-    if (tid < 16) s_cls[tid] = H->classes[tid];
+    if (tid < 16) s_cls[tid] = ((gptr<const int32_t>)H->classes)[tid];
     if (tid < 32) s_colp[tid] = sg.X + (int64_t)H->cols[tid] * sg.ld;
     uint32_t base_votes[kVR];
 #pragma unroll
@@ -504,14 +510,14 @@ __device__ __forceinline__ void cf_segment_vec(const Seg& sg, int64_t blk, int64
     if (g0 < sg.pos_end) {
         const int64_t row = row_of(g0);
         if (U > 0) load_chunk(0, row, xa);
-        ynext = *reinterpret_cast<const int4*>(sg.y + row);
+        ynext = ld_int4(sg.y + row);
     }
     for (; g0 < sg.pos_end; g0 += step) {
         const int64_t row = row_of(g0);
         const bool has_next = g0 + step < sg.pos_end;
         const int64_t nrow = has_next ? row_of(g0 + step) : row;
         const int4 yv = ynext;
-        if (has_next) ynext = *reinterpret_cast<const int4*>(sg.y + nrow);
+        if (has_next) ynext = ld_int4(sg.y + nrow);
         uint32_t votes[kVecRows][kVR];
 #pragma unroll
         for (int i = 0; i < kVecRows; ++i)
@@ -573,7 +579,7 @@ __device__ __forceinline__ void cf_segment_vec(const Seg& sg, int64_t blk, int64
         int64_t g_first = g;
         if (q0 < tile && g < sg.pos_end) {
             const uint32_t p4 = (sg.flags & kSegRowOrder) ? 0x03020100u + (uint32_t)(q0 % pb) * 0x01010101u
-                                                          : *reinterpret_cast<const uint32_t*>(sg.perm + g);
+                                                          : *(gptr<const uint32_t>)(sg.perm + g);
             uint32_t out = 0;
             int first = -1;
 #pragma unroll
@@ -586,7 +592,7 @@ __device__ __forceinline__ void cf_segment_vec(const Seg& sg, int64_t blk, int64
                 if (ok && e && first < 0) first = i;
             }
             if (g + kVecRows <= sg.pos_end) {
-                *reinterpret_cast<uint32_t*>(sg.err + g) = out;
+                *(gptr<uint32_t>)(sg.err + g) = out;
             } else {
                 for (int i = 0; g + i < sg.pos_end; ++i) sg.err[g + i] = (uint8_t)((out >> (8 * i)) & 0xffu);
             }
@@ -881,7 +887,8 @@ extern "C" int ddm_forest_predict(const float* X, int64_t ld, int32_t n_features
     }
     const int64_t n = pos_end - pos_begin;
     if (n == 0) return 0;
-    Seg sg{X, ld, y, perm, err_out, pred_out, reinterpret_cast<unsigned long long*>(first_err), pos_begin, pos_end,
+    Seg sg{X, ld, (gptr<const int32_t>)y, (gptr<const uint8_t>)perm, (gptr<uint8_t>)err_out, (gptr<int32_t>)pred_out,
+           (gptr<unsigned long long>)first_err, pos_begin, pos_end,
            forest->nodes, forest->roots, forest->leaf_value, forest->classes, forest->n_trees, forest->n_classes,
            forest->n_nodes, forest->pure, 0, 0, 0, forest->cforest, forest->cf_slots, forest->cf_vote_regs,
            forest->cf_leaves, 0, forest->cf_tab_words, 0};
@@ -932,7 +939,7 @@ extern "C" int ddm_forest_predict_batch(const ddm_predict_segment* segs_host, dd
             return DDM_E_ARG;
         }
         if (g.first_err && !(g.flags & DDM_SEG_FIRST_ERR_PRESET))
-            if (int rc = ddm::hip_status(hipMemsetAsync(g.first_err, 0xff, sizeof(uint64_t), s), "predict_batch memset"))
+            if (int rc = ddm::hip_status(hipMemsetAsync((void*)g.first_err, 0xff, sizeof(uint64_t), s), "predict_batch memset"))
                 return rc;
     }
     if (ev_begin)
@@ -1068,7 +1075,7 @@ constexpr int kPermThreads = 256;
 __global__ __launch_bounds__(kPermThreads) void k_err_permute(const Seg* __restrict__ segs, int64_t delta, int pb) {
     const Seg sg = ldu(segs + blockIdx.y);
     if (sg.pos_end <= sg.pos_begin) return;
-    const uint8_t* src = sg.err + delta;
+    gptr<const uint8_t> src = sg.err + delta;
     const int64_t tid = (int64_t)blockIdx.x * kPermThreads + threadIdx.x;
     const int64_t step = (int64_t)gridDim.x * kPermThreads;
     const unsigned long long f = sg.first_err ? *sg.first_err : ~0ull;
@@ -1081,14 +1088,14 @@ __global__ __launch_bounds__(kPermThreads) void k_err_permute(const Seg* __restr
     {
         const int64_t a0 = min(zend, (sg.pos_begin + 15) & ~(int64_t)15), a1 = max(a0, zend & ~(int64_t)15);
         for (int64_t g = sg.pos_begin + tid; g < a0; g += step) sg.err[g] = 0;
-        for (int64_t w = a0 / 16 + tid; w < a1 / 16; w += step) reinterpret_cast<uint4*>(sg.err)[w] = make_uint4(0, 0, 0, 0);
+        for (int64_t w = a0 / 16 + tid; w < a1 / 16; w += step) ((gptr<u32x4>)sg.err)[w] = u32x4{0u, 0u, 0u, 0u};
         for (int64_t g = a1 + tid; g < zend; g += step) sg.err[g] = 0;
     }
     // the permutation: [zend, pos_end); zend is batch-aligned
     if (pb % 4 == 0 && zend % 4 == 0) {
         for (int64_t g = zend + 4 * tid; g < sg.pos_end; g += 4 * step) {
             const int64_t b0 = (g / pb) * pb;
-            const uint32_t p4 = *reinterpret_cast<const uint32_t*>(sg.perm + g);
+            const uint32_t p4 = *(gptr<const uint32_t>)(sg.perm + g);
             uint32_t out = 0;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -1097,7 +1104,7 @@ __global__ __launch_bounds__(kPermThreads) void k_err_permute(const Seg* __restr
                 out |= e << (8 * i);
             }
             if (g + 4 <= sg.pos_end) {
-                *reinterpret_cast<uint32_t*>(sg.err + g) = out;
+                *(gptr<uint32_t>)(sg.err + g) = out;
             } else {
                 for (int i = 0; g + i < sg.pos_end; ++i) sg.err[g + i] = (uint8_t)((out >> (8 * i)) & 0xffu);
             }

@@ -40,22 +40,29 @@ constexpr uint32_t kRandRMax = 0x7fffffffu;
 constexpr float kFeatureThreshold = 1e-7f;
 constexpr double kEpsilon = 2.220446049250313e-16;
 
+// The job's pointers as the global address space (device memory): the kernels' accesses
+// through them are global_* instructions instead of flat_* (which also count on lgkmcnt,
+// so every LDS wait waited for them too); pass (T*) casts where a callee also takes LDS.
+using ddm::gget;
+using ddm::lptr;
+using ddm::gptr;
+using ddm::gput;
 struct Job {
-    const float* X;
-    const int32_t* y;
-    const int64_t* seeds;
-    const int64_t* gate;
-    const int64_t* gate2;
+    gptr<const float> X;
+    gptr<const int32_t> y;
+    gptr<const int64_t> seeds;
+    gptr<const int64_t> gate;
+    gptr<const int64_t> gate2;
     int32_t L, F, n_trees, max_features;
     int32_t k_cap, pad;
-    uint8_t* scratch;
-    ddm_node* nodes;
-    int32_t* roots;
-    double* leaf_value;
-    int32_t* classes;
-    uint8_t* blob;
+    gptr<uint8_t> scratch;
+    gptr<ddm_node> nodes;
+    gptr<int32_t> roots;
+    gptr<double> leaf_value;
+    gptr<int32_t> classes;
+    gptr<uint8_t> blob;
     int64_t blob_cap;
-    int64_t* result;
+    gptr<int64_t> result;
 };
 static_assert(sizeof(Job) == sizeof(ddm_dfit_job), "Job must mirror ddm_dfit_job");
 
@@ -133,7 +140,7 @@ __device__ __forceinline__ uint32_t mt_word(uint32_t a, uint32_t b, uint32_t c) 
 // One MT19937 twist of mt[624] in place by one wave: words 0..226 from old words,
 // 227..453 from old words and new 0..226, 454..623 from old words and new 227..396
 // (and new 0 for the last).  Each phase computes into registers before it writes.
-__device__ void twist(uint32_t* mt, int lane) {
+__device__ void twist(lptr<uint32_t> mt, int lane) {
     uint32_t v[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -274,7 +281,7 @@ __device__ __forceinline__ void init_block(uint32_t& v, uint32_t& buf, uint32_t 
     }
 }
 
-__device__ uint32_t tree_boot(uint32_t seed, int L, uint32_t* mt, int32_t* cnt, int lane) {
+__device__ uint32_t tree_boot(uint32_t seed, int L, lptr<uint32_t> mt, lptr<int32_t> cnt, int lane) {
     // init_genrand: the recurrence on the scalar unit (a uniform value: s_mul_i32 and
     // friends, instead of quarter-rate wave64 VALU operations on one lane), each word put
     // into its lane of a VGPR by v_writelane (off the chain; 64 steps unrolled, so no branch
@@ -319,7 +326,8 @@ __device__ uint32_t tree_boot(uint32_t seed, int L, uint32_t* mt, int32_t* cnt, 
                 const uint32_t v = j < 624 ? (temper(mt[j]) & mask) : 0xffffffffu;
                 const bool acc = j < 624 && v <= mx;
                 const uint64_t m = __ballot(acc);
-                if (acc && taken + __popcll(m & lanemask_lt(lane)) < L) atomicAdd(&cnt[v], 1);
+                if (acc && taken + __popcll(m & lanemask_lt(lane)) < L)
+                    __hip_atomic_fetch_add(cnt + v, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
                 taken += __popcll(m);
             }
             if (taken >= L) break;
@@ -360,11 +368,11 @@ __device__ void dfit_boot(const Job& jb, int bblk) {
         jb.k_cap < 1 || jb.k_cap > kMaxK || jb.max_features < 1 || tree >= jb.n_trees)
         return;
     const Layout lo = layout(L, jb.F, jb.n_trees, jb.k_cap);
-    int32_t* bt = reinterpret_cast<int32_t*>(jb.scratch + lo.boot) + (int64_t)tree * (L + 1);
+    gptr<int32_t> bt = (gptr<int32_t>)(jb.scratch + lo.boot) + (int64_t)tree * (L + 1);
 #ifdef DDM_PREP_PROFILE
     const uint64_t tb0 = wall_clock64();
 #endif
-    const uint32_t rs = tree_boot((uint32_t)jb.seeds[tree], L, s_mt[w], s_cnt[w], lane);
+    const uint32_t rs = tree_boot((uint32_t)jb.seeds[tree], L, (lptr<uint32_t>)s_mt[w], (lptr<int32_t>)s_cnt[w], lane);
     if (lane == 0) bt[0] = (int32_t)rs;
     for (int k = lane; k < L; k += 64) bt[1 + k] = s_cnt[w][k];
 #ifdef DDM_PREP_PROFILE
@@ -433,8 +441,8 @@ __global__ __launch_bounds__(kPrepThreads) void k_dfit_prep(const Job* __restric
         return;
     }
     const Layout lo = layout(L, F, jb.n_trees, jb.k_cap);
-    uint8_t* yidx = jb.scratch + lo.yidx;
-    uint8_t* order = jb.scratch + lo.order;
+    gptr<uint8_t> yidx = jb.scratch + lo.yidx;
+    gptr<uint8_t> order = jb.scratch + lo.order;
     if (!one_tile) {
         for (int e = t; e < L * F; e += kPrepThreads)
             if (jb.X[e] != jb.X[e]) s_nan = 1;
@@ -704,9 +712,9 @@ __device__ __forceinline__ void build_tree(const Job& jb, const Layout& lo, int 
                                            uint32_t* mt) {
     const int L = jb.L, F = jb.F;
     const int64_t M = 2 * (int64_t)L - 1;
-    TNode* nodes = reinterpret_cast<TNode*>(jb.scratch + lo.tnodes) + tree * M;
-    double* vals = reinterpret_cast<double*>(jb.scratch + lo.tvals) + tree * M * jb.k_cap;
-    int32_t* meta = reinterpret_cast<int32_t*>(jb.scratch + lo.tmeta) + 4 * tree;
+    gptr<TNode> nodes = (gptr<TNode>)(jb.scratch + lo.tnodes) + tree * M;
+    gptr<double> vals = (gptr<double>)(jb.scratch + lo.tvals) + tree * M * jb.k_cap;
+    gptr<int32_t> meta = (gptr<int32_t>)(jb.scratch + lo.tmeta) + 4 * tree;
 
 #ifdef DDM_DFIT_PROFILE
     const uint64_t t_a = wall_clock64();
@@ -720,7 +728,7 @@ __device__ __forceinline__ void build_tree(const Job& jb, const Layout& lo, int 
         rstate = (uint32_t)bt[0];
         wave_sync();
     } else {
-        rstate = tree_boot((uint32_t)jb.seeds[tree], L, mt, S.cnt, lane);
+        rstate = tree_boot((uint32_t)jb.seeds[tree], L, (lptr<uint32_t>)mt, (lptr<int32_t>)S.cnt, lane);
     }
 #ifdef DDM_DFIT_PROFILE
     const uint64_t t_a1 = wall_clock64();
@@ -804,7 +812,7 @@ __device__ __forceinline__ void build_tree(const Job& jb, const Layout& lo, int 
                 if (S.ccnt[c] > S.ccnt[lc]) lc = c;
             nd.leaf = (uint8_t)(is_leaf ? 1 + lc : 0);   // 1 + leaf class, 0: internal
             nd.threshold = is_leaf ? -2.0 : sp_best.thr;
-            nodes[id] = nd;
+            gput(nodes + id, nd);
             if (parent >= 0) {
                 if (is_left) nodes[parent].left = (int16_t)id;
                 else nodes[parent].right = (int16_t)id;
@@ -950,9 +958,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfit_trees(const Job* __restric
     const int K = (int)jb.result[DDM_DFIT_CLASSES];
     const Layout lo = layout(jb.L, jb.F, jb.n_trees, jb.k_cap);
     const int LF = jb.L * jb.F;
-    const uint8_t* yidx = jb.scratch + lo.yidx;
-    const uint8_t* order = jb.scratch + lo.order;
-    const int32_t* boot = reinterpret_cast<const int32_t*>(jb.scratch + lo.boot);
+    const uint8_t* yidx = (const uint8_t*)(jb.scratch + lo.yidx);
+    const uint8_t* order = (const uint8_t*)(jb.scratch + lo.order);
+    const int32_t* boot = (const int32_t*)(gptr<const int32_t>)(jb.scratch + lo.boot);
     if (LF <= kTreeTile) {
         for (int e = threadIdx.x; e < LF; e += 64 * kWaves) {
             s_X[e] = jb.X[e];
@@ -962,7 +970,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_dfit_trees(const Job* __restric
         __syncthreads();
         if (tree < jb.n_trees) build_tree(jb, lo, tree, K, lds[w], lane, s_X, s_ord, s_yi, boot, nullptr);
     } else if (tree < jb.n_trees) {
-        build_tree(jb, lo, tree, K, lds[w], lane, jb.X, order, yidx, boot, nullptr);
+        build_tree(jb, lo, tree, K, lds[w], lane, (const float*)jb.X, order, yidx, boot, nullptr);
     }
 }
 
@@ -1318,8 +1326,8 @@ __device__ int64_t compile_forest(const TNode* tn, int64_t M, const int32_t* met
     return total;
 }
 
-__device__ void pack_tree(const TNode* tn, int m, int16_t* new_id, int16_t* queue, ddm_node* out, int64_t base,
-                          bool pure, const double* vals, int K, int kcap, double* leaf_value, int64_t leaf_row) {
+__device__ void pack_tree(const TNode* tn, int m, int16_t* new_id, int16_t* queue, gptr<ddm_node> out, int64_t base,
+                          bool pure, gptr<const double> vals, int K, int kcap, gptr<double> leaf_value, int64_t leaf_row) {
     if (m <= 3) {
         // a single leaf or a stump: pre-order ids are already the BFS ids (C3's trees), so
         // no queue; the nodes are loaded before anything is stored
@@ -1345,7 +1353,7 @@ __device__ void pack_tree(const TNode* tn, int m, int16_t* new_id, int16_t* queu
                     nd.child = (int32_t)leaf_row++;
                 }
             }
-            out[base + u] = nd;
+            gput(out + base + u, nd);
         }
         return;
     }
@@ -1379,7 +1387,7 @@ __device__ void pack_tree(const TNode* tn, int m, int16_t* new_id, int16_t* queu
                 nd.child = (int32_t)leaf_row++;
             }
         }
-        out[base + new_id[u]] = nd;
+        gput(out + base + new_id[u], nd);
     }
 }
 
@@ -1392,10 +1400,10 @@ __device__ __forceinline__ void pack_job(const Job& jb) {
     const int T = jb.n_trees, K = (int)jb.result[DDM_DFIT_CLASSES];
     const Layout lo = layout(jb.L, jb.F, T, jb.k_cap);
     const int64_t M = 2 * (int64_t)jb.L - 1;
-    const int32_t* meta = reinterpret_cast<const int32_t*>(jb.scratch + lo.tmeta);
-    const TNode* tn = reinterpret_cast<const TNode*>(jb.scratch + lo.tnodes);
-    const double* tv = reinterpret_cast<const double*>(jb.scratch + lo.tvals);
-    int16_t* bfs = reinterpret_cast<int16_t*>(jb.scratch + lo.bfs);
+    gptr<const int32_t> meta = (gptr<const int32_t>)(jb.scratch + lo.tmeta);
+    gptr<const TNode> tn = (gptr<const TNode>)(jb.scratch + lo.tnodes);
+    gptr<const double> tv = (gptr<const double>)(jb.scratch + lo.tvals);
+    gptr<int16_t> bfs = (gptr<int16_t>)(jb.scratch + lo.bfs);
     __shared__ int s_tmp[kPackThreads];
     __shared__ int s_impure;
     __shared__ TNode s_tn[kPackLdsNodes];
@@ -1414,11 +1422,11 @@ __device__ __forceinline__ void pack_job(const Job& jb) {
             // the tree's nodes, its BFS ids and queue in LDS (each thread its own range): the
             // queue walk and the node loop wait on LDS, not on a global round trip per node
 #pragma unroll 4
-            for (int u = 0; u < nn; ++u) s_tn[base + u] = tn[t * M + u];
+            for (int u = 0; u < nn; ++u) s_tn[base + u] = gget(tn + t * M + u);
             pack_tree(s_tn + base, nn, s_bid + base, s_bid + n_nodes + base, jb.nodes, base, pure,
                       tv + t * M * jb.k_cap, K, jb.k_cap, jb.leaf_value, lbase);
         } else {
-            pack_tree(tn + t * M, nn, bfs + 2 * t * M, bfs + 2 * t * M + M, jb.nodes, base, pure, tv + t * M * jb.k_cap,
+            pack_tree((const TNode*)(tn + t * M), nn, (int16_t*)(bfs + 2 * t * M), (int16_t*)(bfs + 2 * t * M + M), jb.nodes, base, pure, tv + t * M * jb.k_cap,
                       K, jb.k_cap, jb.leaf_value, lbase);
         }
         jb.roots[t] = base;
@@ -1428,12 +1436,13 @@ __device__ __forceinline__ void pack_job(const Job& jb) {
 #endif
     int64_t bytes = 0;
     if (pure && jb.blob)
-        bytes = compile_forest(tn, M, meta, T, jb.classes, K, jb.F, bfs, jb.blob, jb.blob_cap,
+        bytes = compile_forest((const TNode*)tn, M, (const int32_t*)meta, T, (const int32_t*)jb.classes, K, jb.F, (int16_t*)bfs,
+                               (uint8_t*)jb.blob, jb.blob_cap,
                                n_nodes <= kPackLdsNodes ? s_tn : nullptr, s_bid, base);
 #ifdef DDM_DFIT_PROFILE
     if (t == 0)
         jb.result[11] = (int64_t)((t_p - t_pack0) | ((wall_clock64() - t_p) << 16) |
-                                  (bytes ? (uint64_t)*reinterpret_cast<const uint32_t*>(bfs) << 32 : 0));
+                                  (bytes ? (uint64_t)*(gptr<const uint32_t>)bfs << 32 : 0));
 #endif
     if (t == 0) {
         jb.result[DDM_DFIT_NODES] = n_nodes;
@@ -1441,7 +1450,7 @@ __device__ __forceinline__ void pack_job(const Job& jb) {
         jb.result[DDM_DFIT_LEAF_ROWS] = pure ? 0 : n_leaf;
         jb.result[DDM_DFIT_BLOB] = bytes;
         if (bytes) {
-            const ddm_cforest_head* h = reinterpret_cast<const ddm_cforest_head*>(jb.blob);
+            gptr<const ddm_cforest_head> h = (gptr<const ddm_cforest_head>)jb.blob;
             jb.result[DDM_DFIT_CF_SLOTS] = h->n_slots;
             jb.result[DDM_DFIT_CF_VR] = h->vote_regs;
             jb.result[DDM_DFIT_CF_LEAVES] = h->n_leaves;

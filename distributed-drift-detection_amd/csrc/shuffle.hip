@@ -55,7 +55,7 @@ __device__ __forceinline__ uint32_t imask(uint32_t i) { return 0xffffffffu >> __
 // dependency phases (words 0..226 need only old words; 227..453 need new 0..226;
 // 454..623 need new 227..396 and new 0), each thread tempering and storing the words it
 // produced, so a 624-word block costs three barriers.
-__device__ void mt_generate(uint32_t* __restrict__ state, uint32_t* __restrict__ R, int64_t n) {
+__device__ void mt_generate(gptr<uint32_t> __restrict__ state, gptr<uint32_t> __restrict__ R, int64_t n) {
     __shared__ uint32_t buf[2][kN];
     for (int k = threadIdx.x; k < kN; k += 256) buf[0][k] = state[k];
     const int pos0 = (int)state[kN];
@@ -106,7 +106,7 @@ __device__ void mt_generate(uint32_t* __restrict__ state, uint32_t* __restrict__
 
 __global__ __launch_bounds__(256) void k_mt_generate(uint32_t* __restrict__ state, uint32_t* __restrict__ R,
                                                      int64_t n) {
-    mt_generate(state, R, n);
+    mt_generate(as_global(state), as_global(R), n);
 }
 
 // g(T) * key on the device.  T^i(key) is the window (x_i .. x_{i+623}) of the MT19937
@@ -191,7 +191,7 @@ struct GenJob {
 
 __global__ __launch_bounds__(256) void k_mt_generate_batch(const GenJob* __restrict__ jobs) {
     const GenJob j = jobs[blockIdx.x];
-    mt_generate(j.state, j.R, j.n);
+    mt_generate(as_global(j.state), as_global(j.R), j.n);
 }
 
 __device__ __forceinline__ void fsm_step(uint32_t v, uint32_t& s, uint32_t& d, uint32_t S) {

@@ -24,33 +24,34 @@ namespace {
 constexpr int kStageThreads = 1024;
 constexpr int kStageWords = 1024;   // stream words in LDS for one shuffle + the seeds
 
+using ddm::gptr;
 struct Job {
-    const float* X;
+    gptr<const float> X;
     int64_t ld;
-    const int32_t* y;
-    const uint8_t* perm;
+    gptr<const int32_t> y;
+    gptr<const uint8_t> perm;
     int64_t base;
-    const int32_t* ev;
-    const int32_t* stop;
-    const int64_t* pick;
-    const uint32_t* R;
+    gptr<const int32_t> ev;
+    gptr<const int32_t> stop;
+    gptr<const int64_t> pick;
+    gptr<const uint32_t> R;
     int64_t j, g0, nb, b_end, p_after_first, p_tail_after;
     int32_t pb, last_len, n_features, n_words, tail, max_events;
-    float* x_out;
-    int32_t* y_out;
-    uint32_t* w_out;
-    int64_t* info_out;
-    int32_t* ev_out;
-    uint8_t* perm_w;
-    int64_t* seeds_out;
+    gptr<float> x_out;
+    gptr<int32_t> y_out;
+    gptr<uint32_t> w_out;
+    gptr<int64_t> info_out;
+    gptr<int32_t> ev_out;
+    gptr<uint8_t> perm_w;
+    gptr<int64_t> seeds_out;
     int32_t n_trees, win_rule;
     int64_t p_now, win, max_win, seg_start, n_full, min_win, next_avail, dpb_x1024;
-    int64_t* plan_out;
+    gptr<int64_t> plan_out;
     ddm_shuffle_job* next_job;
-    int32_t* log;
-    int64_t* log_n;
+    gptr<int32_t> log;
+    gptr<int64_t> log_n;
     int64_t log_cap;
-    const int32_t* stall;
+    gptr<const int32_t> stall;
 };
 static_assert(sizeof(Job) == sizeof(ddm_stage_job), "Job must mirror ddm_stage_job");
 
@@ -88,7 +89,7 @@ __device__ void plan_next(const Job& jb, int32_t stop, bool drawn, int64_t p_see
         ok = false;
     }
     if (!ok) Wn = 0;
-    int64_t* po = jb.plan_out;
+    gptr<int64_t> po = jb.plan_out;
     po[0] = Pn;
     po[1] = Wn;
     po[2] = g0n;
@@ -98,7 +99,7 @@ __device__ void plan_next(const Job& jb, int32_t stop, bool drawn, int64_t p_see
     if (jb.next_job) {
         jb.next_job->P = Pn;
         jb.next_job->W = Wn;
-        jb.next_job->perm_out = const_cast<uint8_t*>(jb.perm) + jb.base + g0n * jb.pb;
+        jb.next_job->perm_out = (uint8_t*)(gptr<uint8_t>)jb.perm + jb.base + g0n * jb.pb;
         jb.next_job->avail = jb.next_avail;
     }
 }
@@ -148,7 +149,7 @@ __device__ void stage_body(const Job& jb, int64_t pickv, int64_t pos_next = -1) 
         const bool vec = r0 + 8 <= nrows && ((reinterpret_cast<uintptr_t>(jb.ev + 2 * r0) & 15) == 0);
         if (vec) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) q[k] = reinterpret_cast<const int4*>(jb.ev + 2 * r0)[k];
+            for (int k = 0; k < 4; ++k) q[k] = ddm::ld_int4(jb.ev + 2 * r0 + 4 * k);
         } else {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -180,7 +181,7 @@ __device__ void stage_body(const Job& jb, int64_t pickv, int64_t pos_next = -1) 
 #pragma unroll
         for (int w = 0; w < kStageThreads / 64; ++w) round += counts[w];
         int k = before + incl - c;
-        int32_t* out = jb.log ? jb.log + 3 * log0 : jb.ev_out;
+        gptr<int32_t> out = jb.log ? jb.log + 3 * log0 : jb.ev_out;
         const int32_t boff = jb.log ? (int32_t)jb.j : 0;
         while (bits && k < cap) {
             const int s = __builtin_ctz(bits);
