@@ -28,7 +28,7 @@ namespace {
 constexpr int kCtlThreads = 256;
 constexpr int kCtlWaves = kCtlThreads / 64;
 
-// The decisions of every partition (a wave per record), then the grid split (one thread).
+// The decisions of every partition (a wave per record), then the grid split (one wave).
 __global__ __launch_bounds__(kCtlThreads) void k_ctl(const ddm_ctl c) {
     __shared__ ddm_ctl_part s_part[kCtlWaves];
     const int t = threadIdx.x;
@@ -36,7 +36,7 @@ __global__ __launch_bounds__(kCtlThreads) void k_ctl(const ddm_ctl c) {
     for (int i = w; i < c.n; i += kCtlWaves) ctl_record(c, i, &s_part[w], lane, c.entry);
     __threadfence();
     __syncthreads();
-    if (t == 0) ctl_split(c);
+    if (t < 64) ctl_split(c, t);
 }
 
 int launch_ctl(const ddm_ctl& c, int entry, hipStream_t s) {

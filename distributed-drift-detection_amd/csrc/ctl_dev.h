@@ -191,10 +191,19 @@ __device__ void plan(const ddm_ctl& c, ddm_ctl_part& p, int i) {
     st.next_job = nullptr;
 }
 
+// The words commit reads from other kernels' outputs, fetched by the record's wave at once
+// (ctl_record) instead of one dependent load after another by lane 0.
+struct CommitPre {
+    int64_t pstall, stop, lend, loff, slots, info0, info4, info5, info6, pick;
+    ddm_state state;
+};
+constexpr int kPreWords = (int)(sizeof(CommitPre) / 8);
+static_assert(sizeof(CommitPre) % 8 == 0 && kPreWords <= 64, "CommitPre: 64-bit words, one per lane");
+
 // _epoch_after for one partition (after the scan, the pick and the staging of the epoch).
-__device__ void commit(const ddm_ctl& c, ddm_ctl_part& p, int i) {
+__device__ void commit(const ddm_ctl& c, ddm_ctl_part& p, int i, const CommitPre& q) {
     if (p.idle || p.done || p.park) return;
-    if (c.pstall[i]) {                              // the predict found the refit unusable
+    if (q.pstall) {                                 // the predict found the refit unusable
         // the predict wrote no errors for this window, so the scans read stale bytes: their
         // events are void (the host redoes the epoch)
         p.n_log = p.log_mark;
@@ -206,13 +215,13 @@ __device__ void commit(const ddm_ctl& c, ddm_ctl_part& p, int i) {
         }
         return;
     }
-    const int32_t stop = c.stop[i];
+    const int32_t stop = (int32_t)q.stop;
     p.epochs += 1;
-    if (c.lend[i] > c.loff[i]) p.long_scans += 1;   // this epoch's window ran on ddm_scan_long
+    if (q.lend > q.loff) p.long_scans += 1;   // this epoch's window ran on ddm_scan_long
     const int64_t rows = p.p1 - p.p0;
     p.predicted_rows += rows;
     int64_t slots = p.host_slots;
-    if (p.forest_dev && p.res) slots = p.res[DDM_DFIT_CF_SLOTS];
+    if (p.forest_dev && p.res) slots = q.slots;
     // algorithmic bytes of the predict kernel: the referenced feature columns and the label,
     // the error byte written, and (coupled epochs) the in-batch permutation byte read; a
     // decoupled epoch's permutation into DDM order is k_err_permute's (counted by its rows)
@@ -224,27 +233,26 @@ __device__ void commit(const ddm_ctl& c, ddm_ctl_part& p, int i) {
     }
     if (stop >= 0) {
         const int64_t d = p.j + stop;
-        const int64_t* info = p.stage.info_out;
-        const int64_t P_at = info[0];               // the staging's: after batch d's shuffle
+        const int64_t P_at = q.info0;               // the staging's: after batch d's shuffle
         p.P = P_at;
         const int64_t seg = d - p.seg_start + 1;
         p.win = drift_window(seg, p.min_win, p.win_rule);   // the next concept, with a margin
         p.j = d + 1;
         if (p.j >= p.nb) {
             p.done = 1;
-        } else if (info[6] != 1) {
+        } else if (q.info6 != 1) {
             p.stall = DDM_CTL_STALL_WORDS;          // the host draws batch j's shuffle and the seeds
             p.retrain = 1;
         } else {
             p.retrain = 1;                          // the device refit runs this epoch
-            p.P1 = info[4];
-            p.P2 = info[5];
+            p.P1 = q.info4;
+            p.P2 = q.info5;
         }
         return;
     }
-    if (p.Wg > 0) p.P = c.pick[i] + 1;
+    if (p.Wg > 0) p.P = q.pick + 1;
     else if (p.P_after_first >= 0) p.P = p.P_after_first;
-    p.state = c.state[i];
+    p.state = q.state;
     p.j = p.b_end;
     p.win *= 2;
     if (p.j >= p.nb) p.done = 1;
@@ -265,10 +273,32 @@ __device__ __forceinline__ int ctl_record(const ddm_ctl& c, int i, ddm_ctl_part*
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // lane k fetches word k of CommitPre (the reads commit would make one after another)
+    int64_t v = 0;
+    if (!entry && lane < kPreWords) {
+        const ddm_ctl_part& r = *lds_part;
+        switch (lane) {
+            case 0: v = c.pstall[i]; break;
+            case 1: v = c.stop[i]; break;
+            case 2: v = c.lend[i]; break;
+            case 3: v = c.loff[i]; break;
+            case 4: v = (r.forest_dev && r.res) ? r.res[DDM_DFIT_CF_SLOTS] : 0; break;
+            case 5: v = r.stage.info_out ? r.stage.info_out[0] : 0; break;
+            case 6: v = r.stage.info_out ? r.stage.info_out[4] : 0; break;
+            case 7: v = r.stage.info_out ? r.stage.info_out[5] : 0; break;
+            case 8: v = r.stage.info_out ? r.stage.info_out[6] : 0; break;
+            case 9: v = c.pick ? c.pick[i] : 0; break;
+            default: v = reinterpret_cast<const int64_t*>(c.state + i)[lane - 10]; break;
+        }
+    }
+    CommitPre pre;
+    int64_t* pw = reinterpret_cast<int64_t*>(&pre);
+#pragma unroll
+    for (int k = 0; k < kPreWords; ++k) pw[k] = __shfl(v, k, 64);
     int st = 0;
     if (lane == 0) {
         ddm_ctl_part& p = *lds_part;
-        if (!entry) commit(c, p, i);
+        if (!entry) commit(c, p, i, pre);
         plan(c, p, i);
         st = p.done ? 3 : p.stall ? 1 : p.park ? 2 : 0;
     }
@@ -284,34 +314,64 @@ __device__ __forceinline__ int ctl_record(const ddm_ctl& c, int i, ddm_ctl_part*
 
 // After every record: the predict grid split over the windows in proportion to their rows
 // (at least one block per non-empty window), the status counts, and whether the next epoch
-// has a long window (ddm_scan_long's blocks return at once when none has).  One thread.
-__device__ __forceinline__ void ctl_split(const ddm_ctl& c) {
+// has a long window (ddm_scan_long's blocks return at once when none has).  One wave, a
+// partition per lane (64 at a time): the records' loads are issued together instead of one
+// dependent load after another by one thread (10.8 -> ~2 us at the end of every epoch).
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ void ctl_split(const ddm_ctl& c, int lane) {
     int64_t total = 0, nz = 0;
-    int any_long = 0;
-    for (int i = 0; i < c.n; ++i) {
-        const int64_t r = c.segs[i].pos_end - c.segs[i].pos_begin;
+    bool any_long = false;
+    int64_t cnt[4] = {0, 0, 0, 0};
+    for (int b = 0; b < c.n; b += 64) {
+        const int i = b + lane;
+        int64_t r = 0;
+        int cls = -1;
+        if (i < c.n) {
+            r = c.segs[i].pos_end - c.segs[i].pos_begin;
+            any_long |= c.lend[i] > c.loff[i];
+            if (c.status) {
+                const ddm_ctl_part& p = c.parts[i];
+                cls = p.done ? 3 : p.stall ? 1 : p.park ? 2 : 0;
+            }
+        }
         total += r;
         nz += r > 0;
-        any_long |= c.lend[i] > c.loff[i];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cnt[k] += __popcll(__ballot(cls == k));
     }
+    total = wave_sum_i64(total);
+    nz = wave_sum_i64(nz);
+    const bool long_any = __ballot(any_long) != 0;
     int64_t b0 = 0;
     const int64_t spare = max((int64_t)0, c.predict_blocks - nz);
-    for (int i = 0; i < c.n; ++i) {
-        const int64_t r = c.segs[i].pos_end - c.segs[i].pos_begin;
-        int64_t nbk = r > 0 ? 1 + (total > 0 ? spare * r / total : 0) : 0;
-        nbk = min(nbk, max((int64_t)r > 0 ? 1 : 0, (r + 499) / 500));   // no more blocks than 500-row tiles
-        c.segs[i].block0 = b0;
-        c.segs[i].nblocks = nbk;
-        b0 += nbk;
-    }
-    if (c.sync) c.sync[1] = (uint32_t)any_long;
-    if (c.status) {
-        int64_t cnt[4] = {0, 0, 0, 0};
-        for (int i = 0; i < c.n; ++i) {
-            const ddm_ctl_part& p = c.parts[i];
-            ++cnt[p.done ? 3 : p.stall ? 1 : p.park ? 2 : 0];
+    for (int b = 0; b < c.n; b += 64) {
+        const int i = b + lane;
+        int64_t nbk = 0;
+        if (i < c.n) {
+            const int64_t r = c.segs[i].pos_end - c.segs[i].pos_begin;
+            nbk = r > 0 ? 1 + (total > 0 ? spare * r / total : 0) : 0;
+            nbk = min(nbk, max((int64_t)r > 0 ? 1 : 0, (r + 499) / 500));   // no more blocks than 500-row tiles
         }
-        for (int k = 0; k < 4; ++k) c.status[k] = cnt[k];
+        int64_t incl = nbk;                         // inclusive prefix over the lanes
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t u = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += u;
+        }
+        if (i < c.n) {
+            c.segs[i].block0 = b0 + incl - nbk;
+            c.segs[i].nblocks = nbk;
+        }
+        b0 += __shfl(incl, 63, 64);
+    }
+    if (lane == 0) {
+        if (c.sync) c.sync[1] = (uint32_t)long_any;
+        if (c.status)
+            for (int k = 0; k < 4; ++k) c.status[k] = cnt[k];
     }
 }
 

@@ -405,6 +405,9 @@ __global__ __launch_bounds__(kStageThreads) void k_stage_ctl(const Job* __restri
     const int t = threadIdx.x;
     const int i = (int)blockIdx.x;
     const Job jb = jobs[i];
+#ifdef DDM_STAGE_PROFILE
+    const uint64_t tk0 = wall_clock64();
+#endif
     if (c.predict_clock && i == 0 && t < 64) {
         // the epoch's predict launch: its span on the device clock into the running sum (the
         // 16 shards read and reset by 16 lanes at once, then reduced over the wave)
@@ -449,19 +452,39 @@ __global__ __launch_bounds__(kStageThreads) void k_stage_ctl(const Job* __restri
         s_next = nx;
     }
     __syncthreads();
+#ifdef DDM_STAGE_PROFILE
+    const uint64_t tk1 = wall_clock64();
+#endif
     stage_body(jb, s_pick, s_next);
     __syncthreads();
+#ifdef DDM_STAGE_PROFILE
+    const uint64_t tk2 = wall_clock64();
+#endif
     if (t < 64) ctl_record(c, i, &s_part, t, 0);
+#ifdef DDM_STAGE_PROFILE
+    const uint64_t tk3 = wall_clock64();
+#endif
     __threadfence();
     __syncthreads();
     if (t == 0) s_last = atomicAdd(c.sync, 1u) == gridDim.x - 1;
     __syncthreads();
-    if (s_last && t == 0) {
+#ifdef DDM_STAGE_PROFILE
+    const uint64_t tk4 = wall_clock64();
+#endif
+    if (s_last && t < 64) {
         __threadfence();
-        ctl_split(c);
-        c.sync[0] = 0;                              // the ticket, for the next epoch
-        if (fs.pub) ddm::flag_publish(fs.pub, fs.pub_v);   // the fork (ctl.hip): every block's
-    }                                                       // records are released before its ticket
+        ctl_split(c, t);
+        if (t == 0) {
+            c.sync[0] = 0;                          // the ticket, for the next epoch
+            if (fs.pub) ddm::flag_publish(fs.pub, fs.pub_v);   // the fork (ctl.hip): every block's
+        }                                                   // records are released before its ticket
+    }
+#ifdef DDM_STAGE_PROFILE
+    if (t == 0)
+        printf("stage-ctl block %d scan+pick %.2f stage %.2f record %.2f ticket %.2f split %.2f us%s\n", i,
+               (tk1 - tk0) / 100.0, (tk2 - tk1) / 100.0, (tk3 - tk2) / 100.0, (tk4 - tk3) / 100.0,
+               (wall_clock64() - tk4) / 100.0, s_last ? " (last)" : "");
+#endif
 }
 
 }  // namespace
