@@ -30,6 +30,8 @@ using ddm::gptr;
 
 namespace {
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 constexpr int kN = 624;
 constexpr int kSub = 128;            // draws per sub-chunk
 constexpr int kSubPerChunk = 64;     // sub-chunks per chunk
@@ -231,8 +233,8 @@ struct TabJob {
     uint32_t* Tchunk;
 };
 
-__device__ void fsm_prefix(const uint32_t* __restrict__ R, int64_t chunk0, int64_t nchunk, int L,
-                           uint32_t* __restrict__ Tpre, uint32_t* __restrict__ Tchunk, int64_t blk) {
+__device__ void fsm_prefix(gptr<const uint32_t> __restrict__ R, int64_t chunk0, int64_t nchunk, int L,
+                           gptr<uint32_t> __restrict__ Tpre, gptr<uint32_t> __restrict__ Tchunk, int64_t blk) {
     extern __shared__ __attribute__((aligned(16))) uint32_t pre_lds[];
     constexpr int kW = kPreThreads / 64;
     __shared__ int wsum[kW];
@@ -267,8 +269,8 @@ __device__ void fsm_prefix(const uint32_t* __restrict__ R, int64_t chunk0, int64
         __syncthreads();
         for (int e = tid; e < nc * (kSub / 4); e += kPreThreads) {
             const int c = e / (kSub / 4), q = e % (kSub / 4);
-            *reinterpret_cast<uint4*>(draws + c * kPreRow + 4 * q) =
-                *reinterpret_cast<const uint4*>(R + (cb + c) * kChunk + (int64_t)k * kSub + 4 * q);
+            *reinterpret_cast<u32x4*>(draws + c * kPreRow + 4 * q) =
+                *(gptr<const u32x4>)(R + (cb + c) * kChunk + (int64_t)k * kSub + 4 * q);
         }
         __syncthreads();
         const int n = n_sh;
@@ -345,12 +347,12 @@ __device__ void fsm_prefix(const uint32_t* __restrict__ R, int64_t chunk0, int64
 __global__ __launch_bounds__(kPreThreads) void k_fsm_prefix(const uint32_t* __restrict__ R, int64_t chunk0,
                                                             int64_t nchunk, int L, uint32_t* __restrict__ Tpre,
                                                             uint32_t* __restrict__ Tchunk) {
-    fsm_prefix(R, chunk0, nchunk, L, Tpre, Tchunk, blockIdx.x);
+    fsm_prefix(as_global(R), chunk0, nchunk, L, as_global(Tpre), as_global(Tchunk), blockIdx.x);
 }
 
 __global__ __launch_bounds__(kPreThreads) void k_fsm_prefix_batch(const TabJob* __restrict__ jobs, int L) {
     const TabJob j = jobs[blockIdx.y];
-    fsm_prefix(j.R, j.chunk0, j.nchunk, L, j.Tpre, j.Tchunk, blockIdx.x);
+    fsm_prefix(as_global(j.R), j.chunk0, j.nchunk, L, as_global(j.Tpre), as_global(j.Tchunk), blockIdx.x);
 }
 
 struct Job {
@@ -375,7 +377,6 @@ struct ChunkStart {
     int32_t batch;    // batches completed (relative to the window) before pos
 };
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void put_piece(gptr<ChunkStart> out, int64_t k, int64_t pos, int32_t state, int32_t batch) {
     out[k].pos = pos;
