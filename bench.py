@@ -74,8 +74,8 @@ SEED = 20261015
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c3w", "c1", "c4", "c5"])
     ap.add_argument("--c2-mult", type=int, default=512, help="c2 MULT_DATA")
     ap.add_argument("--c2-instances", type=int, default=16, help="c2 INSTANCES")
@@ -475,14 +475,19 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    allocs0 = torch.cuda.memory_stats(dev).get("num_device_alloc", 0)
+    step_ms = []
     t0 = time.perf_counter()
     for k in range(args.steps):
+        ts = time.perf_counter()
         results.clear()
-        step()
+        step()                            # returns with the run's outputs on the host
+        step_ms.append((time.perf_counter() - ts) * 1e3)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    timed_allocs = torch.cuda.memory_stats(dev).get("num_device_alloc", 0) - allocs0
     runner.set_predict_timing(False)
     for g, r in results.items():          # every step reproduces the same events
         if args.warmup and not np.array_equal(r, ref_events[g]):
@@ -586,6 +591,8 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
              "device_refit_kernels_ms_per_step": agg["dfit_ms"] / args.steps,
              "host_s_per_step": agg["host_s"] / args.steps, "gpu_wait_s_per_step": agg["gpu_s"] / args.steps,
              "stream_prep_s_per_step": agg["prep_s"] / args.steps,
+             "timed_step_ms": [round(v, 3) for v in step_ms],
+             "device_allocs_in_timed_steps": timed_allocs,
              "kernel_ms_from": "one instrumented step after the timed ones (HIP events around each launch)",
              "gather_ms_per_step": gather_s[0] / args.steps * 1e3 if world > 1 else None,
              "gather_backend": (None if world == 1 else "rccl (ctypes ncclAllGather, HBM to HBM)" if args.comm
