@@ -102,6 +102,8 @@ def parse():
                     help="rows of partition 0 re-run by the oracle after the timed region (0: off)")
     ap.add_argument("--c4-streams", type=int, default=1_000_000)
     ap.add_argument("--c4-len", type=int, default=4096)
+    ap.add_argument("--c4-check-stride", type=int, default=16,
+                    help="c4: run the C oracle on every k-th stream after the timed calls (1: all, 0: off)")
     ap.add_argument("--c5-rows", type=int, default=64_000_000, help="c5 rows (all partitions)")
     ap.add_argument("--c5-flip", type=float, default=0.0, help="c5 label-noise rate")
     ap.add_argument("--drift-window", type=int, default=0,
@@ -733,6 +735,42 @@ def run_c1(args, world, rank, dev, torch, dist, cpu):
     return n * args.steps, elapsed, info, extra, roofline, cpu_res, "replicas"
 
 
+def c4_checks(args, err, ev, state, S, L, nb, rank):
+    """After the timed calls: the digest of the last call's events and states, and the C
+    oracle (oracle/scan.py, DDM_Process.py:135-159 with the reset of :207-210) on every
+    `--c4-check-stride`-th stream (1: all of them), events and states bit for bit."""
+    import numpy as np
+    from ddm_amd import kernels
+    from oracle.scan import scan_equal_streams
+    evh = ev.cpu().numpy()
+    sth = state.cpu().numpy().view(kernels.STATE_DTYPE)[:S]
+    h = hashlib.sha1()
+    h.update(evh.tobytes())
+    h.update(sth.tobytes())
+    k = max(1, int(args.c4_check_stride))
+    sub = err[:S * L].view(S, L)[::k].contiguous().cpu().numpy()
+    n = sub.shape[0]
+    t = time.perf_counter()
+    oev, ost = scan_equal_streams(sub.reshape(-1), n, L, mode=1, threads=16)
+    dt = time.perf_counter() - t
+    gev = evh.reshape(S, nb, 2)[::k].reshape(-1, 2)
+    gst = np.stack([sth["miss_prob"], sth["miss_std"], sth["miss_prob_min"], sth["miss_sd_min"],
+                    sth["miss_prob_sd_min"], sth["sample_count"].astype(np.float64),
+                    sth["in_concept_change"].astype(np.float64), sth["in_warning_zone"].astype(np.float64)],
+                   axis=1)[::k]
+    ok_ev = bool(np.array_equal(gev, oev))
+    ok_st = bool(np.array_equal(gst, ost))
+    if not (ok_ev and ok_st):
+        bad = np.nonzero((gev.reshape(n, nb, 2) != oev.reshape(n, nb, 2)).any(axis=(1, 2)))[0]
+        print(f"[rank {rank}] c4 oracle check FAILED: {len(bad)} of {n} sampled streams differ "
+              f"(first: stream {int(bad[0]) * k if len(bad) else -1}); states equal: {ok_st}", file=sys.stderr)
+        raise SystemExit(3)
+    return {"events_sha1": h.hexdigest(), "oracle_streams": n, "oracle_stride": k, "oracle_equal": True,
+            "oracle_s": dt, "events_sha1_note": "sha1 of the last call's ev int32 [S*nb, 2] then its ddm_state "
+                                                "records; oracle_*: oracle/ddm_scan.c on every oracle_stride-th "
+                                                "stream, events and states bit for bit"}
+
+
 def run_c4(args, world, rank, dev, torch, dist, cpu):
     """configs[3]: 1M independent error streams x 4096 rows, DDM only, fresh DDM after each change."""
     import numpy as np
@@ -772,6 +810,7 @@ def run_c4(args, world, rank, dev, torch, dist, cpu):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     changes = int((ev[:, 1] >= 0).sum().item())
+    checks = c4_checks(args, err, ev, state, S, L, nb, rank) if args.c4_check_stride > 0 else {}
     # rows the DDM actually consumes: a batch is read up to its change (DDM_Process.py:150-152)
     blen = torch.full((nb,), 100, dtype=torch.int64, device=dev)
     blen[-1] = L - 100 * (nb - 1)
@@ -801,7 +840,7 @@ def run_c4(args, world, rank, dev, torch, dist, cpu):
     info = {"workload": f"configs[3]: {S} independent streams x {L} rows (Bernoulli r0~U(.01,.2) stepping "
                         f"by U(.05,.3)), DDM only, fresh DDM at the batch after each change"}
     rows_s = S * L / (avg_ms * 1e-3)
-    extra = {"changes_per_step": changes, "scan_kernel_ms": avg_ms, "rows_scanned_per_call": scanned,
+    extra = {"changes_per_step": changes, "scan_kernel_ms": avg_ms, "rows_scanned_per_call": scanned, "checks": checks,
              "rows_scanned_per_s": scanned / (avg_ms * 1e-3),
              "rows_note": "value counts every row of every stream (nominal); rows_scanned counts the rows the DDM "
                           "consumes (each batch up to its change), the same way on the CPU side"}

@@ -65,8 +65,11 @@ __device__ __forceinline__ T gget(gptr<const T> p) {
 
 // Cross-stream order by a sequence number in device memory (ddm_ctl_epoch.sync_flags):
 // the producer's data are released (agent scope) before the number is stored; a poll ends
-// when the number reaches v, or gives up after ~0.1 s and counts that in *timeouts.  One
-// thread each.
+// when the number reaches v, or gives up and counts that in timeouts[0].  The give-up is a
+// hang guard only: timeouts[1] (sync_flags[3]) is the join polls' limit in 10-ns ticks, 0 = 2 s (a
+// group of epochs lasts ~0.5-2 ms; the limit must also outlast serialised dispatch under a
+// profiler).  A give-up voids the phase and the runner redoes the run with event-ordered
+// fork / join (ddm_amd/devctl.py FlagTimeout).  One thread each.
 __device__ inline void flag_publish(uint32_t* flag, uint32_t v) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -74,9 +77,15 @@ __device__ inline void flag_publish(uint32_t* flag, uint32_t v) {
 
 __device__ inline void flag_poll(const uint32_t* flag, uint32_t v, uint32_t* timeouts) {
     const uint64_t t0 = wall_clock64();
+    // the override applies to the join polls only: their consumers read perm bytes, every
+    // one of which is a valid in-batch offset whenever it is read; the fork's consumers read
+    // job tables, so the fork wait (flags[0], timeouts - 2) keeps the 2-s guard
+    const uint32_t lim =
+        flag == timeouts - 2 ? 0u : __hip_atomic_load(timeouts + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t limit = lim ? (uint64_t)lim : 200000000ull;   // 2 s at 100 MHz
     while ((int32_t)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - v) < 0) {
         __builtin_amdgcn_s_sleep(1);
-        if (wall_clock64() - t0 > 10000000ull) {            // 0.1 s at 100 MHz
+        if (wall_clock64() - t0 > limit) {
             atomicAdd(timeouts, 1u);
             break;
         }

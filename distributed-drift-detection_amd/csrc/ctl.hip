@@ -64,8 +64,9 @@ constexpr int32_t kPermBlocks = 256;            // ddm_err_permute_dev blocks pe
 // pack; decoupled epochs poll it by a one-wave kernel before the permutation.  A fork +
 // join by one-wave kernels costs ~12 us against ~30 us with two events
 // (profiles/r04/gap_bench.log).  Every poll is enqueued after the store it waits for, so
-// even streams sharing one hardware queue cannot deadlock; a poll still gives up after
-// ~0.1 s and counts it in flags[2], which voids the phase (ddm_amd/devctl.py raises).
+// even streams sharing one hardware queue cannot deadlock; a poll still gives up (a hang
+// guard: after flags[3] ticks, 0 = 2 s) and counts it in flags[2], which voids the phase
+// (ddm_amd/devctl.py raises FlagTimeout and the runner redoes the run with events).
 __global__ __launch_bounds__(64) void k_flag_pub(uint32_t* flag, uint32_t v) {
     if (threadIdx.x == 0) ddm::flag_publish(flag, v);
 }

@@ -30,6 +30,7 @@ import pandas as pd
 import torch
 
 from . import dfit, kernels
+from .devctl import FlagTimeout
 from ._capi import DDM_STOP_FAILED, DdmEpoch, check, lib
 from .forest import upload_forests
 from .params import OUTPUT_COLUMNS, DDMSettings, infer_x_features
@@ -172,12 +173,14 @@ class RunStats:
     __slots__ = ("epochs", "refits", "predicted_rows", "refit_s", "gpu_s", "host_s", "predict_ms", "predict_bytes",
                  "scan_ms", "scan_rows", "shuffle_ms", "sklearn_refits", "refit_fit_s", "refit_readback_s",
                  "prep_s", "dfit_ms", "device_refits", "long_scans", "preshuffled", "device_epochs", "device_phases",
-                 "permute_rows", "device_rows", "predict_dev_ms", "predict_dev_launches", "device_predict_bytes")
+                 "permute_rows", "device_rows", "predict_dev_ms", "predict_dev_launches", "device_predict_bytes",
+                 "flag_recoveries")
 
     def __init__(self):
         self.epochs = self.refits = self.predicted_rows = self.predict_bytes = self.scan_rows = 0
         self.sklearn_refits = self.device_refits = self.long_scans = self.preshuffled = 0
         self.device_epochs = self.device_phases = self.permute_rows = self.device_rows = 0
+        self.flag_recoveries = 0       # runs redone with event-ordered fork / join (devctl.FlagTimeout)
         self.predict_dev_ms, self.predict_dev_launches, self.device_predict_bytes = 0.0, 0, 0
         self.refit_s = self.gpu_s = self.host_s = self.predict_ms = self.scan_ms = self.shuffle_ms = 0.0
         self.refit_fit_s = self.refit_readback_s = self.prep_s = self.dfit_ms = 0.0
@@ -758,10 +761,29 @@ class BatchRunner:
     def run(self, rngs):
         """Returns, per partition, int64 [n_batches-1, 2]: partition rows of (first warning,
         change) per batch 1.. (-1 = none).  Consumes each `rngs[p]` (an MTStream, advanced
-        in place) exactly as the reference consumes np.random in that partition's worker."""
-        s, st, pb = self.s, self.stats, self.s.per_batch
+        in place) exactly as the reference consumes np.random in that partition's worker.
+
+        A device phase whose cross-stream flag wait gave up (a hang guard, csrc/common.h
+        flag_poll) is void: the run is redone from the callers' RNG states with the fork /
+        join ordered by HIP events for the rest of the runner's life, so the results stay
+        exact (stats.flag_recoveries counts it)."""
         if len(rngs) != len(self.parts):
             raise ValueError("one MT19937 stream per partition")
+        snaps = [r.snapshot() for r in rngs]
+        try:
+            return self._run(rngs)
+        except FlagTimeout as e:
+            if self.devctl is None or not self.devctl.flags_ok:
+                raise
+            self._mark(f"flag timeout: {e}; run redone with event-ordered fork / join")
+            for r, snap in zip(rngs, snaps):
+                r.restore(snap)
+            self.devctl.flags_off()
+            self.stats.flag_recoveries += 1
+            return self._run(rngs)
+
+    def _run(self, rngs):
+        s, st, pb = self.s, self.stats, self.s.per_batch
         self._t_run = time.perf_counter()
         self._gen_rest = None
         self._forked = False

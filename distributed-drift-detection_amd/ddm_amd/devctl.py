@@ -51,6 +51,12 @@ CTL_GRAPH = os.environ.get("DDM_CTL_GRAPH", "0") not in ("", "0")
 CTL_FLAGS = os.environ.get("DDM_CTL_FLAGS", "1") not in ("", "0")
 
 
+class FlagTimeout(RuntimeError):
+    """A cross-stream flag wait of a device phase gave up (csrc/common.h flag_poll, a hang
+    guard): a consumer may have read data its producer had not finished, so the phase's
+    results are void.  BatchRunner.run redoes the run with event-ordered fork / join."""
+
+
 class PredictTimer:
     """The span of every device-epoch predict launch of the timed runs on the 100 MHz device
     clock (ddm_ctl.predict_clock): the kernel stamps its workgroups' starts and ends into 8
@@ -123,6 +129,7 @@ class DeviceController:
         self.sync_flags = torch.zeros(4, dtype=torch.int32, device=dev)
         self.sync_seq = (ctypes.c_uint32 * 3)()
         self.sync_h = torch.zeros(4, dtype=torch.int32, pin_memory=True)
+        self.flags_ok = True         # off for the runner's life after a FlagTimeout
         self._E = None
 
     # ---------------------------------------------------------------- eligibility
@@ -303,7 +310,7 @@ class DeviceController:
         # HIP cannot time events that a graph records (hipEventElapsedTime: invalid resource
         # handle), so timed predicts keep the launched form
         use_graph = CTL_GRAPH and pt is None and not (timing or logging)
-        flags = CTL_FLAGS and not use_graph
+        flags = CTL_FLAGS and self.flags_ok and not use_graph
         E.sync_flags = self.sync_flags.data_ptr() if flags else None
         E.sync_seq = ctypes.addressof(self.sync_seq) if flags else None
         if use_graph:
@@ -392,6 +399,22 @@ class DeviceController:
             self.graphs[key] = g
         return g
 
+    def set_flag_limit(self, ticks):
+        """The join polls' give-up limit in 10-ns device-clock ticks (sync_flags[3]; 0: the
+        default 2 s, which the fork wait always keeps).  Tests force a give-up with a tiny
+        limit."""
+        self.sync_flags[3] = int(ticks)
+        torch.cuda.synchronize(self.r.device)
+
+    def flags_off(self):
+        """After a FlagTimeout: fork / join by HIP events from now on (the numbers and the
+        give-up count start over should flags be turned back on)."""
+        self.flags_ok = False
+        self.sync_flags[:3].zero_()
+        for k in range(3):
+            self.sync_seq[k] = 0
+        torch.cuda.synchronize(self.r.device)
+
     def close(self):
         for g in self.graphs.values():
             lib.ddm_ctl_graph_destroy(g)
@@ -459,9 +482,8 @@ class DeviceController:
         r.stream.synchronize()
         r._mark("records copied")
         if int(self.sync_h[2]):
-            raise RuntimeError(f"{int(self.sync_h[2])} cross-stream flag waits of the device epochs gave up "
-                               "(ddm_ctl_epoch.sync_flags): the epochs' results are void (DDM_CTL_FLAGS=0 "
-                               "orders the streams by events)")
+            raise FlagTimeout(f"{int(self.sync_h[2])} cross-stream flag waits of the device epochs gave up "
+                              "(ddm_ctl_epoch.sync_flags): the phase's results are void")
         rec = self.rec
         epochs = int(rec["epochs"].max()) if len(rec) else 0
         # every partition's event log in one read-back

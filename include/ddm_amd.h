@@ -677,7 +677,10 @@ typedef struct ddm_ctl_epoch {
                                                       join_ev) or device words [4], zeroed once
                                                       for the streams' life: [0] / [1] the last
                                                       fork / join number published, [2] waits
-                                                      that gave up (nonzero voids the results) */
+                                                      that gave up (nonzero voids the results),
+                                                      [3] the join polls' give-up limit in
+                                                      10-ns ticks (0: 2 s, as the fork wait's
+                                                      always; a hang guard)                    */
     uint32_t* sync_seq;                            /* ABI 21: host words [3], the fork / join
                                                       numbers enqueued so far and the last
                                                       join the epoch stream polled (advanced

@@ -80,9 +80,15 @@ def test_decoupled_epochs_equal_host_epochs(case, monkeypatch):
     assert st.refits == st_h.refits
 
 
-def test_device_epochs_vs_oracle():
-    """Partitions with many refits, run with device epochs, == the oracle on each."""
+@pytest.mark.parametrize("flags,device_start", [(True, True), (False, True), (True, False), (False, False)])
+def test_device_epochs_vs_oracle(flags, device_start, monkeypatch):
+    """Partitions with many refits, run with device epochs, == the oracle on each: fork / join
+    by device flags or by HIP events (DDM_CTL_FLAGS=0), the first fit on the device or a
+    host-planned first epoch (DDM_DEVICE_START=0)."""
+    from ddm_amd import controller, devctl
     from oracle.controller import run_partition
+    monkeypatch.setattr(devctl, "CTL_FLAGS", flags)
+    monkeypatch.setattr(controller, "DEVICE_START", device_start)
     parts = _parts((12_000, 9_050, 15_100), 27, 0, 11, flip=0.005, jitter=True)
     seeds = [7, 8, 9]
     out, rng, st = _run(parts, True, seeds, win=7, maxwin=64)
@@ -138,4 +144,37 @@ def test_graph_epochs_equal_host_epochs(case, decouple, timed, monkeypatch):
     if timed:
         assert st.predict_dev_launches > 0 and st.predict_dev_ms > 0
         runner.set_predict_timing(False)
+    runner.close()
+
+
+@pytest.mark.parametrize("decouple", [False, True])
+def test_flag_timeout_voids_and_redoes_the_run(decouple, monkeypatch):
+    """A cross-stream flag wait that gives up (csrc/common.h flag_poll, forced here by a
+    1-tick limit in sync_flags[3]) voids the device phase: the runner redoes the run from
+    the callers' RNG states with event-ordered fork / join, and the events, RNG positions
+    and refits equal host epochs (DDM_Process.py:189-210)."""
+    from ddm_amd import devctl
+    from ddm_amd.controller import BatchRunner
+    from ddm_amd.params import DDMSettings
+    from ddm_amd.rng import MTStream
+    if decouple:
+        monkeypatch.setattr(devctl, "DECOUPLE_ROWS", 0)
+    parts = _parts((30_000, 30_000), 27, 0, 7, flip=0.01, jitter=True)
+    seeds = [400, 401]
+    host_out, host_rng, st_h = _run(parts, False, seeds)
+    runner = BatchRunner(parts, DDMSettings(), device_ctl=True)
+    runner.devctl.set_flag_limit(1)
+    rngs = [MTStream.from_seed(s) for s in seeds]
+    out = runner.run(rngs)
+    st = runner.stats
+    assert st.flag_recoveries == 1 and not runner.devctl.flags_ok
+    for k in range(len(parts)):
+        assert np.array_equal(out[k], host_out[k]), k
+        assert np.array_equal(rngs[k].key, host_rng[k][0]) and rngs[k].pos.value == host_rng[k][1], k
+    # the runner stays usable (events from now on), and a second run gives the same
+    rngs = [MTStream.from_seed(s) for s in seeds]
+    out = runner.run(rngs)
+    for k in range(len(parts)):
+        assert np.array_equal(out[k], host_out[k]), k
+    assert runner.stats.flag_recoveries == 1
     runner.close()

@@ -154,3 +154,46 @@ def test_scan_batches_prefix_table_exhaustive(oracle_lib, per_batch, L):
     oev, _, ost, _ = oracle_scan_c(oracle_lib, err, off, per_batch=per_batch, mode=1)
     assert np.array_equal(ev, oev)
     np.testing.assert_array_equal(_state_matrix(st), ost)
+
+
+def test_scan_batches_c4_full_size():
+    """configs[3] at FULL size, built exactly as `bench.py --workload c4` builds it (1M streams
+    x 4096 rows, Bernoulli streams from the bench's seed): every event, event count and end
+    state of ddm_scan_batches against the C oracle over all 1M streams (oracle/scan.py,
+    DDM_Process.py:135-159 with the reset of :207-210) and against ddm_scan_streams in mode 1.
+    Only at this size do the chain kernel's carried streams outnumber its waves (grid
+    stride) and the classify pass run ~156 fills per wave."""
+    import bench
+    from ddm_amd import kernels
+    from oracle.scan import scan_equal_streams
+    from test_gpu_scan import _state_matrix
+    S, L, pb = 1_000_000, 4096, 100
+    nb = -(-L // pb)
+    dev = torch.device("cuda", 0)
+    err = torch.empty(S * L + 16, dtype=torch.uint8, device=dev)
+    kernels.synth_bernoulli_streams(err, S, L, bench.SEED)
+    ev = torch.full((S * nb, 2), 7, dtype=torch.int32, device=dev)
+    scratch = torch.empty(kernels.scan_batches_scratch_size(S, L), dtype=torch.uint8, device=dev)
+    st = torch.from_numpy(kernels.fresh_states(S).view(np.uint8)).to(dev)
+    nev = torch.empty(S, dtype=torch.int64, device=dev)
+    kernels.scan_batches(err, S, L, kernels.params_struct(), st, ev, scratch, nev=nev)
+    # the oracle-pinned one-lane kernel on the same device bytes
+    off = torch.arange(S + 1, dtype=torch.int64, device=dev) * L
+    ref_ev = torch.full((S * nb, 2), 7, dtype=torch.int32, device=dev)
+    ref_st = torch.from_numpy(kernels.fresh_states(S).view(np.uint8)).to(dev)
+    ref_nev = torch.empty(S, dtype=torch.int64, device=dev)
+    kernels.scan_streams(err, off, kernels.params_struct(), ref_st, torch.arange(S, dtype=torch.int64, device=dev) * nb,
+                         S * nb, ref_ev, nev=ref_nev, mode=1)
+    torch.cuda.synchronize()
+    assert torch.equal(ev, ref_ev)
+    assert torch.equal(nev, ref_nev)
+    assert torch.equal(st, ref_st)
+    evh = ev.cpu().numpy()
+    sth = _state_matrix(st.cpu().numpy().view(kernels.STATE_DTYPE))
+    del ref_ev, ref_st, scratch
+    oev, ost = scan_equal_streams(err[:S * L].cpu().numpy(), S, L, per_batch=pb, mode=1, threads=16)
+    assert np.array_equal(evh, oev)
+    np.testing.assert_array_equal(sth, ost)
+    o_nev = ((oev[:, 0] >= 0) | (oev[:, 1] >= 0)).reshape(S, nb).sum(axis=1)
+    assert np.array_equal(nev.cpu().numpy(), o_nev)
+    assert (oev[:, 1] >= 0).mean() > 0.9
