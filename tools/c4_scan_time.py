@@ -45,6 +45,7 @@ def child(a):
         torch.cuda.synchronize()
         if r >= 2:
             times.append(e0.elapsed_time(e1))
+    prof = scratch[64:128].cpu().numpy().view(np.uint64)
     h = hashlib.sha1()
     h.update(ev.cpu().numpy().tobytes())
     h.update(st.cpu().numpy().view(kernels.STATE_DTYPE)[:S].tobytes())
@@ -52,6 +53,12 @@ def child(a):
     alg = S * L * 1.08
     out = {"label": a.label, "median_ms": med, "min_ms": min(times), "frac_8TBs": alg / (med * 1e-3) / 8e12,
            "sha1_ok": h.hexdigest() == EXPECT_SHA1 if S == 1_000_000 else None, "sha1": h.hexdigest()}
+    if prof.any():      # a -DDDM_OP_PROFILE build: one-pass phase cycles summed over the waves (last call)
+        names = ["load", "decide", "drain", "walk", "write", "tail", "-", "chunks"]
+        tot = float(prof[:6].sum())
+        out["phases"] = {n: round(float(v) / tot, 4) for n, v in zip(names[:6], prof[:6])}
+        out["chunks"] = int(prof[7])
+        out["wave_cycles_per_chunk"] = tot / max(1, int(prof[7]))
     print(json.dumps(out), flush=True)
 
 
