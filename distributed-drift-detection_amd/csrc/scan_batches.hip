@@ -1102,632 +1102,6 @@ __global__ __launch_bounds__(kChainThreads) void k_scan_batches_chain(
     }
 }
 
-// 5. The one-pass form (streams of at most kOpMaxRows rows, configs[3]): every wave claims
-// chunks of G whole streams from a counter and resolves them alone, so nothing but the
-// events and the streams' states is written (the multi-kernel form above also writes flag
-// bytes, end states and level-1 records, and its fix-up kernels wait for the whole stream
-// pass).  A wave's iteration k:
-//   a. chunk k's bytes by coalesced 16-byte loads, folded into the wave's LDS bit image;
-//   b. every batch of chunk k from a fresh detector, one lane per batch (trivial: the change
-//      is the first error after two zeros; else the prefix table), recorded in chunk k's
-//      record buffer (two buffers, k & 1); the rest into the wave's exact queue, which idle
-//      lanes step two rows at a time between rounds -- oldest first, so chunk k - 1's
-//      leftovers run beside chunk k's new entries and the lanes stay full;
-//   c. chunk k - 1: its last exact rows, then its streams, one lane each, from their
-//      carried-in states: a fresh carry takes the speculation (runs of changes by bit
-//      masks), a trivial carry the batch's first error row, anything else -- rare: 0.24 %
-//      of C4's batches -- is a wave task, the batch's rows (re-read from memory) through
-//      wave_tile from the lane's detector; then its events (perm_map labels) and states.
-// Waves that meet a long carried run simply claim fewer chunks.
-constexpr int kOpThreads = 256;
-constexpr int kOpWaves = kOpThreads / 64;
-constexpr int kOpImgPieces = 2050;                       // 16-row pieces of a chunk (+ alignment)
-constexpr int kOpMaxRows = (kOpImgPieces - 2) * 16;      // rows of a chunk: 32,768
-constexpr int kOpImgWords = kOpImgPieces * 16 / 64 + 3;  // the image in u64 words (+ 128-bit cut slack)
-constexpr int kOpRecCap = 384;                           // batches of a chunk
-constexpr int kOpMaskWords = kOpRecCap / 64;
-constexpr int kOpQ = 64;                                 // the exact queue (ring)
-constexpr int kOpSlots = 16;                             // end states of unchanged exact batches per chunk
-constexpr int kOpLoads = 8;                              // 16-byte loads in flight per lane
-
-// Batch record (u32): bits 0-7 first warning row + 1, 8-15 change row + 1 (0: none), 16 the
-// exact rows are pending, 17 the fresh detector ends TRIVIAL (no error after two zeros), 18
-// its end state is in slot bits 24-31, 19 that state's warning flag, 20 the state was not
-// kept (no free slot: the walk reruns the batch).  ferr: the batch's first error row (255:
-// none), what a trivial carried detector makes of it.  chg: bit i = batch i changed.
-constexpr uint32_t kRecPending = 1u << 16, kRecTrivEnd = 1u << 17, kRecSlot = 1u << 18, kRecWarn = 1u << 19,
-                   kRecLost = 1u << 20;
-
-struct OpChunk {
-    uint32_t rec[kOpRecCap];
-    uint64_t chg[kOpMaskWords];
-    double slot[kOpSlots][5];    // p, s, p_min, s_min, ps_min
-    uint8_t ferr[kOpRecCap];
-};
-struct OpWave {
-    uint64_t img[kOpImgWords];
-    OpChunk ch[2];
-    uint64_t qm0[kOpQ], qm1[kOpQ];
-    uint32_t qhdr[kOpQ];         // batch (bits 0-14) | chunk parity << 15 | first warning row + 1 << 16 | first row << 24
-    double tile[kTileScratch];
-};
-
-// the 128 row bits at bit b of the image, masked to blen rows
-__device__ __forceinline__ void op_cut(const uint64_t* img, int b, int blen, uint64_t& m0, uint64_t& m1) {
-    const int wo = b >> 6, sh = b & 63;
-    const uint64_t x0 = img[wo], x1 = img[wo + 1], x2 = img[wo + 2];
-    m0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
-    m1 = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
-    if (blen < 64) {
-        m0 &= (1ull << blen) - 1;
-        m1 = 0;
-    } else if (blen < 128) {
-        m1 &= (1ull << (blen - 64)) - 1;
-    }
-}
-
-// the 128 row bits of rows [row, row + blen) straight from memory, uniform over the wave
-// (lanes 0-8 load one 16-byte piece each)
-__device__ __forceinline__ void op_mask_mem(const uint8_t* __restrict__ err, int64_t row, int blen, uint64_t& m0,
-                                            uint64_t& m1) {
-    const int lane = threadIdx.x & 63;
-    const int64_t a = row & ~(int64_t)15;
-    const int nch = (int)((row + blen - a + 15) >> 4);
-    uint32_t h = 0;
-    if (lane < nch) {
-        uint4 v = *reinterpret_cast<const uint4*>(err + a + 16 * lane);
-        v.x = nzbytes(v.x);
-        v.y = nzbytes(v.y);
-        v.z = nzbytes(v.z);
-        v.w = nzbytes(v.w);
-        h = fold16(v);
-    }
-    uint64_t w[3] = {0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        const uint64_t hk = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h, k);
-        w[k >> 2] |= hk << (16 * (k & 3));
-    }
-    const int sh = (int)(row - a);
-    m0 = sh ? (w[0] >> sh) | (w[1] << (64 - sh)) : w[0];
-    m1 = sh ? (w[1] >> sh) | (w[2] << (64 - sh)) : w[1];
-    if (blen < 64) {
-        m0 &= (1ull << blen) - 1;
-        m1 = 0;
-    } else if (blen < 128) {
-        m1 &= (1ull << (blen - 64)) - 1;
-    }
-}
-
-// bits [i, i + 64) of a bit array (zeros past its last word)
-__device__ __forceinline__ uint64_t bits_at(const uint64_t* a, int nwords, int i) {
-    const int w = i >> 6, sh = i & 63;
-    const uint64_t lo = w < nwords ? a[w] : 0ull;
-    const uint64_t hi = w + 1 < nwords ? a[w + 1] : 0ull;
-    return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
-}
-
-// Phase clocks of a profile build (-DDDM_OP_PROFILE, tools/build_variant.sh): shader cycles
-// of every wave per phase (load, decide, finish the last chunk's exact rows, walk, write)
-// and the chunks, summed into the scratch's bytes 64-127 (u64 [8]; the memset zeroes them).
-#ifdef DDM_OP_PROFILE
-#define OP_T(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); ph[k] += t_ - tl; tl = t_; } while (0)
-#else
-#define OP_T(k) do { } while (0)
-#endif
-
-template <bool kPmap>
-__global__ __launch_bounds__(kOpThreads) void k_scan_batches_onepass(
-    const uint8_t* __restrict__ err, int64_t n_streams, int32_t L, int32_t nb, ddm_params P,
-    ddm_state* __restrict__ state_io, int2* __restrict__ ev, int64_t* __restrict__ nev_out,
-    const uint8_t* __restrict__ pmap, const uint16_t* __restrict__ ptab, const double4* __restrict__ pst,
-    uint32_t* __restrict__ ctr, int32_t G, uint32_t magic, int32_t msh, bool use_pre, int32_t steps,
-    int32_t pop_min, int32_t step_min, int32_t straggle) {
-    __shared__ OpWave W_[kOpWaves];
-    __shared__ double rcp[kBatchRcp];
-    for (int k = threadIdx.x; k < kBatchRcp; k += kOpThreads) rcp[k] = 1.0 / (double)(k > 0 ? k : 1);
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    OpWave& W = W_[wv];
-    uint16_t* const img16 = reinterpret_cast<uint16_t*>(W.img);
-    const uint64_t below = (1ull << lane) - 1;
-    const int pb = (int)P.per_batch;
-    const int min_inst = P.min_num_instances;
-    const double wl = P.warning_level, cl = P.out_control_level;
-    const bool shortcuts = min_inst == 3;
-    const int64_t n_chunks = (n_streams + G - 1) / G;
-#ifdef DDM_OP_PROFILE
-    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t tl = __builtin_amdgcn_s_memtime();
-#endif
-    // the exact queue and its lanes (wave-uniform ring state; pending batches per chunk)
-    uint32_t q_head = 0, q_cnt = 0;
-    uint32_t pend0 = 0, pend1 = 0, nslot0 = 0, nslot1 = 0;
-    bool busy = false;
-    SmallDet d;
-    small_fresh(d);
-    int ei = 0, eblen = 0, ewp = -1, eidx = 0, epar = 0;
-    uint64_t em0 = 0, em1 = 0;
-    const auto finish = [&](bool fin, bool chg, int r) {
-        // finished exact batches: records, change bits, end states of unchanged ones
-        const uint64_t um0 = __ballot(fin && !chg && epar == 0), um1 = __ballot(fin && !chg && epar == 1);
-        const uint64_t f0 = __ballot(fin && epar == 0), f1 = __ballot(fin && epar == 1);
-        if (fin) {
-            OpChunk& C = W.ch[epar];
-            uint32_t rc = (uint32_t)(ewp + 1) | ((uint32_t)(chg ? ei : 0) << 8);
-            if (chg) {
-                __hip_atomic_fetch_or(&C.chg[eidx >> 6], 1ull << (eidx & 63), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else {
-                if (r == 1) rc |= kRecWarn;
-                const uint32_t sl = (epar ? nslot1 : nslot0) + (uint32_t)__popcll((epar ? um1 : um0) & below);
-                if (sl < (uint32_t)kOpSlots) {
-                    double* e = C.slot[sl];
-                    e[0] = d.p;
-                    e[1] = d.s;
-                    e[2] = d.pmin;
-                    e[3] = d.smin;
-                    e[4] = d.psmin;
-                    rc |= kRecSlot | (sl << 24);
-                } else {
-                    rc |= kRecLost;
-                }
-            }
-            C.rec[eidx] = rc;
-            busy = false;
-        }
-        nslot0 += (uint32_t)__popcll(um0);
-        nslot1 += (uint32_t)__popcll(um1);
-        pend0 -= (uint32_t)__popcll(f0);
-        pend1 -= (uint32_t)__popcll(f1);
-    };
-    const auto step = [&]() {
-        // two exact rows of this lane's batch (p and s of row i + 1 depend on p_i alone)
-        bool fin = false, chg = false;
-        int r = 0;
-        if (busy) {
-            const bool two = ei + 1 < eblen;
-            const int n0 = d.n;
-            const double nd0 = (double)n0, r0 = rcp[n0], nd1 = (double)(n0 + 1), r1 = rcp[n0 + 1];
-            const double p0 = d.p + div_rn((double)mask_bit(em0, em1, ei) - d.p, nd0, r0);
-            const double p1 = p0 + div_rn((double)(two ? mask_bit(em0, em1, ei + 1) : 0) - p0, nd1, r1);
-            const double sa = sqrt_q(div_rn(p0 * (1.0 - p0), nd0, r0));
-            const double sb = sqrt_q(div_rn(p1 * (1.0 - p1), nd1, r1));
-            r = small_test(d, p0, sa, min_inst, wl, cl);
-            if (r == 1 && ewp < 0) ewp = ei;
-            ++ei;
-            if (r != 2 && two) {
-                r = small_test(d, p1, sb, min_inst, wl, cl);
-                if (r == 1 && ewp < 0) ewp = ei;
-                ++ei;
-            }
-            chg = r == 2;
-            fin = chg || ei >= eblen;
-        }
-        finish(fin, chg, r);
-    };
-    // idle lanes take queued batches (in lane order, oldest first)
-    const auto pop = [&](bool force) {
-        const uint64_t idle_m = __ballot(!busy);
-        const int nidle = __popcll(idle_m);
-        if (q_cnt > 0 && (force || nidle >= pop_min || nidle == 64 || q_cnt == (uint32_t)kOpQ)) {
-            const uint32_t take = min((uint32_t)nidle, q_cnt);
-            const uint32_t rank = (uint32_t)__popcll(idle_m & below);
-            bool got = false;
-            uint32_t hdr = 0;
-            if (!busy && rank < take) {
-                const uint32_t sl = (q_head + rank) & (kOpQ - 1);
-                em0 = W.qm0[sl];
-                em1 = W.qm1[sl];
-                hdr = W.qhdr[sl];
-                got = true;
-            }
-            q_head = (q_head + take) & (kOpQ - 1);
-            q_cnt -= take;
-            // the detector after the prefix rows (a table entry) or a fresh one
-            const double4 t = pst[got ? (uint32_t)(em0 & (uint64_t)(kPreN - 1)) : 0u];
-            if (got) {
-                busy = true;
-                eidx = (int)(hdr & 0x7fffu);
-                epar = (int)((hdr >> 15) & 1u);
-                ewp = (int)((hdr >> 16) & 0xffu) - 1;
-                ei = (int)(hdr >> 24);
-                d.p = ei ? t.x : 1.0;
-                d.s = 0.0;
-                d.pmin = ei ? t.y : __builtin_huge_val();
-                d.smin = ei ? t.z : __builtin_huge_val();
-                d.psmin = ei ? t.w : __builtin_huge_val();
-                d.n = ei + 1;
-                const int sl2 = (int)(__umulhi((uint32_t)eidx, magic) >> msh);
-                const int j2 = eidx - sl2 * nb;
-                eblen = min(pb, L - j2 * pb);
-            }
-        }
-    };
-    int64_t prev = -1;                                     // the chunk still to walk
-    for (int64_t k = 0;; ++k) {
-        uint32_t cid = 0;
-        if (lane == 0) cid = atomicAdd(ctr + 3, 1u);
-        const int64_t c = (int64_t)__builtin_amdgcn_readfirstlane(cid);
-        const bool have = c < n_chunks;
-        const int par = (int)(k & 1);
-        if (have) {
-#ifdef DDM_OP_PROFILE
-            ph[7] += 1;
-#endif
-            const int64_t s0 = c * G;
-            const int Gc = (int)min((int64_t)G, n_streams - s0);
-            const int nbc = Gc * nb;
-            const int64_t row0 = s0 * (int64_t)L;
-            const int64_t org = row0 & ~(int64_t)15;
-            const int off0 = (int)(row0 - org);
-            const int np = (int)((row0 + (int64_t)Gc * L - org + 15) >> 4);
-            // a. the chunk's bytes -> the bit image (kOpLoads loads of 1 KiB in flight per wave)
-            for (int q0 = 0; q0 < np; q0 += kOpLoads * 64) {
-                u32x4 v[kOpLoads];
-#pragma unroll
-                for (int kk = 0; kk < kOpLoads; ++kk)
-                    v[kk] = __builtin_nontemporal_load(
-                        reinterpret_cast<const u32x4*>(err + org + 16 * (int64_t)min(q0 + kk * 64 + lane, np - 1)));
-                uint32_t odd = 0;
-#pragma unroll
-                for (int kk = 0; kk < kOpLoads; ++kk) odd |= v[kk].x | v[kk].y | v[kk].z | v[kk].w;
-                if (__ballot((odd & 0xfefefefeu) != 0u)) {      // bytes other than 0/1
-#pragma unroll
-                    for (int kk = 0; kk < kOpLoads; ++kk) {
-                        v[kk].x = nzbytes(v[kk].x);
-                        v[kk].y = nzbytes(v[kk].y);
-                        v[kk].z = nzbytes(v[kk].z);
-                        v[kk].w = nzbytes(v[kk].w);
-                    }
-                }
-#pragma unroll
-                for (int kk = 0; kk < kOpLoads; ++kk)
-                    img16[min(q0 + kk * 64 + lane, np - 1)] =
-                        (uint16_t)fold16(make_uint4(v[kk].x, v[kk].y, v[kk].z, v[kk].w));
-            }
-            wave_sync_lds();
-            OP_T(0);
-            // b. every batch from a fresh detector; exact rows by idle lanes between rounds
-            OpChunk& C = W.ch[par];
-            if (par) nslot1 = 0;
-            else nslot0 = 0;
-            for (int r0 = 0; r0 < nbc; r0 += 64) {
-                const int i = r0 + lane;
-                const bool valid = i < nbc;
-                const int ii = valid ? i : nbc - 1;
-                const int sl = (int)(__umulhi((uint32_t)ii, magic) >> msh);
-                const int j = ii - sl * nb;
-                const int blen = min(pb, L - j * pb);
-                uint64_t m0, m1;
-                op_cut(W.img, off0 + sl * L + j * pb, blen, m0, m1);
-                const bool triv = shortcuts && blen >= 2 && (m0 & 3ull) == 0;
-                const bool pre = valid && !triv && use_pre && blen >= kPre;
-                const uint32_t inf = ptab[pre ? (uint32_t)(m0 & (uint64_t)(kPreN - 1)) : 0u];
-                bool exact = false, changed = false;
-                uint32_t hdr = (uint32_t)ii | ((uint32_t)par << 15);
-                if (valid) {
-                    uint32_t rc = 0;
-                    if (triv) {
-                        const int t = mask_next(m0, m1, 2);
-                        changed = t < blen;
-                        rc = changed ? ((uint32_t)(t + 1) << 8) : kRecTrivEnd;
-                    } else if (pre) {
-                        const int cp = (int)(inf >> 5) - 1;
-                        const int wp = (int)(inf & 31u) - 1;
-                        if (cp >= 0) {
-                            changed = true;
-                            rc = (uint32_t)(wp + 1) | ((uint32_t)(cp + 1) << 8);
-                        } else {
-                            exact = true;
-                            if (blen > kPre) hdr |= ((uint32_t)(wp + 1) << 16) | ((uint32_t)kPre << 24);
-                        }
-                    } else {
-                        exact = true;
-                    }
-                    if (exact) rc = kRecPending;
-                    C.rec[i] = rc;
-                    const int fe = mask_next(m0, m1, 0);
-                    C.ferr[i] = (uint8_t)(fe < blen ? fe : 255);
-                }
-                const uint64_t cm = __ballot(changed);
-                if (lane == 0) C.chg[r0 >> 6] = cm;
-                // into the exact queue; a full queue is stepped until it has room
-                uint64_t xm = __ballot(exact);
-                if (par) pend1 += (uint32_t)__popcll(xm);
-                else pend0 += (uint32_t)__popcll(xm);
-                while (xm) {
-                    const uint32_t room = (uint32_t)kOpQ - q_cnt;
-                    const uint32_t rank = (uint32_t)__popcll(xm & below);
-                    if (exact && rank < room) {
-                        const uint32_t sl2 = (q_head + q_cnt + rank) & (kOpQ - 1);
-                        W.qm0[sl2] = m0;
-                        W.qm1[sl2] = m1;
-                        W.qhdr[sl2] = hdr;
-                        exact = false;
-                    }
-                    q_cnt += min((uint32_t)__popcll(xm), room);
-                    xm = __ballot(exact);
-                    if (xm) {                                   // full: make room
-                        wave_sync_lds();
-                        pop(false);
-                        step();
-                    }
-                }
-                wave_sync_lds();
-                // steps only while enough lanes are busy (a step costs the same for 2 lanes as
-                // for 64); what is left is stepped when its chunk is walked
-                for (int kk = 0; kk < steps; ++kk) {
-                    pop(false);
-                    if (__popcll(__ballot(busy)) < step_min) break;
-                    step();
-                }
-            }
-            OP_T(1);
-        }
-        if (prev >= 0) {
-            // c. chunk prev: its last exact rows (the queue's oldest entries), then its streams
-            const int pp = par ^ 1;
-            for (;;) {
-                const uint32_t pend = pp ? pend1 : pend0;
-                if (pend == 0) break;
-                wave_sync_lds();
-                pop(true);
-                const uint64_t bm = __ballot(busy), bp = __ballot(busy && epar == pp);
-                if ((uint32_t)__popcll(bp) != pend || __popcll(bm) > straggle) {
-                    step();
-                    continue;
-                }
-                // the last few batches of the chunk: the rest of each one's rows by the whole wave
-                uint64_t tm = bp;
-                while (tm) {
-                    const int t = __builtin_ctzll(tm);
-                    tm &= tm - 1;
-                    Det cd;
-                    cd.p = readlane_d(d.p, t);
-                    cd.s = readlane_d(d.s, t);
-                    cd.pmin = readlane_d(d.pmin, t);
-                    cd.smin = readlane_d(d.smin, t);
-                    cd.psmin = readlane_d(d.psmin, t);
-                    cd.n = __builtin_amdgcn_readlane(d.n, t);
-                    cd.chg = 0;
-                    cd.warn = 0;
-                    const int ti = __builtin_amdgcn_readlane(ei, t), tb = __builtin_amdgcn_readlane(eblen, t);
-                    const uint64_t a0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(em0 >> 32), t) << 32) |
-                                        (uint32_t)__builtin_amdgcn_readlane((int)em0, t);
-                    const uint64_t a1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(em1 >> 32), t) << 32) |
-                                        (uint32_t)__builtin_amdgcn_readlane((int)em1, t);
-                    int ci = ti, cw = -1, cp = -1;
-                    while (ci < tb) {
-                        const int cnt = min(64, tb - ci);
-                        const uint64_t m = ci < 64 ? m0_shift(a0, a1, ci) : (a1 >> (ci - 64));
-                        const TileOut to = wave_tile(cd, m, cnt, min_inst, wl, cl, W.tile);
-                        const uint64_t upto = to.last >= 63 ? ~0ull : ((1ull << (to.last + 1)) - 1);
-                        const uint64_t wb = to.warn & upto;
-                        if (cw < 0 && wb) cw = ci + __builtin_ctzll(wb);
-                        if (to.kc >= 0) {
-                            cp = ci + to.kc;
-                            break;
-                        }
-                        ci += cnt;
-                    }
-                    const bool me = lane == t;
-                    if (me) {
-                        d.p = cd.p;
-                        d.s = cd.s;
-                        d.pmin = cd.pmin;
-                        d.smin = cd.smin;
-                        d.psmin = cd.psmin;
-                        d.n = (int)cd.n;
-                        if (ewp < 0) ewp = cw;
-                        ei = cp >= 0 ? cp + 1 : tb;
-                    }
-                    finish(me, cp >= 0, cd.warn ? 1 : 0);
-                }
-            }
-            wave_sync_lds();
-            OP_T(2);
-            OpChunk& C = W.ch[pp];
-            const int64_t s0 = prev * G;
-            const int Gc = (int)min((int64_t)G, n_streams - s0);
-            const int nbc = Gc * nb;
-            const int nw = (nbc + 63) >> 6;
-            const int64_t row0 = s0 * (int64_t)L;
-            const int64_t sid = s0 + lane;
-            const bool walker = lane < Gc;
-            Det dw;
-            if (walker) load_det(dw, state_io[sid]);
-            else det_reset(dw);
-            int jw = 0;
-            int64_t nev = 0;
-            bool active = walker;
-            for (;;) {
-                int task = 0;                               // 1: carried rows, 2: rerun from fresh
-                while (active) {
-                    if (jw >= nb) {
-                        active = false;
-                        break;
-                    }
-                    const int bi = lane * nb + jw;
-                    const int blen = min(pb, L - jw * pb);
-                    if (det_fresh(dw)) {
-                        // a run of batches whose speculative change stands
-                        const uint64_t run_m = bits_at(C.chg, nw, bi);
-                        const int run = min(nb - jw, run_m == ~0ull ? 64 : __builtin_ctzll(~run_m));
-                        if (run > 0) {
-                            nev += run;
-                            det_reset(dw);
-                            jw += run;
-                            continue;
-                        }
-                        const uint32_t rc = C.rec[bi];
-                        nev += (rc & 0xffu) ? 1 : 0;
-                        if (rc & kRecTrivEnd) {
-                            dw.p = dw.s = dw.pmin = dw.smin = dw.psmin = 0.0;
-                            dw.n = 1 + blen;
-                            dw.chg = dw.warn = 0;
-                            ++jw;
-                            continue;
-                        }
-                        if (rc & kRecSlot) {
-                            const double* e = C.slot[rc >> 24];
-                            dw.p = e[0];
-                            dw.s = e[1];
-                            dw.pmin = e[2];
-                            dw.smin = e[3];
-                            dw.psmin = e[4];
-                            dw.n = 1 + blen;
-                            dw.chg = 0;
-                            dw.warn = (rc & kRecWarn) ? 1 : 0;
-                            ++jw;
-                            continue;
-                        }
-                        nev -= (rc & 0xffu) ? 1 : 0;        // counted again after the rerun
-                        task = 2;
-                        break;
-                    }
-                    if (shortcuts && det_trivial(dw)) {
-                        // a trivial carried detector: the first error is the change, zeros move n
-                        const int t = C.ferr[bi];
-                        if (t < blen) {
-                            C.rec[bi] = (uint32_t)(t + 1) << 8;
-                            ++nev;
-                            det_reset(dw);
-                        } else {
-                            C.rec[bi] = 0u;
-                            dw.n += blen;
-                            dw.warn = 0;
-                        }
-                        ++jw;
-                        continue;
-                    }
-                    task = 1;
-                    break;
-                }
-                uint64_t tm = __ballot(task != 0);
-                if (!tm) break;
-                while (tm) {
-                    const int t = __builtin_ctzll(tm);
-                    tm &= tm - 1;
-                    // the task's detector and batch, uniform over the wave
-                    const int tj = __builtin_amdgcn_readlane(jw, t);
-                    const int tk = __builtin_amdgcn_readlane(task, t);
-                    Det cd;
-                    if (tk == 2) {
-                        det_reset(cd);
-                    } else {
-                        cd.p = readlane_d(dw.p, t);
-                        cd.s = readlane_d(dw.s, t);
-                        cd.pmin = readlane_d(dw.pmin, t);
-                        cd.smin = readlane_d(dw.smin, t);
-                        cd.psmin = readlane_d(dw.psmin, t);
-                        const uint32_t nlo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)dw.n, t);
-                        const uint32_t nhi = (uint32_t)__builtin_amdgcn_readlane((int)(dw.n >> 32), t);
-                        cd.n = (int64_t)(((uint64_t)nhi << 32) | nlo);
-                        cd.chg = 0;
-                        cd.warn = __builtin_amdgcn_readlane(dw.warn, t);
-                    }
-                    const int blen = min(pb, L - tj * pb);
-                    uint64_t a0, a1;
-                    op_mask_mem(err, row0 + (int64_t)t * L + (int64_t)tj * pb, blen, a0, a1);
-                    int ci = 0, cw = -1, cp = -1;
-                    while (ci < blen) {
-                        const int cnt = min(64, blen - ci);
-                        const uint64_t m = ci < 64 ? m0_shift(a0, a1, ci) : (a1 >> (ci - 64));
-                        const TileOut to = wave_tile(cd, m, cnt, min_inst, wl, cl, W.tile);
-                        const uint64_t upto = to.last >= 63 ? ~0ull : ((1ull << (to.last + 1)) - 1);
-                        const uint64_t wb = to.warn & upto;
-                        if (cw < 0 && wb) cw = ci + __builtin_ctzll(wb);
-                        if (to.kc >= 0) {
-                            cp = ci + to.kc;
-                            break;
-                        }
-                        ci += cnt;
-                    }
-                    if (lane == t) {
-                        C.rec[lane * nb + tj] = (uint32_t)(cw + 1) | ((uint32_t)(cp + 1) << 8);
-                        nev += (cw >= 0 || cp >= 0) ? 1 : 0;
-                        dw = cd;
-                        if (cp >= 0) det_reset(dw);         // DDM dropped (DDM_Process.py:209)
-                        ++jw;
-                        task = 0;
-                    }
-                }
-            }
-            if (walker) {
-                state_io[sid] = store_det(dw);
-                if (nev_out) nev_out[sid] = nev;
-            }
-            wave_sync_lds();
-            OP_T(3);
-            // the events, one lane per batch (perm_map labels)
-            const int64_t b0 = s0 * nb;
-            for (int r0 = 0; r0 < nbc; r0 += 64) {
-                const int i = r0 + lane;
-                if (i < nbc) {
-                    const uint32_t rc = C.rec[i];
-                    int w = (int)(rc & 0xffu) - 1, cc = (int)((rc >> 8) & 0xffu) - 1;
-                    if (kPmap) {
-                        const int sl = (int)(__umulhi((uint32_t)i, magic) >> msh);
-                        const int j = i - sl * nb;
-                        const int64_t brow = row0 + (int64_t)sl * L + (int64_t)j * pb;
-                        if (w >= 0) w = pmap[brow + w];
-                        if (cc >= 0) cc = pmap[brow + cc];
-                    }
-                    ev[b0 + i] = make_int2(w, cc);
-                }
-            }
-            wave_sync_lds();
-            OP_T(4);
-        }
-        if (!have) break;
-        prev = c;
-    }
-#ifdef DDM_OP_PROFILE
-    OP_T(5);
-    if (lane == 0) {
-        unsigned long long* acc = reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(ctr) + 64);
-        for (int kk = 0; kk < 8; ++kk) atomicAdd(acc + kk, (unsigned long long)ph[kk]);
-    }
-#endif
-}
-
-// streams per chunk of the one-pass form (0: the stream does not fit a chunk)
-int onepass_streams(int64_t L, int64_t nb) {
-    if (L <= 0 || L > kOpMaxRows || nb > kOpRecCap) return 0;
-    return (int)std::min<int64_t>(std::min<int64_t>(kOpMaxRows / L, kOpRecCap / nb), 64);
-}
-
-// i / nb by (i * magic) >> (32 + msh) for every i < kOpRecCap (checked once per nb)
-bool op_magic(int nb, uint32_t& magic, int& msh) {
-    for (int s = 0; s < 32; ++s) {
-        const uint64_t m = (((uint64_t)1 << (32 + s)) + (uint64_t)nb - 1) / (uint64_t)nb;
-        if (m >> 32) break;
-        bool ok = true;
-        for (uint64_t i = 0; i < (uint64_t)kOpRecCap && ok; ++i) ok = ((i * m) >> (32 + s)) == i / (uint64_t)nb;
-        if (ok) {
-            magic = (uint32_t)m;
-            msh = s;
-            return true;
-        }
-    }
-    return false;
-}
-
-int64_t onepass_blocks() {
-    static const int64_t b = [] {
-        int dev = 0, cus = 256, per_cu = 4;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_scan_batches_onepass<false>, kOpThreads, 0) !=
-                hipSuccess ||
-            per_cu <= 0)
-            per_cu = 4;
-        return (int64_t)cus * per_cu;
-    }();
-    return b;
-}
-
 // Scratch: counters, the fix-up list, flag bytes, the per-wave queues and the end states /
 // level-1 records of unchanged batches (written sparsely, indexed by item).
 constexpr int64_t kMaxWaves = 1 << 14;
@@ -1848,31 +1222,6 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
     if (int rc = ddm::hip_status(hipMemsetAsync(scratch, 0, (size_t)(256 + ((4 * n_streams + 255) & ~255)), s),
                                  "ddm_scan_batches: memset"))
         return rc;
-    // the one-pass form when a chunk holds at least one whole stream
-    static const bool onepass_on = env_int("DDM_SCAN_ONEPASS", 1) != 0;
-    static const int op_steps = std::max(0, env_int("DDM_OP_STEPS", 4));
-    static const int op_step_min = std::max(1, std::min(64, env_int("DDM_OP_STEP_MIN", 32)));
-    static const int op_straggle = std::max(0, std::min(64, env_int("DDM_OP_STRAGGLE", 8)));
-    uint32_t op_m = 0;
-    int op_s = 0;
-    const int op_g = onepass_on ? onepass_streams(stream_len, nb) : 0;
-    if (n_items > 0 && op_g > 0 && op_magic((int)nb, op_m, op_s)) {
-        const bool pre = use_pre && prm->per_batch >= kPre;
-        hipLaunchKernelGGL(k_scan_prefix_table, dim3(kPreN / 256), dim3(256), 0, s, *prm, sc.pst, sc.ptab);
-        if (int rc = ddm::launch_status("ddm_scan_batches/prefix")) return rc;
-        const int64_t n_chunks = ddm::ceil_div(n_streams, op_g);
-        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(onepass_blocks(), ddm::ceil_div(n_chunks, kOpWaves)));
-        const auto k = perm_map ? k_scan_batches_onepass<true> : k_scan_batches_onepass<false>;
-        hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kOpThreads), 0, s, err, n_streams, (int32_t)stream_len,
-                           (int32_t)nb, *prm, state_io, reinterpret_cast<int2*>(ev_out), nev_out, perm_map, sc.ptab,
-                           sc.pst, sc.ctr, (int32_t)op_g, op_m, (int32_t)op_s, pre, op_steps, cls_pop, op_step_min,
-                           op_straggle);
-        if (int rc = ddm::launch_status("ddm_scan_batches/onepass")) return rc;
-        if (ev_end)
-            if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record"))
-                return rc;
-        return 0;
-    }
     if (n_items > 0) {
         // whole workgroups of waves, each with a queue of qcap slots (its fills' items)
         const int64_t nfill = ddm::ceil_div(n_items, 64);
