@@ -119,6 +119,9 @@ def parse():
     ap.add_argument("--predict-replays", type=int, default=0,
                     help="isolated back-to-back replays of the last timed step's predict tables (a side figure; "
                          "0 for PMC runs, whose rows must be the steps' own)")
+    ap.add_argument("--gc", default="on", choices=["on", "freeze", "off"],
+                    help="Python's cyclic garbage collector during the timed steps: on, frozen after setup "
+                         "(gc.freeze: the setup's objects leave the collected generations), or off")
     ap.add_argument("--solo-world", type=int, default=0,
                     help="measurement aid: run only rank 0's partitions of an N-GPU job (d % N == 0), one "
                          "process, no collective (the per-GPU share of the strong-scaling workloads)")
@@ -443,12 +446,16 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
 
     def step():
         streams = [MTStream.from_seed(seed_base + d) for d, _ in parts]
+        tr = time.perf_counter()
         outs = runner.run(streams)
+        tr = time.perf_counter() - tr
         for (d, _), o, g in zip(parts, outs, streams):
             results[d] = o
             rngs[d] = g
+        step.run_ms = tr * 1e3
         if getattr(runner, "trace", None) and os.environ.get("DDM_HOST_TRACE_OUT"):
-            with open(os.environ["DDM_HOST_TRACE_OUT"], "w") as f:    # the last run's host phases
+            step.n = getattr(step, "n", 0) + 1
+            with open(f"{os.environ['DDM_HOST_TRACE_OUT']}.{step.n}", "w") as f:    # every run's host phases
                 json.dump(runner.trace, f)
         if world > 1:
             # the collect of DDM_Process.py:258: the drift/warning positions of every
@@ -470,26 +477,39 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     # the timed steps enqueue no timing events; the kernel times come from one instrumented
     # step after them
     runner.set_kernel_timing(False)
-    # the predict launches of the timed steps are timed by HIP events on the epoch stream
-    # (a pair per device epoch, read after each run)
+    # the predict launches of the timed steps are timed on the device clock (devctl.PredictTimer:
+    # each launch's first workgroups stamp their start and every workgroup its end, and the
+    # staging kernel after it folds the span into a running sum); without it (c2 / c5 by
+    # default) the instrumented step's HIP events around each predict are the fallback
     timed_predicts = args.predict_timing if args.predict_timing >= 0 else int(kind in ("c3", "c3w"))
     runner.set_predict_timing(bool(timed_predicts))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     allocs0 = torch.cuda.memory_stats(dev).get("num_device_alloc", 0)
-    step_ms = []
+    import gc
+    if args.gc != "on":
+        gc.collect()
+        gc.freeze()
+        if args.gc == "off":
+            gc.disable()
+    step_ms, step_epochs, run_ms = [], [], []
     t0 = time.perf_counter()
     for k in range(args.steps):
         ts = time.perf_counter()
         results.clear()
         step()                            # returns with the run's outputs on the host
         step_ms.append((time.perf_counter() - ts) * 1e3)
+        step_epochs.append(runner.stats.epochs)
+        run_ms.append(step.run_ms)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     timed_allocs = torch.cuda.memory_stats(dev).get("num_device_alloc", 0) - allocs0
+    if args.gc != "on":
+        gc.enable()
+        gc.unfreeze()
     runner.set_predict_timing(False)
     for g, r in results.items():          # every step reproduces the same events
         if args.warmup and not np.array_equal(r, ref_events[g]):
@@ -548,9 +568,10 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     replay_ms, replay_n = runner.replay_predict(repeats=args.predict_replays) if args.predict_replays else (0.0, 0)
     runner.predict_log = None
     runner.close()
-    # headline: the in-step launches (HIP events around each predict of the instrumented
-    # step, the side stream's shuffles co-running as in the timed steps); the isolated
-    # back-to-back replays of the same tables are a side figure
+    # headline: the timed steps' own predict launches on the device clock (the side stream's
+    # shuffles co-running), or the instrumented step's HIP events when that is off; the
+    # isolated back-to-back replays of the same tables (in the form the epochs ran them) are a
+    # side figure
     avg_ms = avg_ms_step
     bytes_launch = dev_bytes / launches
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
@@ -594,6 +615,8 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
              "host_s_per_step": agg["host_s"] / args.steps, "gpu_wait_s_per_step": agg["gpu_s"] / args.steps,
              "stream_prep_s_per_step": agg["prep_s"] / args.steps,
              "timed_step_ms": [round(v, 3) for v in step_ms],
+             "timed_step_epochs": [b - a for a, b in zip([0] + step_epochs[:-1], step_epochs)],
+             "timed_step_run_ms": [round(v, 3) for v in run_ms],
              "device_allocs_in_timed_steps": timed_allocs,
              "kernel_ms_from": "one instrumented step after the timed ones (HIP events around each launch)",
              "gather_ms_per_step": gather_s[0] / args.steps * 1e3 if world > 1 else None,
@@ -621,8 +644,9 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
                 "isolated_replay": {"avg_launch_ms": replay_ms if replay_n else None, "launches": replay_n,
                                     "achieved": replay_gbs,
                                     "frac": replay_gbs / PEAK_HBM_GBS if replay_gbs else None,
-                                    "note": "the last timed step's segment tables replayed back to back in coupled "
-                                            "form (permutation read in the predict), nothing co-running"},
+                                    "note": "the instrumented step's segment tables replayed back to back in the "
+                                            "form each epoch ran them (row order for decoupled epochs, the "
+                                            "permutation read for coupled ones), nothing co-running"},
                 "k_err_permute": {"rows_per_step": agg["permute_rows"] / args.steps,
                                   "alg_bytes_per_row": "1 (error-free batches before the first error's batch: "
                                                        "zero-fill) to 3 (row-order error read, permutation read, "
@@ -903,8 +927,27 @@ def companion_c2(args, rank, dev, torch, dist):
             "predict_roofline_frac": roofline["frac"]}
 
 
+def keep_freed_outputs_in_heap():
+    """glibc serves the runs' dense per-batch outputs (DDM_Process.py:212: one row per batch,
+    20 MB per C3 partition) by mmap and, the first time such an array is freed, unmaps its
+    pages and raises its dynamic mmap threshold; that one-off munmap of the previous step's
+    ~160 MB (7-10 ms) landed in a timed step of most processes (round 4's "slow first step":
+    run() itself took its usual time, profiles/r05/slowstep).  With the mmap and
+    trim thresholds set up front, large arrays come from the heap and freed ones are reused,
+    as they are after that first free anyway."""
+    import ctypes
+    try:
+        libc = ctypes.CDLL("libc.so.6")
+    except OSError:
+        return False
+    M_TRIM_THRESHOLD, M_MMAP_THRESHOLD = -1, -3
+    ok = libc.mallopt(M_MMAP_THRESHOLD, 1 << 30) == 1
+    return ok and libc.mallopt(M_TRIM_THRESHOLD, 1 << 30) == 1
+
+
 def main():
     args = parse()
+    keep_freed_outputs_in_heap()
     world, rank, local_rank = dist_env()
     if "WORLD_SIZE" in os.environ:
         if args.gpus != world and args.solo_world == 0:

@@ -56,3 +56,52 @@ extern "C" int ddm_event_elapsed_ms(ddm_event_t begin, ddm_event_t end, float* m
     return ddm::hip_status(hipEventElapsedTime(ms, reinterpret_cast<hipEvent_t>(begin), reinterpret_cast<hipEvent_t>(end)),
                            "ddm_event_elapsed_ms");
 }
+
+// ABI 22: a stream whose kernels run on a subset of the device's CUs (hipExtStreamCreateWithCUMask):
+// CU i is in the mask when i % stride == offset % stride (stride 1: every CU).  The runner's
+// side stream takes the next windows' shuffles off the CUs the epoch stream's predict needs.
+extern "C" int ddm_stream_create_cu_stride(int32_t stride, int32_t offset, ddm_stream_t* out, int32_t* n_cus) {
+    if (!out || stride < 1) {
+        ddm::set_error("ddm_stream_create_cu_stride: invalid argument");
+        return DDM_E_ARG;
+    }
+    int dev = 0, cus = 0;
+    if (int rc = ddm::hip_status(hipGetDevice(&dev), "ddm_stream_create_cu_stride")) return rc;
+    if (int rc = ddm::hip_status(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev),
+                                 "ddm_stream_create_cu_stride"))
+        return rc;
+    const int words = (cus + 31) / 32;
+    uint32_t mask[64] = {0};
+    if (words > 64) {
+        ddm::set_error("ddm_stream_create_cu_stride: %d CUs", cus);
+        return DDM_E_ARG;
+    }
+    int n = 0;
+    for (int i = 0; i < cus; ++i)
+        if (i % stride == offset % stride) {
+            mask[i / 32] |= 1u << (i % 32);
+            ++n;
+        }
+    hipStream_t st;
+    if (int rc = ddm::hip_status(hipExtStreamCreateWithCUMask(&st, (uint32_t)words, mask), "hipExtStreamCreateWithCUMask"))
+        return rc;
+    *out = reinterpret_cast<ddm_stream_t>(st);
+    if (n_cus) *n_cus = n;
+    return 0;
+}
+
+// ABI 22: the CU mask a stream runs with (words of 32 CUs, n_words at most 64); *n_cus its CU count.
+extern "C" int ddm_stream_cu_count(ddm_stream_t stream, int32_t* n_cus) {
+    if (!n_cus) return DDM_E_ARG;
+    uint32_t mask[64] = {0};
+    if (int rc = ddm::hip_status(hipExtStreamGetCUMask(ddm::as_hip(stream), 64, mask), "hipExtStreamGetCUMask"))
+        return rc;
+    int n = 0;
+    for (int k = 0; k < 64; ++k) n += __builtin_popcount(mask[k]);
+    *n_cus = n;
+    return 0;
+}
+
+extern "C" int ddm_stream_destroy(ddm_stream_t stream) {
+    return ddm::hip_status(hipStreamDestroy(ddm::as_hip(stream)), "ddm_stream_destroy");
+}

@@ -736,7 +736,19 @@ bool cf_usable(const Seg& g, int pb) {
 // not compile, or needs more LDS than the launch has) sets stall[s]: the partition waits
 // for the host, which refits or walks it.
 constexpr size_t kDevLds = 80 * 1024;
-constexpr size_t kDevLdsRowOrder = 24 * 1024;
+constexpr size_t kDevLdsRowOrderDefault = 24 * 1024;
+// the row-order launch's LDS per workgroup (tuning builds: DDM_ROW_LDS_KB)
+size_t row_order_lds() {
+#ifdef DDM_TUNING
+    static const size_t v = [] {
+        const char* e = getenv("DDM_ROW_LDS_KB");
+        return e ? (size_t)atoi(e) * 1024 : kDevLdsRowOrderDefault;
+    }();
+    return v;
+#else
+    return kDevLdsRowOrderDefault;
+#endif
+}
 
 __device__ __forceinline__ int cf_rows_dev(const Seg& g, int pb) {
     if (g.cf_leaves > 0) return 1;
@@ -1131,10 +1143,10 @@ extern "C" int ddm_forest_predict_dev_orig(const ddm_predict_segment* segs_dev, 
     // run, and a predict workgroup that does not fit waits for them (a 20 us gap per C3
     // epoch at 48 KB).  A forest that needs more stalls its partition to the host, as any
     // unusable forest, and the runner stops decoupling (ddm_amd/devctl.py).
-    hipLaunchKernelGGL(k_cforest_predict_dev, dim3((unsigned)grid), dim3(kCfThreads), kDevLdsRowOrder,
-                       ddm::as_hip(stream), reinterpret_cast<const Seg*>(segs_dev), res_dev, (int)n_segs,
-                       (int)per_batch, stall, delta, (int)kDevLdsRowOrder, reinterpret_cast<unsigned long long*>(clk),
-                       join_flag, join_v, timeouts);
+    const size_t lds = row_order_lds();
+    hipLaunchKernelGGL(k_cforest_predict_dev, dim3((unsigned)grid), dim3(kCfThreads), lds, ddm::as_hip(stream),
+                       reinterpret_cast<const Seg*>(segs_dev), res_dev, (int)n_segs, (int)per_batch, stall, delta,
+                       (int)lds, reinterpret_cast<unsigned long long*>(clk), join_flag, join_v, timeouts);
     return ddm::launch_status("ddm_forest_predict_dev_orig");
 }
 

@@ -12,7 +12,7 @@ import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 # DDM_AMD_LIB: an alternative build of the same library (e.g. an instrumented one)
 LIB_PATH = os.environ.get("DDM_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
@@ -132,6 +132,11 @@ SIGNATURES = {
     "ddm_event_destroy": (ctypes.c_int, [_vp]),
     "ddm_event_elapsed_ms": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(ctypes.c_float)]),
     "ddm_event_record": (ctypes.c_int, [_vp, _vp]),
+    "ddm_stream_create_cu_stride": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, _vp, _pi32]),
+    "ddm_forest_predict_dev_orig": (ctypes.c_int, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, _i64, _vp, _i64, _vp,
+                                                   _vp, ctypes.c_uint32, _vp, _vp]),
+    "ddm_stream_cu_count": (ctypes.c_int, [_vp, _pi32]),
+    "ddm_stream_destroy": (ctypes.c_int, [_vp]),
     "ddm_event_synchronize": (ctypes.c_int, [_vp]),
     "ddm_mt_perms": (ctypes.c_int, [_vp, _pi32, _vp, _i64, _vp, _vp]),
     "ddm_mt_randint31": (ctypes.c_int, [_vp, _pi32, _i64, _vp]),

@@ -72,6 +72,11 @@ GEN_PIECE_MIN = int(os.environ.get("DDM_GEN_PIECE_MIN", 1 << 23))
 # host time with the GPU otherwise idle): C3 56.0 / 56.7 / 56.4 -> 54.9 / 54.8 / 55.1 ms
 # per step (the same box, alternating)
 EARLY_PIECES = int(os.environ.get("DDM_EARLY_PIECES", "1"))
+# The side stream (the next windows' shuffles, beside the refits and the next predict) on
+# every SIDE_CU_STRIDE-th CU only (ddm_stream_create_cu_stride; 1: all CUs): its fused replay
+# holds ~17 KB of LDS per one-wave workgroup, so on every CU it left no room for the
+# predict's workgroups, which then ran at 0.50 of HBM instead of 0.71.
+SIDE_CU_STRIDE = int(os.environ.get("DDM_SIDE_CU_STRIDE", "1"))
 
 
 def _round_up(n, m):
@@ -607,6 +612,10 @@ class BatchRunner:
         if getattr(self, "devctl", None) is not None:
             self.stream.synchronize()
             self.devctl.close()
+        if getattr(self, "_side_raw", None) is not None:
+            self.side_stream.synchronize()
+            lib.ddm_stream_destroy(self._side_raw)
+            self._side_raw = None
 
     # -- per-epoch tables: per-partition template records (the static fields), of which an
     #    epoch takes the live partitions' rows and sets the fields that move
@@ -1004,7 +1013,18 @@ class BatchRunner:
         E.stage_jobs, E.dfit_jobs = self.stage_jobs.d.data_ptr(), self.dfit_jobs.d.data_ptr()
         E.max_trees = self.s.n_estimators
         E.next_jobs = self.njobs.d.data_ptr()
-        self.side_stream = torch.cuda.Stream(self.device, priority=-1)   # the next windows' shuffles: as long as the refits
+        self._side_raw = None
+        if SIDE_CU_STRIDE > 1:
+            raw, ncu = ctypes.c_void_p(), ctypes.c_int32()
+            with torch.cuda.device(self.device):
+                check(lib.ddm_stream_create_cu_stride(SIDE_CU_STRIDE, 0, ctypes.byref(raw), ctypes.byref(ncu)),
+                      "ddm_stream_create_cu_stride")
+            self._side_raw = raw
+            self.side_cus = int(ncu.value)
+            self.side_stream = torch.cuda.ExternalStream(raw.value, device=self.device)
+        else:
+            self.side_cus = None
+            self.side_stream = torch.cuda.Stream(self.device, priority=-1)   # the next windows' shuffles
         E.side_stream = self.side_stream.cuda_stream
         self._fork_ev, self._join_ev = ctypes.c_void_p(), ctypes.c_void_p()
         check(lib.ddm_event_create_sync(ctypes.byref(self._fork_ev)), "ddm_event_create_sync")

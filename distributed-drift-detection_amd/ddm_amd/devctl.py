@@ -41,7 +41,7 @@ GROUP = 4                       # epochs per enqueued group
 # permutation kernel puts them into DDM order after it; small windows (C5, c2) keep the
 # shuffles before the predict (they finish under the refit, and the permutation would be one
 # launch more per epoch).
-DECOUPLE_ROWS = 200_000
+DECOUPLE_ROWS = int(os.environ.get("DDM_DECOUPLE_ROWS", 200_000))
 # DDM_CTL_GRAPH=1: each group of epochs is one replayed hipGraph (ddm_ctl_graph_create) instead
 # of ~20 launches and event operations per epoch enqueued from the host
 CTL_GRAPH = os.environ.get("DDM_CTL_GRAPH", "0") not in ("", "0")
@@ -310,7 +310,10 @@ class DeviceController:
         # HIP cannot time events that a graph records (hipEventElapsedTime: invalid resource
         # handle), so timed predicts keep the launched form
         use_graph = CTL_GRAPH and pt is None and not (timing or logging)
-        flags = CTL_FLAGS and self.flags_ok and not use_graph
+        # the instrumented (timing / logging) epochs order the streams by HIP events: with
+        # flags the joins sit inside the refit's pack and the predict's first workgroup, so
+        # the event pairs around those kernels would time the wait for the side stream too
+        flags = CTL_FLAGS and self.flags_ok and not use_graph and not (timing or logging)
         E.sync_flags = self.sync_flags.data_ptr() if flags else None
         E.sync_seq = ctypes.addressof(self.sync_seq) if flags else None
         if use_graph:
@@ -447,7 +450,7 @@ class DeviceController:
             with torch.cuda.stream(r.stream):
                 segs.copy_(r.segs.d[:self.n * kernels.SEG_DTYPE.itemsize], non_blocking=True)
                 res.copy_(self.res_ptrs, non_blocking=True)
-            r.predict_log.append(("dev", segs, res, k))
+            r.predict_log.append(("dev", segs, res, k, int(E.decouple)))
         check(lib.ddm_ctl_epochs(ctypes.byref(E), 1), "ddm_ctl_epochs")
         for k in range(12):
             E.ev[k] = None
@@ -466,19 +469,32 @@ class DeviceController:
         return tot
 
     def replay(self, entry, stream):
-        """One logged device-mode predict launch again (the bench's roofline replays)."""
-        _, segs, res, _ = entry
-        check(lib.ddm_forest_predict_dev(segs.data_ptr(), res.data_ptr(), self.n, self.r.s.per_batch, PREDICT_BLOCKS,
-                                         self.pstall.data_ptr(), ctypes.c_void_p(stream.cuda_stream), None, None),
-              "ddm_forest_predict_dev")
+        """One logged device-mode predict launch again, in the form the epoch ran it: row
+        order into the decoupled epochs' second buffer, or DDM order through the shuffle (the
+        bench's roofline replays)."""
+        _, segs, res, _, dec = entry
+        if dec:
+            check(lib.ddm_forest_predict_dev_orig(segs.data_ptr(), res.data_ptr(), self.n, self.r.s.per_batch,
+                                                  PREDICT_BLOCKS, self.pstall.data_ptr(),
+                                                  self.err_rows.data_ptr() - self.r.err_all.data_ptr(), None, None, 0,
+                                                  None, ctypes.c_void_p(stream.cuda_stream)),
+                  "ddm_forest_predict_dev_orig")
+        else:
+            check(lib.ddm_forest_predict_dev(segs.data_ptr(), res.data_ptr(), self.n, self.r.s.per_batch,
+                                             PREDICT_BLOCKS, self.pstall.data_ptr(),
+                                             ctypes.c_void_p(stream.cuda_stream), None, None),
+                  "ddm_forest_predict_dev")
 
     def _take_back(self, live):
         """Device records -> the partitions' host state (and their events)."""
         r, st, pb = self.r, self.r.stats, self.r.s.per_batch
         with torch.cuda.stream(r.stream):
             self.parts_h.copy_(self.parts_d, non_blocking=True)
+            r._mark("records copy enqueued")
             r.ctrl_h.copy_(r.ctrl_d, non_blocking=True)        # staging slots and refit results
+            r._mark("slab copy enqueued")
             self.sync_h.copy_(self.sync_flags, non_blocking=True)
+            r._mark("flags copy enqueued")
         r.stream.synchronize()
         r._mark("records copied")
         if int(self.sync_h[2]):

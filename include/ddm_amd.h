@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 21
+#define DDM_AMD_ABI_VERSION 22
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 256) */
@@ -322,6 +322,20 @@ int ddm_event_destroy(ddm_event_t ev);
 int ddm_event_record(ddm_event_t ev, ddm_stream_t stream);
 int ddm_event_synchronize(ddm_event_t ev);
 int ddm_event_elapsed_ms(ddm_event_t begin, ddm_event_t end, float* ms);
+
+/* ABI 22: a stream on a subset of the current device's CUs (hipExtStreamCreateWithCUMask):
+ * CU i belongs to it when i % stride == offset % stride; *n_cus (nullable) = their count.
+ * The device epochs put the next windows' shuffles on such a stream so that they leave the
+ * other CUs to the predict (DDM_Process.py:110-128 beside :187/:190's shuffles). */
+int ddm_stream_create_cu_stride(int32_t stride, int32_t offset, ddm_stream_t* out, int32_t* n_cus);
+/* ABI 22: the number of CUs a stream may run on (hipExtStreamGetCUMask). */
+int ddm_stream_cu_count(ddm_stream_t stream, int32_t* n_cus);
+int ddm_stream_destroy(ddm_stream_t stream);
+/* ABI 22: the decoupled epochs' predict launch (row order into err + delta; clk, join_flag and
+ * timeouts nullable), exported for the bench's back-to-back replays of an epoch's tables. */
+int ddm_forest_predict_dev_orig(const ddm_predict_segment* segs_dev, const int64_t* const* res_dev, int32_t n_segs,
+                                int32_t per_batch, int64_t grid, int32_t* stall, int64_t delta, uint64_t* clk,
+                                const uint32_t* join_flag, uint32_t join_v, uint32_t* timeouts, ddm_stream_t stream);
 
 /* ---- host-side MT19937 (numpy legacy RandomState layout: key[624], pos) ---------- */
 
