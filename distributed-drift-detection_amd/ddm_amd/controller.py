@@ -864,12 +864,14 @@ class BatchRunner:
             self._mark("head copy done")
             heads = head_h.numpy().view(np.uint32)
             for k, ps in enumerate(pss):
-                r = fy_from_words(heads[k, :n0 - (3 * pb + s.n_estimators + 64)], ps.blen(0))
+                # batches[0].sample (:187), natively (the Python loop took ~0.1 ms per partition
+                # on the step's critical path)
+                r = perm_seeds_from_words(heads[k, :n0 - (3 * pb + s.n_estimators + 64)], ps.blen(0), 0)
                 ps.words0 = None
                 if r is None:                                   # rejections ran past the read-back
                     perm0, ps.P = self.shuffles[ps.i].host_perm(0, ps.blen(0))
                 else:
-                    perm0, ps.P = r                             # batches[0].sample (:187)
+                    perm0, ps.P = r[0], r[2]
                     ps.words0 = heads[k, ps.P:ps.P + 3 * pb + s.n_estimators + 64].copy()
                 started.append(ps)
                 if ps.nb < 2:

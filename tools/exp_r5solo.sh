@@ -1,0 +1,7 @@
+# per-GPU shares of the strong-scaling workloads at N = 2 / 4 / 8 (bench.py --solo-world), final tree
+mkdir -p gpurun_out/r5solo
+for w in c3 c5 c2; do
+  for n in 2 4 8; do
+    timeout -k 10 300 python bench.py --workload $w --solo-world $n --cpu-baseline 0 --companion 0 > gpurun_out/r5solo/${w}_s$n.json 2> gpurun_out/r5solo/${w}_s$n.err || exit 1
+  done
+done
