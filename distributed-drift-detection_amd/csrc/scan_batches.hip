@@ -21,8 +21,6 @@
 //      carried chains run in the chain kernel, one wave per stream (wave_det.h).
 // Every decision is the exact fp64 recurrence of det.h; the results equal ddm_scan_streams
 // in mode 1 and the C oracle bit for bit.
-#include <mutex>
-
 #include "common.h"
 #include "det.h"
 #include "wave_det.h"
@@ -1229,142 +1227,11 @@ int64_t classify_waves() {
     return w;
 }
 
-// Stream chunks of one call: the tail kernels (exact<0>, exact<1>, walk, chain: latency-bound,
-// ~0.3 ms on configs[3]) of chunk c run on a side stream beside the classify pass of chunk
-// c + 1 (bandwidth-bound), so only the last chunk's tail is exposed.  Chunks are whole
-// multiples of 64 streams (their event rows start on 512-byte lines, their bytes on 16-byte
-// boundaries); a call below 2 * kMinChunkStreams streams is one chunk on the caller's stream.
-constexpr int64_t kMinChunkStreams = 65536;
-
-int64_t scan_chunks(int64_t n_streams) {
-    static const int64_t want = std::max(1, std::min(8, env_int("DDM_SCAN_CHUNKS", 4)));
-    static const int64_t min_streams = std::max(64, env_int("DDM_SCAN_MIN_CHUNK", (int)kMinChunkStreams));
-    return std::max<int64_t>(1, std::min<int64_t>(want, n_streams / min_streams));
-}
-
-// streams [c * n / k, (c + 1) * n / k) rounded down to multiples of 64 (the last chunk ends at n)
-int64_t chunk_start(int64_t n_streams, int64_t k, int64_t c) {
-    return c >= k ? n_streams : (n_streams * c / k) & ~(int64_t)63;
-}
-
-int64_t scratch_total(int64_t n_streams, int64_t nb) {
-    const int64_t k = scan_chunks(n_streams);
-    int64_t total = 0;
-    for (int64_t c = 0; c < k; ++c)
-        total += batch_scratch(nullptr, chunk_start(n_streams, k, c + 1) - chunk_start(n_streams, k, c), nb).bytes;
-    return total;
-}
-
-// The side stream and the fork / join events of the chunked form, per device, created at the
-// first chunked call and kept for the process (a mutex orders concurrent callers' enqueues,
-// so one caller's event records cannot interleave with another's waits).
-struct ChunkSide {
-    hipStream_t side = nullptr;
-    hipEvent_t fork[8] = {}, join = nullptr;
-};
-std::mutex g_chunk_mu;
-ChunkSide g_chunk_side[64];
-
-int chunk_side(ChunkSide** out) {
-    int dev = 0;
-    if (int rc = ddm::hip_status(hipGetDevice(&dev), "ddm_scan_batches: hipGetDevice")) return rc;
-    if (dev < 0 || dev >= 64) {
-        ddm::set_error("ddm_scan_batches: device %d", dev);
-        return DDM_E_ARG;
-    }
-    ChunkSide& cs = g_chunk_side[dev];
-    if (!cs.side) {
-        if (int rc = ddm::hip_status(hipStreamCreateWithFlags(&cs.side, hipStreamNonBlocking), "ddm_scan_batches: side stream"))
-            return rc;
-        for (auto& e : cs.fork)
-            if (int rc = ddm::hip_status(hipEventCreateWithFlags(&e, hipEventDisableTiming), "ddm_scan_batches: event"))
-                return rc;
-        if (int rc = ddm::hip_status(hipEventCreateWithFlags(&cs.join, hipEventDisableTiming), "ddm_scan_batches: event"))
-            return rc;
-    }
-    *out = &cs;
-    return 0;
-}
-
-// One chunk: streams [0, n_streams) of the pointers given (already offset), its own scratch
-// (sc), the prefix table built once per call (pst / ptab).  The classify pass runs on s_cls;
-// when s_tail differs, `fork` is recorded after it and the tail runs on s_tail.
-int scan_chunk(const uint8_t* err, int64_t n_streams, int64_t stream_len, const ddm_params* prm, ddm_state* state_io,
-               int32_t* ev_out, int64_t* nev_out, const BatchScratch& sc, const double4* pst, const uint16_t* ptab,
-               const uint8_t* perm_map, hipStream_t s_cls, hipStream_t s_tail, hipEvent_t fork) {
-    const int64_t nb = ddm::ceil_div(stream_len, prm->per_batch);
-    const int64_t nbp = ddm::ceil_div(nb, 64) * 64;
-    const int64_t n_items = n_streams * nb;
-    static const int ex_refill = std::max(1, std::min(64, env_int("DDM_EXACT_REFILL", 24)));
-    static const int fix_blocks_max = env_int("DDM_FIX_BLOCKS", 2048);
-    static const bool use_pre = env_int("DDM_SCAN_PRE", 1) != 0;
-    static const int cls_steps = std::max(0, env_int("DDM_SCAN_STEPS", 2));
-    static const int cls_pop = std::max(1, std::min(64, env_int("DDM_SCAN_POP", 16)));
-    if (int rc = ddm::hip_status(hipMemsetAsync(sc.ctr, 0, (size_t)(256 + ((4 * n_streams + 255) & ~255)), s_cls),
-                                 "ddm_scan_batches: memset"))
-        return rc;
-    // whole workgroups of waves, each with a queue of qcap slots (its fills' items)
-    const int64_t nfill = ddm::ceil_div(n_items, 64);
-    const int64_t blocks = ddm::ceil_div(std::max<int64_t>(1, std::min<int64_t>(classify_waves(), nfill)), kClsThreads / 64);
-    const int64_t qcap = ddm::ceil_div(std::max<int64_t>(1, nfill), blocks * (kClsThreads / 64)) * 64;
-    int2* ev = reinterpret_cast<int2*>(ev_out);
-    if (n_items > 0) {
-        // the prefix table is used when batches have at least kPre rows
-        const bool pre = use_pre && prm->per_batch >= kPre;
-        // 16-byte chunks per fill: (63 * pb + 128 + 15) / 16 + 1, per 64 lanes
-        const bool small = prm->per_batch <= 100;
-        const auto cls = perm_map ? (small ? k_scan_batches_classify<true, 7> : k_scan_batches_classify<true, kClsLoads>)
-                                  : (small ? k_scan_batches_classify<false, 7> : k_scan_batches_classify<false, kClsLoads>);
-#ifdef DDM_TUNING
-        static const bool probe = env_int("DDM_SCAN_PROBE", 0) != 0;
-        if (probe)
-        {
-            static const int pm = env_int("DDM_SCAN_PROBE", 0);
-            const auto pk = pm == 2 ? k_scan_batches_probe<7, 1>
-                          : pm == 3 ? k_scan_batches_probe<7, 2> : k_scan_batches_probe<7, 0>;
-            hipLaunchKernelGGL(pk, dim3((unsigned)blocks), dim3(kClsThreads), 0, s_cls, err, n_items, stream_len, nb, nbp,
-                               *prm, ev, sc.qcnt, sc.q1cnt);
-        }
-        else
-#endif
-            hipLaunchKernelGGL(cls, dim3((unsigned)blocks), dim3(kClsThreads), 0, s_cls, err, n_items, stream_len, nb,
-                               nbp, *prm, ev, sc.flags, perm_map, qcap, sc.need, pre, ptab, pst, sc.q,
-                               sc.qcnt, sc.q1, sc.q1cnt, sc.pend, cls_steps, cls_pop);
-        if (int rc = ddm::launch_status("ddm_scan_batches/classify")) return rc;
-    }
-    if (s_tail != s_cls) {
-        if (int rc = ddm::hip_status(hipEventRecord(fork, s_cls), "ddm_scan_batches: fork")) return rc;
-        if (int rc = ddm::hip_status(hipStreamWaitEvent(s_tail, fork, 0), "ddm_scan_batches: fork wait")) return rc;
-    }
-    if (n_items > 0) {
-        const auto ex0 = perm_map ? k_scan_batches_exact<0, true> : k_scan_batches_exact<0, false>;
-        const auto ex1 = perm_map ? k_scan_batches_exact<1, true> : k_scan_batches_exact<1, false>;
-        hipLaunchKernelGGL(ex0, dim3((unsigned)blocks), dim3(kExThreads), 0, s_tail, err, n_items, stream_len, nb, nbp,
-                           *prm, ev, sc.flags, perm_map, qcap, sc.need, sc.q, sc.qcnt, sc.q1, sc.q1cnt,
-                           sc.pend, sc.ev1, sc.flags1, sc.pend1, ex_refill);
-        if (int rc = ddm::launch_status("ddm_scan_batches/exact")) return rc;
-        hipLaunchKernelGGL(ex1, dim3((unsigned)blocks), dim3(kExThreads), 0, s_tail, err, n_items, stream_len, nb, nbp,
-                           *prm, ev, sc.flags, perm_map, qcap, sc.need, sc.q, sc.qcnt, sc.q1, sc.q1cnt,
-                           sc.pend, sc.ev1, sc.flags1, sc.pend1, ex_refill);
-        if (int rc = ddm::launch_status("ddm_scan_batches/exact1")) return rc;
-    }
-    hipLaunchKernelGGL(k_scan_batches_walk, dim3((unsigned)ddm::ceil_div(n_streams, kWalkThreads)), dim3(kWalkThreads),
-                       0, s_tail, n_streams, stream_len, nb, nbp, *prm, state_io, ev, sc.flags, nev_out, perm_map,
-                       sc.need, sc.ctr, sc.pend, sc.ev1, sc.flags1, sc.pend1, sc.coop);
-    if (int rc = ddm::launch_status("ddm_scan_batches/walk")) return rc;
-    const int64_t fix_blocks =
-        std::max<int64_t>(1, std::min<int64_t>(fix_blocks_max, ddm::ceil_div(n_streams, kChainThreads / 64)));
-    hipLaunchKernelGGL(k_scan_batches_chain, dim3((unsigned)fix_blocks), dim3(kChainThreads), 0, s_tail, err, stream_len,
-                       nb, nbp, *prm, state_io, ev, sc.flags, nev_out, perm_map, sc.coop, sc.ctr, sc.pend, sc.ev1,
-                       sc.flags1, sc.pend1);
-    return ddm::launch_status("ddm_scan_batches/chain");
-}
-
 }  // namespace
 
 extern "C" int64_t ddm_scan_batches_scratch_bytes(int64_t n_streams, int64_t stream_len, int32_t per_batch) {
     if (n_streams < 0 || stream_len < 0 || per_batch <= 0) return -1;
-    return scratch_total(n_streams, ddm::ceil_div(stream_len, per_batch));
+    return batch_scratch(nullptr, n_streams, ddm::ceil_div(stream_len, per_batch)).bytes;
 }
 
 extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t stream_len, const ddm_params* prm,
@@ -1377,37 +1244,73 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
                        kMaxBatch);
         return DDM_E_ARG;
     }
-    if (n_streams == 0) return 0;
     const int64_t nb = ddm::ceil_div(stream_len, prm->per_batch);
+    const int64_t nbp = ddm::ceil_div(nb, 64) * 64;
+    const int64_t n_items = n_streams * nb;
+    if (n_streams == 0) return 0;
+    const BatchScratch sc = batch_scratch(scratch, n_streams, nb);
     hipStream_t s = ddm::as_hip(stream);
-    const int64_t k = scan_chunks(n_streams);
-    ChunkSide* cs = nullptr;
-    std::unique_lock<std::mutex> lock(g_chunk_mu, std::defer_lock);
-    if (k > 1) {
-        lock.lock();
-        if (int rc = chunk_side(&cs)) return rc;
-    }
+    static const int ex_refill = std::max(1, std::min(64, env_int("DDM_EXACT_REFILL", 24)));
+    static const int fix_blocks_max = env_int("DDM_FIX_BLOCKS", 2048);
+    static const bool use_pre = env_int("DDM_SCAN_PRE", 1) != 0;
+    static const int cls_steps = std::max(0, env_int("DDM_SCAN_STEPS", 2));
+    static const int cls_pop = std::max(1, std::min(64, env_int("DDM_SCAN_POP", 16)));
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
-    uint8_t* sb = static_cast<uint8_t*>(scratch);
-    const BatchScratch sc0 = batch_scratch(sb, chunk_start(n_streams, k, 1), nb);
-    // the prefix table once per call (the classify pass reads it whatever the batch length)
-    hipLaunchKernelGGL(k_scan_prefix_table, dim3(kPreN / 256), dim3(256), 0, s, *prm, sc0.pst, sc0.ptab);
-    if (int rc = ddm::launch_status("ddm_scan_batches/prefix")) return rc;
-    for (int64_t c = 0; c < k; ++c) {
-        const int64_t s0 = chunk_start(n_streams, k, c), n = chunk_start(n_streams, k, c + 1) - s0;
-        const BatchScratch sc = batch_scratch(sb, n, nb);
-        if (int rc = scan_chunk(err + s0 * stream_len, n, stream_len, prm, state_io + s0, ev_out + 2 * s0 * nb,
-                                nev_out ? nev_out + s0 : nullptr, sc, sc0.pst, sc0.ptab,
-                                perm_map ? perm_map + s0 * stream_len : nullptr, s, k > 1 ? cs->side : s,
-                                k > 1 ? cs->fork[c] : nullptr))
-            return rc;
-        sb += sc.bytes;
+    if (int rc = ddm::hip_status(hipMemsetAsync(scratch, 0, (size_t)(256 + ((4 * n_streams + 255) & ~255)), s),
+                                 "ddm_scan_batches: memset"))
+        return rc;
+    if (n_items > 0) {
+        // whole workgroups of waves, each with a queue of qcap slots (its fills' items)
+        const int64_t nfill = ddm::ceil_div(n_items, 64);
+        const int64_t blocks = ddm::ceil_div(std::min<int64_t>(classify_waves(), nfill), kClsThreads / 64);
+        const int64_t qcap = ddm::ceil_div(nfill, blocks * (kClsThreads / 64)) * 64;
+        // the prefix table is built whatever the batch length (the classify pass reads it
+        // unconditionally) and used when batches have at least kPre rows
+        const bool pre = use_pre && prm->per_batch >= kPre;
+        hipLaunchKernelGGL(k_scan_prefix_table, dim3(kPreN / 256), dim3(256), 0, s, *prm, sc.pst, sc.ptab);
+        if (int rc = ddm::launch_status("ddm_scan_batches/prefix")) return rc;
+        int2* ev = reinterpret_cast<int2*>(ev_out);
+        // 16-byte chunks per fill: (63 * pb + 128 + 15) / 16 + 1, per 64 lanes
+        const bool small = prm->per_batch <= 100;
+        const auto cls = perm_map ? (small ? k_scan_batches_classify<true, 7> : k_scan_batches_classify<true, kClsLoads>)
+                                  : (small ? k_scan_batches_classify<false, 7> : k_scan_batches_classify<false, kClsLoads>);
+#ifdef DDM_TUNING
+        static const bool probe = env_int("DDM_SCAN_PROBE", 0) != 0;
+        if (probe)
+        {
+            static const int pm = env_int("DDM_SCAN_PROBE", 0);
+            const auto pk = pm == 2 ? k_scan_batches_probe<7, 1>
+                          : pm == 3 ? k_scan_batches_probe<7, 2> : k_scan_batches_probe<7, 0>;
+            hipLaunchKernelGGL(pk, dim3((unsigned)blocks), dim3(kClsThreads), 0, s, err, n_items, stream_len, nb, nbp,
+                               *prm, ev, sc.qcnt, sc.q1cnt);
+        }
+        else
+#endif
+            hipLaunchKernelGGL(cls, dim3((unsigned)blocks), dim3(kClsThreads), 0, s, err, n_items, stream_len, nb,
+                               nbp, *prm, ev, sc.flags, perm_map, qcap, sc.need, pre, sc.ptab, sc.pst, sc.q,
+                               sc.qcnt, sc.q1, sc.q1cnt, sc.pend, cls_steps, cls_pop);
+        if (int rc = ddm::launch_status("ddm_scan_batches/classify")) return rc;
+        const auto ex0 = perm_map ? k_scan_batches_exact<0, true> : k_scan_batches_exact<0, false>;
+        const auto ex1 = perm_map ? k_scan_batches_exact<1, true> : k_scan_batches_exact<1, false>;
+        hipLaunchKernelGGL(ex0, dim3((unsigned)blocks), dim3(kExThreads), 0, s, err, n_items, stream_len, nb, nbp, *prm, ev,
+                           sc.flags, perm_map, qcap, sc.need, sc.q, sc.qcnt, sc.q1, sc.q1cnt,
+                           sc.pend, sc.ev1, sc.flags1, sc.pend1, ex_refill);
+        if (int rc = ddm::launch_status("ddm_scan_batches/exact")) return rc;
+        hipLaunchKernelGGL(ex1, dim3((unsigned)blocks), dim3(kExThreads), 0, s, err, n_items, stream_len, nb, nbp, *prm, ev,
+                           sc.flags, perm_map, qcap, sc.need, sc.q, sc.qcnt, sc.q1, sc.q1cnt,
+                           sc.pend, sc.ev1, sc.flags1, sc.pend1, ex_refill);
+        if (int rc = ddm::launch_status("ddm_scan_batches/exact1")) return rc;
     }
-    if (k > 1) {
-        if (int rc = ddm::hip_status(hipEventRecord(cs->join, cs->side), "ddm_scan_batches: join")) return rc;
-        if (int rc = ddm::hip_status(hipStreamWaitEvent(s, cs->join, 0), "ddm_scan_batches: join wait")) return rc;
-    }
+    hipLaunchKernelGGL(k_scan_batches_walk, dim3((unsigned)ddm::ceil_div(n_streams, kWalkThreads)), dim3(kWalkThreads),
+                       0, s, n_streams, stream_len, nb, nbp, *prm, state_io, reinterpret_cast<int2*>(ev_out),
+                       sc.flags, nev_out, perm_map, sc.need, sc.ctr, sc.pend, sc.ev1, sc.flags1, sc.pend1, sc.coop);
+    if (int rc = ddm::launch_status("ddm_scan_batches/walk")) return rc;
+    const int64_t fix_blocks =
+        std::max<int64_t>(1, std::min<int64_t>(fix_blocks_max, ddm::ceil_div(n_streams, kChainThreads / 64)));
+    hipLaunchKernelGGL(k_scan_batches_chain, dim3((unsigned)fix_blocks), dim3(kChainThreads), 0, s, err, stream_len,
+                       nb, nbp, *prm, state_io, reinterpret_cast<int2*>(ev_out), sc.flags, nev_out, perm_map,
+                       sc.coop, sc.ctr, sc.pend, sc.ev1, sc.flags1, sc.pend1);
     if (ev_end)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
     return ddm::launch_status("ddm_scan_batches");
