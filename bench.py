@@ -97,7 +97,9 @@ def parse():
                     help="CPU baseline worker processes (P); P x CORES = 16 = the GPU box's CPU share per GPU")
     ap.add_argument("--cpu-cores", type=int, default=1,
                     help="CPU baseline CORES = RF n_jobs per process (> 1: joblib threading backend)")
-    ap.add_argument("--cpu-sample-rows", type=int, default=90_000, help="rows per CPU baseline process")
+    ap.add_argument("--cpu-sample-rows", type=int, default=90_000, help="rows per CPU baseline process (c5, c4)")
+    ap.add_argument("--c3-cpu-rows", type=int, default=400_000,
+                    help="rows per CPU baseline process, c3 / c3w (stratified windows of the stream)")
     ap.add_argument("--oracle-check-rows", type=int, default=40_000,
                     help="rows of partition 0 re-run by the oracle after the timed region (0: off)")
     ap.add_argument("--c4-streams", type=int, default=1_000_000)
@@ -155,7 +157,7 @@ def _cpu_sample(spec):
     from oracle import synth
     kind, d, n_parts, r0, n, F, seed, extra = spec
     if kind == "c3":
-        y = synth.block_labels(r0 + n, d, n_parts, extra, 10)[r0:]
+        y = synth.block_labels(n, d, n_parts, extra, 10, start=r0)
     else:
         y = synth.jitter_labels(r0 + n, d, n_parts, extra[0], extra[1], 10, extra[2], seed)[r0:]
     X = synth.features(y, d + n_parts * r0, n_parts, seed, F)
@@ -269,16 +271,19 @@ class CpuBaseline:
                                                          f"result, sample building included)"}
 
 
-def c3_cpu_specs(args, n_parts, block):
-    """One sample per worker process: partition k % n_parts, a window of cpu_sample_rows
-    rows centred on its (k // n_parts + 1)-th class boundary (the predict, DDM, drift and
-    refit work of the stream)."""
-    half = args.cpu_sample_rows // 2
+def c3_cpu_specs(args, n_parts, block, n_rows):
+    """One sample per worker process: partition k % n_parts, a window of c3_cpu_rows rows at
+    a stratified position (sample j of the partition in the j-th of its equal strata, offset
+    by the partition's phase), so that the samples hold class boundaries (drifts + refits) at
+    the stream's own density instead of one each.  Each window still starts with the first
+    fit, as every partition run does; at 400k rows that fit is ~1-2 % of the sample's time."""
+    rows = min(args.c3_cpu_rows, n_rows)
+    per = -(-args.cpu_procs // n_parts)              # samples per partition
     specs = []
     for k in range(args.cpu_procs):
-        d, m = k % n_parts, k // n_parts + 1
-        b = (m * block - d + n_parts - 1) // n_parts
-        specs.append(("c3", d, n_parts, max(0, b - half), args.cpu_sample_rows, args.features, args.seed, block))
+        d, j = k % n_parts, k // n_parts
+        r0 = int((j + (d + 0.5) / n_parts) / per * (n_rows - rows))
+        specs.append(("c3", d, n_parts, r0, rows, args.features, args.seed, block))
     return specs
 
 
@@ -667,9 +672,11 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
             cpu_res = cpu.run(specs, f"{len(specs)} windows of {half} rows (partition k % {instances}, window k // "
                                      f"{instances}) of the c5 stream")
         else:
-            cpu_res = cpu.run(c3_cpu_specs(args, instances, block),
-                              f"{args.cpu_sample_rows} rows around each partition's first class boundary "
-                              f"(one drift + refit each) of the c3 stream")
+            cpu_res = cpu.run(c3_cpu_specs(args, instances, block, n),
+                              f"windows of {min(args.c3_cpu_rows, n)} rows of the c3 stream at stratified positions "
+                              f"(partition k % {instances}, sample k // {instances} in that stratum of the partition: "
+                              f"class boundaries at the stream's own density, one per {block // instances} "
+                              f"partition rows)")
     scaling = "weak" if kind == "c3w" else "strong"
     return rows_rank, elapsed, info, extra, roofline, cpu_res, scaling
 

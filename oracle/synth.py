@@ -30,8 +30,9 @@ def unit(seed, a, b):
     return (h >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
 
 
-def block_labels(n, part, n_parts, block_rows, n_classes):
-    g = np.arange(n, dtype=np.int64) * n_parts + part
+def block_labels(n, part, n_parts, block_rows, n_classes, start=0):
+    """Labels of partition rows [start, start + n)."""
+    g = np.arange(start, start + n, dtype=np.int64) * n_parts + part
     return ((g // block_rows) % n_classes).astype(np.int32)
 
 
