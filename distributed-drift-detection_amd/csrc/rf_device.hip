@@ -436,9 +436,6 @@ __global__ __launch_bounds__(kPrepThreads) void k_dfit_prep(const Job* __restric
     }
     __syncthreads();
     if (s_skip) return;                          // the result words keep the last refit's
-    // the count of the job's finished tree workgroups (k_dfit_trees_pack), zeroed here:
-    // the trees kernel starts after this one ends
-    if (lead && t == 0) *(gptr<uint32_t>)jb.scratch = 0u;
     if (!args_ok) {
         if (lead && t == 0) jb.result[DDM_DFIT_STATUS] = DDM_E_ARG;
         return;
@@ -1009,29 +1006,6 @@ __device__ int block_scan_excl(int v, int* tmp, int& total) {
     return base + inc - v;
 }
 
-// compile_forest's LDS (a struct, so that a kernel can overlay it on LDS it is done with)
-struct CompileLds {
-    int s_tmp[kPackThreads];
-    uint32_t s_first[kMaxF];
-    int16_t s_slot_of[kMaxF];
-    int s_cols[kMaxSlots];
-    uint8_t s_kind[256];
-    int16_t s_col[256], s_cl[256], s_cr[256], s_srank[256], s_prank[256], s_sid[256];
-    uint8_t s_nl[256];
-    float s_thr[256];
-    int16_t s_skey[256];
-    float s_sthr[256];
-    uint32_t s_key32[256];
-    uint64_t s_pkey[256];
-    uint32_t s_sdel[256][4];
-    uint32_t s_rtab[kMaxTabWords];
-    int s_gnode[256], s_gleaf[256], s_gtree[256], s_nint[256], s_nlv[256];
-    int s_m[kMaxSlots], s_n4[kMaxSlots], s_tab[kMaxSlots], s_xq[kMaxSlots];
-    uint32_t s_base[4];
-    int s_bad, s_anynl, s_U;
-    int64_t s_off[8];
-};
-
 // ddm_forest_compile (forest_compile.cpp) for a pure forest given as creation-order tree
 // nodes, by the whole workgroup.  The blob is byte for byte the host compiler's:
 //   * slots in order of first use over (tree, pre-order internal node): a min-key per
@@ -1044,43 +1018,28 @@ struct CompileLds {
 // Returns the blob size, or 0 when the forest does not compile.
 // tn_lds: when not null, this thread's tree (> 3 nodes) is at tn_lds[my_base ...] in LDS and
 // lrank_lds[my_base ...] is its scratch (k_dfit_pack copied it there)
-__device__ __forceinline__ int64_t compile_forest(const TNode* tn, int64_t M, const int32_t* meta, int T,
-                                                  const int32_t* classes, int K, int F, int16_t* lrank, uint8_t* out,
-                                                  int64_t cap, const TNode* tn_lds, int16_t* lrank_lds, int my_base,
-                                                  CompileLds& C) {
-    auto& s_tmp = C.s_tmp;
-    auto& s_first = C.s_first;
-    auto& s_slot_of = C.s_slot_of;
-    auto& s_cols = C.s_cols;
-    auto& s_kind = C.s_kind;
-    auto& s_col = C.s_col;
-    auto& s_cl = C.s_cl;
-    auto& s_cr = C.s_cr;
-    auto& s_srank = C.s_srank;
-    auto& s_prank = C.s_prank;
-    auto& s_sid = C.s_sid;
-    auto& s_nl = C.s_nl;
-    auto& s_thr = C.s_thr;
-    auto& s_skey = C.s_skey;
-    auto& s_sthr = C.s_sthr;
-    auto& s_key32 = C.s_key32;
-    auto& s_pkey = C.s_pkey;
-    auto& s_sdel = C.s_sdel;
-    auto& s_rtab = C.s_rtab;
-    auto& s_gnode = C.s_gnode;
-    auto& s_gleaf = C.s_gleaf;
-    auto& s_gtree = C.s_gtree;
-    auto& s_nint = C.s_nint;
-    auto& s_nlv = C.s_nlv;
-    auto& s_m = C.s_m;
-    auto& s_n4 = C.s_n4;
-    auto& s_tab = C.s_tab;
-    auto& s_xq = C.s_xq;
-    auto& s_base = C.s_base;
-    auto& s_bad = C.s_bad;
-    auto& s_anynl = C.s_anynl;
-    auto& s_U = C.s_U;
-    auto& s_off = C.s_off;
+__device__ int64_t compile_forest(const TNode* tn, int64_t M, const int32_t* meta, int T, const int32_t* classes,
+                                  int K, int F, int16_t* lrank, uint8_t* out, int64_t cap, const TNode* tn_lds,
+                                  int16_t* lrank_lds, int my_base) {
+    __shared__ int s_tmp[kPackThreads];
+    __shared__ uint32_t s_first[kMaxF];
+    __shared__ int16_t s_slot_of[kMaxF];
+    __shared__ int s_cols[kMaxSlots];
+    __shared__ uint8_t s_kind[256];
+    __shared__ int16_t s_col[256], s_cl[256], s_cr[256], s_srank[256], s_prank[256], s_sid[256];
+    __shared__ uint8_t s_nl[256];
+    __shared__ float s_thr[256];
+    __shared__ int16_t s_skey[256];
+    __shared__ float s_sthr[256];
+    __shared__ uint32_t s_key32[256];
+    __shared__ uint64_t s_pkey[256];
+    __shared__ uint32_t s_sdel[256][4];
+    __shared__ uint32_t s_rtab[kMaxTabWords];
+    __shared__ int s_gnode[256], s_gleaf[256], s_gtree[256], s_nint[256], s_nlv[256];
+    __shared__ int s_m[kMaxSlots], s_n4[kMaxSlots], s_tab[kMaxSlots], s_xq[kMaxSlots];
+    __shared__ uint32_t s_base[4];
+    __shared__ int s_bad, s_anynl, s_U;
+    __shared__ int64_t s_off[8];
 #ifdef DDM_DFIT_PROFILE
     __shared__ uint64_t s_prof[4];
     if (threadIdx.x == 0) s_prof[0] = wall_clock64();
@@ -1432,16 +1391,7 @@ __device__ void pack_tree(const TNode* tn, int m, int16_t* new_id, int16_t* queu
     }
 }
 
-// pack_job's LDS (with the compiler's inside)
-struct PackLds {
-    int s_tmp[kPackThreads];
-    int s_impure;
-    TNode s_tn[kPackLdsNodes];
-    int16_t s_bid[2 * kPackLdsNodes];
-    CompileLds c;
-};
-
-__device__ __forceinline__ void pack_job(const Job& jb, PackLds& P) {
+__device__ __forceinline__ void pack_job(const Job& jb) {
 #ifdef DDM_DFIT_PROFILE
     const uint64_t t_pack0 = wall_clock64();
 #endif
@@ -1454,10 +1404,10 @@ __device__ __forceinline__ void pack_job(const Job& jb, PackLds& P) {
     gptr<const TNode> tn = (gptr<const TNode>)(jb.scratch + lo.tnodes);
     gptr<const double> tv = (gptr<const double>)(jb.scratch + lo.tvals);
     gptr<int16_t> bfs = (gptr<int16_t>)(jb.scratch + lo.bfs);
-    auto& s_tmp = P.s_tmp;
-    auto& s_impure = P.s_impure;
-    auto& s_tn = P.s_tn;
-    auto& s_bid = P.s_bid;
+    __shared__ int s_tmp[kPackThreads];
+    __shared__ int s_impure;
+    __shared__ TNode s_tn[kPackLdsNodes];
+    __shared__ int16_t s_bid[2 * kPackLdsNodes];
     if (t == 0) s_impure = 0;
     __syncthreads();
     const int nn = t < T ? meta[4 * t] : 0;
@@ -1488,7 +1438,7 @@ __device__ __forceinline__ void pack_job(const Job& jb, PackLds& P) {
     if (pure && jb.blob)
         bytes = compile_forest((const TNode*)tn, M, (const int32_t*)meta, T, (const int32_t*)jb.classes, K, jb.F, (int16_t*)bfs,
                                (uint8_t*)jb.blob, jb.blob_cap,
-                               n_nodes <= kPackLdsNodes ? s_tn : nullptr, s_bid, base, P.c);
+                               n_nodes <= kPackLdsNodes ? s_tn : nullptr, s_bid, base);
 #ifdef DDM_DFIT_PROFILE
     if (t == 0)
         jb.result[11] = (int64_t)((t_p - t_pack0) | ((wall_clock64() - t_p) << 16) |
@@ -1514,80 +1464,9 @@ __device__ __forceinline__ void pack_job(const Job& jb, PackLds& P) {
 // they are done.
 __global__ __launch_bounds__(kPackThreads) void k_dfit_pack(const Job* __restrict__ jobs, const uint32_t* join_flag,
                                                             uint32_t join_v, uint32_t* timeouts) {
-    __shared__ PackLds lds;
     refit_priority();
-    pack_job(jobs[blockIdx.x], lds);
+    pack_job(jobs[blockIdx.x]);
     if (join_flag && blockIdx.x == 0 && threadIdx.x == 0) ddm::flag_poll(join_flag, join_v, timeouts);
-}
-
-// k_dfit_trees (prep kernel form) with the pack folded in: the last of a job's tree
-// workgroups to finish (a counter in the job's scratch word 0, zeroed by k_dfit_prep) packs
-// and compiles the job's forest, so each job's pack starts when its own trees are done and
-// the pack launch is gone.  Workgroup (0, 0) holds the kernel open until *join_flag
-// reaches join_v, as k_dfit_pack's workgroup 0 did.
-__global__ __launch_bounds__(64 * kWaves) void k_dfit_trees_pack(const Job* __restrict__ jobs, const uint32_t* join_flag,
-                                                                 uint32_t join_v, uint32_t* timeouts) {
-    // the trees' LDS, and once they are built, the pack's over it
-    __shared__ union {
-        struct {
-            WaveLds lds[kWaves];
-            float s_X[kTreeTile];
-            uint8_t s_ord[kTreeTile];
-            uint8_t s_yi[kMaxL];
-        } t;
-        PackLds p;
-    } U;
-    __shared__ int s_last;
-    auto& lds = U.t.lds;
-    auto& s_X = U.t.s_X;
-    auto& s_ord = U.t.s_ord;
-    auto& s_yi = U.t.s_yi;
-    refit_priority();
-    const Job jb = jobs[blockIdx.y];
-    const int w = threadIdx.x / 64, lane = threadIdx.x & 63;
-    const int tree = blockIdx.x * kWaves + w;
-    if (!gated_off(jb) && jb.result[DDM_DFIT_STATUS] == 0) {
-        const int K = (int)jb.result[DDM_DFIT_CLASSES];
-        const Layout lo = layout(jb.L, jb.F, jb.n_trees, jb.k_cap);
-        const int LF = jb.L * jb.F;
-        const uint8_t* yidx = (const uint8_t*)(jb.scratch + lo.yidx);
-        const uint8_t* order = (const uint8_t*)(jb.scratch + lo.order);
-        const int32_t* boot = (const int32_t*)(gptr<const int32_t>)(jb.scratch + lo.boot);
-        if (LF <= kTreeTile) {
-            for (int e = threadIdx.x; e < LF; e += 64 * kWaves) {
-                s_X[e] = jb.X[e];
-                s_ord[e] = order[e];
-            }
-            for (int e = threadIdx.x; e < jb.L; e += 64 * kWaves) s_yi[e] = yidx[e];
-            __syncthreads();
-            if (tree < jb.n_trees) build_tree(jb, lo, tree, K, lds[w], lane, s_X, s_ord, s_yi, boot, nullptr);
-        } else if (tree < jb.n_trees) {
-            build_tree(jb, lo, tree, K, lds[w], lane, (const float*)jb.X, order, yidx, boot, nullptr);
-        }
-        // every wave's tree is in scratch (release), then the ticket
-        __threadfence();
-        __syncthreads();
-        if (threadIdx.x == 0)
-            s_last = atomicAdd((uint32_t*)(gptr<uint32_t>)jb.scratch, 1u) == gridDim.x - 1;
-        __syncthreads();
-        if (s_last) {
-            __threadfence();                        // the other workgroups' trees (acquire)
-            pack_job(jb, U.p);
-        }
-    }
-    if (join_flag && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) ddm::flag_poll(join_flag, join_v, timeouts);
-}
-static_assert(64 * kWaves == kPackThreads, "the trees kernel's workgroup packs with kPackThreads threads");
-
-// Tuning knobs from the environment exist only in a tuning build (-DDDM_TUNING).
-int dfit_env_int(const char* name, int dflt) {
-#ifdef DDM_TUNING
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-#else
-    (void)name;
-    return dflt;
-#endif
 }
 
 }  // namespace
@@ -1617,16 +1496,10 @@ int rf_fit_device_join(const ddm_dfit_job* jobs_dev, int32_t n_jobs, int32_t max
     hipStream_t s = ddm::as_hip(stream);
     const Job* jobs = reinterpret_cast<const Job*>(jobs_dev);
     const bool fused = max_lf > 0 && max_lf <= kTreeTile;
-    static const bool pack_in_trees = dfit_env_int("DDM_DFIT_PACK_IN_TREES", 1) != 0;
     if (!fused) {
         hipLaunchKernelGGL(k_dfit_prep, dim3((unsigned)n_jobs, kSortBlocks + (unsigned)ddm::ceil_div(max_trees, kBootWaves)),
                            dim3(kPrepThreads), 0, s, jobs);
         if (int rc = ddm::launch_status("ddm_rf_fit_device/prep")) return rc;
-        if (pack_in_trees) {
-            hipLaunchKernelGGL(k_dfit_trees_pack, dim3((unsigned)ddm::ceil_div(max_trees, kWaves), (unsigned)n_jobs),
-                               dim3(64 * kWaves), 0, s, jobs, join_flag, join_v, timeouts);
-            return ddm::launch_status("ddm_rf_fit_device/trees+pack");
-        }
     }
     hipLaunchKernelGGL(fused ? k_dfit_trees<true> : k_dfit_trees<false>,
                        dim3((unsigned)ddm::ceil_div(max_trees, kWaves), (unsigned)n_jobs), dim3(64 * kWaves), 0, s,
