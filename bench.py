@@ -551,7 +551,7 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
     agg = {k: getattr(st, k) for k in ("epochs", "refits", "predicted_rows", "predict_bytes", "host_s", "gpu_s",
                                        "device_refits", "prep_s", "device_epochs", "device_phases", "permute_rows",
                                        "device_rows", "predict_dev_ms", "predict_dev_launches",
-                                       "device_predict_bytes", "spec_refits")}
+                                       "device_predict_bytes")}
     # kernel times of one step (the instrumented one), scaled to the timed steps
     for k in ("predict_ms", "scan_ms", "shuffle_ms", "dfit_ms"):
         agg[k] = getattr(st_kern, k) * args.steps
@@ -606,7 +606,6 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
                           "scan, stage and refit launch per epoch")}
     extra = {"drifts_per_step": drifts, "warnings_per_step": warns,
              "refits_per_step": agg["refits"] / args.steps, "epochs_per_step": agg["epochs"] / args.steps,
-             "speculative_refits_taken_per_step": agg["spec_refits"] / args.steps,
              "device_epochs_per_step": agg["device_epochs"] / args.steps,
              "device_phases_per_step": agg["device_phases"] / args.steps,
              "refits_per_s": agg["refits"] / elapsed,

@@ -75,11 +75,6 @@ __device__ inline void flag_publish(uint32_t* flag, uint32_t v) {
     __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Between two polls a poller sleeps DDM_FLAG_SLEEP x 64 clocks (1, 8 and 32 measured alike
-// on c2 / c3 / c5: profiles/r05/spec/sleep_*.json).
-#ifndef DDM_FLAG_SLEEP
-#define DDM_FLAG_SLEEP 1
-#endif
 __device__ inline void flag_poll(const uint32_t* flag, uint32_t v, uint32_t* timeouts) {
     const uint64_t t0 = wall_clock64();
     // the override applies to the join polls only: their consumers read perm bytes, every
@@ -89,7 +84,7 @@ __device__ inline void flag_poll(const uint32_t* flag, uint32_t v, uint32_t* tim
         flag == timeouts - 2 ? 0u : __hip_atomic_load(timeouts + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t limit = lim ? (uint64_t)lim : 200000000ull;   // 2 s at 100 MHz
     while ((int32_t)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - v) < 0) {
-        __builtin_amdgcn_s_sleep(DDM_FLAG_SLEEP);
+        __builtin_amdgcn_s_sleep(1);
         if (wall_clock64() - t0 > limit) {
             atomicAdd(timeouts, 1u);
             break;

@@ -108,7 +108,6 @@ int epoch_stage_ctl_pub(const ddm_stage_job* jobs_dev, const ddm_shuffle_job* sh
                         uint32_t pub_v, ddm_stream_t stream);
 int rf_fit_device_join(const ddm_dfit_job* jobs_dev, int32_t n_jobs, int32_t max_trees, int64_t max_lf,
                        const uint32_t* join_flag, uint32_t join_v, uint32_t* timeouts, ddm_stream_t stream);
-int epoch_spec_stage(const ddm_ctl* ctl, uint32_t wait_v, uint32_t pub_v, uint32_t* timeouts, ddm_stream_t stream);
 
 namespace {
 
@@ -224,14 +223,6 @@ int ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs, bool graph) {
     }
     // the predict's device-clock stamps are folded by k_stage_ctl: only with the fused tail
     uint64_t* const clk = c.sync ? c.predict_clock : nullptr;
-    // speculative refits (ABI 23): with the flags and the fused tail only
-    const bool spec = flags && c.sync && c.spec_k > 0 && c.spec_jobs && c.spec_gate && c.spec_flags && e->spec_stream;
-    hipStream_t spec_s = spec ? ddm::as_hip(e->spec_stream) : nullptr;
-#ifdef DDM_TUNING
-    // measurement: the candidates' refits on the epoch stream itself (no concurrency)
-    static const bool same = getenv("DDM_SPEC_SAME_STREAM") && atoi(getenv("DDM_SPEC_SAME_STREAM"));
-    if (same) spec_s = s;
-#endif
     auto join = [&]() {
         if (flags) {
             if (seq[2] == seq[1]) return 0;           // a pack kernel held the last one already
@@ -264,21 +255,6 @@ int ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs, bool graph) {
         if (int rc = rec(pb1, s)) return rc;
         if (dec && !first_in_graph)
             if (int rc = join()) return rc;
-        if (spec) {
-            // the candidates' staging right after the predict (and the window's shuffles),
-            // their refits on the speculative stream beside the scan and the staging
-            const uint32_t wait_v = seq[4];         // the last epoch's candidate refits
-            ++seq[3];
-            if (int rc = epoch_spec_stage(&c, wait_v, seq[3], flags + 2, e->stream)) return rc;
-            hipLaunchKernelGGL(k_flag_wait, dim3(1), dim3(64), 0, spec_s, c.spec_flags, seq[3], flags + 2);
-            if (int rc = ddm::launch_status("ddm_ctl_epochs/spec wait")) return rc;
-            if (int rc = rf_fit_device_join(c.spec_jobs, c.n * c.spec_k, e->max_trees, e->dfit_max_lf, nullptr, 0,
-                                            nullptr, reinterpret_cast<ddm_stream_t>(spec_s)))
-                return rc;
-            ++seq[4];
-            hipLaunchKernelGGL(k_flag_pub, dim3(1), dim3(64), 0, spec_s, c.spec_flags + 1, seq[4]);
-            if (int rc = ddm::launch_status("ddm_ctl_epochs/spec pub")) return rc;
-        }
         if (int rc = rec(e->ev[2], s)) return rc;
         if (dec)
             if (int rc = ddm_err_permute_dev(c.segs, c.n, e->per_batch, e->row_order_delta, kPermBlocks, e->stream))
@@ -304,8 +280,6 @@ int ctl_epochs(const ddm_ctl_epoch* e, int32_t n_epochs, bool graph) {
             if (int rc = rec(e->ev[4], s)) return rc;
             ddm_ctl cd = c;
             cd.decoupled = dec ? 1 : 0;
-            cd.spec_k = spec ? c.spec_k : 0;
-            cd.spec_v = spec ? seq[4] : 0u;
             if (int rc = epoch_stage_ctl_pub(c.stage, c.jobs, &cd, e->err, e->params, e->perm_map,
                                              flags ? flags : nullptr, flags ? seq[0] + 1 : 0, e->stream))
                 return rc;

@@ -381,145 +381,6 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(const Job* __restrict__
     stage_body(jb, jb.pick ? *jb.pick : -1);
 }
 
-// ---- speculative refits (ABI 23, ddm_ctl.spec_k > 0) ------------------------------------
-// A workgroup per (partition, candidate k): candidate batch c = fb + k, fb the batch of the
-// window's first error (c.first: the predict's first error position, or in decoupled epochs
-// its first error row -- the same batch).  When batch c + 1 lies in the window's shuffles
-// (so its shuffle is the reference's next draw after batch c's, DDM_Process.py:190, and the
-// staging of a change in batch c takes the seeds after it: stage_body's pos_next path), the
-// candidate gets batch c's rows in shuffled order and the tree seeds drawn from E[c + 1] + 1,
-// exactly what stage_body gathers and draws for a change in batch c, and spec_gate = c;
-// otherwise spec_gate = -1 and its refit is gated off.  wait_v: the last epoch's candidate
-// refits are done before their inputs are overwritten; the last workgroup publishes pub_v
-// (the refits' stream polls it).
-constexpr int kSpecThreads = 256;
-
-__global__ __launch_bounds__(kSpecThreads) void k_spec_stage(const ddm_ctl c, uint32_t wait_v, uint32_t pub_v,
-                                                             uint32_t* timeouts) {
-    __shared__ int64_t s_c, s_pos;
-    __shared__ uint8_t off_d[256];
-    __shared__ uint32_t words[kStageWords];
-    __shared__ int s_ok, s_last;
-    const int i = (int)blockIdx.x, k = (int)blockIdx.y, K = c.spec_k, t = (int)threadIdx.x;
-    const int slot = i * K + k;
-    if (t == 0) {
-        if (wait_v) ddm::flag_poll(c.spec_flags + 1, wait_v, timeouts);
-        int64_t cb = -1, pos = -1;
-        const ddm_ctl_part& p = c.parts[i];
-        const uint64_t f = c.first[i];
-        if (!(p.idle || p.done || p.stall || p.park) && f != ~0ull && p.Wg > 0) {
-            const int64_t cc = ((int64_t)f - p.base) / p.pb + k;
-            if (cc >= p.j && cc + 1 >= p.g0 && cc + 1 < min(p.b_end, p.n_full)) {
-                cb = cc;
-                pos = c.jobs[i].E[cc + 1 - p.g0] + 1;
-            }
-        }
-        s_c = cb;
-        s_pos = pos;
-        s_ok = 0;
-    }
-    __syncthreads();
-    const ddm_dfit_job& jb = c.spec_jobs[slot];
-    const ddm_stage_job& sj = c.stage[i];
-    const int64_t cb = s_c;
-    if (cb >= 0) {
-        const int L = sj.pb, F = sj.n_features;
-        for (int kk = t; kk < L; kk += kSpecThreads) off_d[kk] = sj.perm[sj.base + cb * sj.pb + kk];
-        for (int w = t; w < kStageWords; w += kSpecThreads) words[w] = sj.R[s_pos + w];
-        __syncthreads();
-        float* x = const_cast<float*>(jb.X);
-        int32_t* y = const_cast<int32_t*>(jb.y);
-        const int64_t row0 = cb * sj.pb;
-        for (int e = t; e < L * F; e += kSpecThreads) x[e] = sj.X[(int64_t)(e % F) * sj.ld + row0 + off_d[e / F]];
-        for (int kk = t; kk < L; kk += kSpecThreads) y[kk] = sj.y[row0 + off_d[kk]];
-        if (t < 64) {
-            // randint(2**31 - 1) x n_trees from the draw after batch c + 1's shuffle (stage_body)
-            const int lane = t;
-            int64_t* seeds = const_cast<int64_t*>(jb.seeds);
-            int q = 0, got = 0;
-            bool good = true;
-            while (got < jb.n_trees) {
-                if (q >= kStageWords) {
-                    good = false;
-                    break;
-                }
-                const int w = q + lane;
-                const uint32_t v = w < kStageWords ? (words[w] & 0x7fffffffu) : 0xffffffffu;
-                const bool acc = v <= 0x7ffffffeu;
-                const uint64_t b = __ballot(acc);
-                const int before = __popcll(b & ((1ull << lane) - 1ull));
-                if (acc && got + before < jb.n_trees) seeds[got + before] = (int64_t)v;
-                const int need = jb.n_trees - got, nb = __popcll(b);
-                if (nb >= need) {
-                    got = jb.n_trees;
-                } else {
-                    got += nb;
-                    q += 64;
-                }
-            }
-            if (lane == 0) s_ok = good ? 1 : 0;
-        }
-    }
-    __syncthreads();
-    if (t == 0) c.spec_gate[slot] = s_ok ? cb : -1;
-    // the last workgroup publishes (every workgroup's inputs and gate released before its ticket)
-    __threadfence();
-    __syncthreads();
-    if (t == 0) s_last = atomicAdd(c.spec_flags + 3, 1u) == gridDim.x * gridDim.y - 1;
-    __syncthreads();
-    if (s_last && t == 0) {
-        c.spec_flags[3] = 0;
-        ddm::flag_publish(c.spec_flags, pub_v);
-    }
-}
-
-// In k_stage_ctl: the change is in candidate batch d with the staging's own seeds: wait for
-// the candidates' refits, copy that candidate's forest into the partition's refit buffers
-// (as the epoch's own refit would have written it) and return 1 (the caller gates that
-// refit off).  Every thread calls it.
-__device__ int spec_take(const ddm_ctl& c, const Job& jb, int i, int64_t pos_next, uint32_t* timeouts) {
-    __shared__ int s_hit;
-    const int t = threadIdx.x, K = c.spec_k;
-    if (t == 0) {
-        s_hit = -1;
-        if (!(jb.stall && *jb.stall) && pos_next >= 0 && jb.info_out[6] == 1 && *jb.stop >= 0) {
-            const int64_t d = jb.j + *jb.stop;
-            for (int k = 0; k < K; ++k)
-                if (c.spec_gate[i * K + k] == d) {
-                    s_hit = i * K + k;
-                    break;
-                }
-            if (s_hit >= 0) ddm::flag_poll(c.spec_flags + 1, c.spec_v, timeouts);
-        }
-    }
-    __syncthreads();
-    const int slot = s_hit;
-    if (slot < 0) return 0;
-    const ddm_dfit_job& sp = c.spec_jobs[slot];
-    // the candidate drew the staging's seeds and refit without a status
-    const bool bad = (t < sp.n_trees && sp.seeds[t] != jb.seeds_out[t]) || (t == 0 && sp.result[DDM_DFIT_STATUS] != 0);
-    if (__syncthreads_or(bad)) return 0;
-    const ddm_ctl_part& p = c.parts[i];
-    const int64_t* r = sp.result;
-    const int64_t nodes = r[DDM_DFIT_NODES], K_cls = r[DDM_DFIT_CLASSES], blob = r[DDM_DFIT_BLOB];
-    const int64_t leaf = r[DDM_DFIT_PURE] ? 0 : r[DDM_DFIT_LEAF_ROWS] * K_cls;
-    const auto copy = [&](void* dst, const void* src, int64_t bytes) {
-        const int64_t n16 = bytes / 16;
-        for (int64_t e = t; e < n16; e += kStageThreads)
-            reinterpret_cast<uint4*>(dst)[e] = reinterpret_cast<const uint4*>(src)[e];
-        for (int64_t e = 16 * n16 + t; e < bytes; e += kStageThreads)
-            reinterpret_cast<uint8_t*>(dst)[e] = reinterpret_cast<const uint8_t*>(src)[e];
-    };
-    copy(const_cast<ddm_node*>(p.dnodes), sp.nodes, nodes * (int64_t)sizeof(ddm_node));
-    copy(const_cast<int32_t*>(p.droots), sp.roots, (int64_t)sp.n_trees * 4);
-    copy(const_cast<int32_t*>(p.dclasses), sp.classes, K_cls * 4);
-    if (leaf > 0) copy(const_cast<double*>(p.dleaf), sp.leaf_value, leaf * 8);
-    if (blob > 0) copy(const_cast<uint8_t*>(p.dblob), sp.blob, blob);
-    if (t < 12) const_cast<int64_t*>(p.res)[t] = r[t];
-    if (t == 0) atomicAdd(c.spec_flags + 2, 1u);
-    return 1;
-}
-
 // The one-lane DDM scan of the epoch's windows, when the fused kernel runs it (err set).
 struct FoldScan {
     const uint8_t* err;
@@ -618,15 +479,6 @@ __global__ __launch_bounds__(kStageThreads) void k_stage_ctl(const Job* __restri
             if (fs.pub) ddm::flag_publish(fs.pub, fs.pub_v);   // the fork (ctl.hip): every block's
         }                                                   // records are released before its ticket
     }
-    if (c.spec_k > 0 && fs.pub) {
-        // ABI 23: the forest of a speculative refit of the change's batch, when one ran.  After
-        // the decisions (commit reads the staging's info -- the refit goes through -- and this
-        // epoch's forest statistics) and after the fork (the next windows' shuffles need no
-        // forest); the epoch's own refit of this partition is then gated off
-        // (ddm_dfit_job.gate2 = info_out + 6 != 1)
-        __syncthreads();
-        if (spec_take(c, jb, i, s_next, fs.pub + 2) && t == 0) jb.info_out[6] = 2;
-    }
 #ifdef DDM_STAGE_PROFILE
     if (t == 0)
         printf("stage-ctl block %d scan+pick %.2f stage %.2f record %.2f ticket %.2f split %.2f us%s\n", i,
@@ -666,17 +518,6 @@ int epoch_stage_ctl_pub(const ddm_stage_job* jobs_dev, const ddm_shuffle_job* sh
     hipLaunchKernelGGL(k_stage_ctl, dim3((unsigned)ctl->n), dim3(kStageThreads), 0, ddm::as_hip(stream),
                        reinterpret_cast<const Job*>(jobs_dev), shuffle_jobs, *ctl, fs);
     return ddm::launch_status("ddm_epoch_stage_ctl");
-}
-
-// ABI 23: the speculative staging (ddm_ctl.spec_k > 0), every partition x candidate.
-int epoch_spec_stage(const ddm_ctl* ctl, uint32_t wait_v, uint32_t pub_v, uint32_t* timeouts, ddm_stream_t stream) {
-    if (!ctl || ctl->spec_k <= 0 || !ctl->spec_jobs || !ctl->spec_gate || !ctl->spec_flags || ctl->n <= 0) {
-        ddm::set_error("ddm_ctl_epochs: invalid speculative refit tables");
-        return DDM_E_ARG;
-    }
-    hipLaunchKernelGGL(k_spec_stage, dim3((unsigned)ctl->n, (unsigned)ctl->spec_k), dim3(kSpecThreads), 0,
-                       ddm::as_hip(stream), *ctl, wait_v, pub_v, timeouts);
-    return ddm::launch_status("ddm_ctl_epochs/spec stage");
 }
 
 extern "C" int ddm_epoch_stage(const ddm_stage_job* jobs_dev, int32_t n_jobs, ddm_stream_t stream) {

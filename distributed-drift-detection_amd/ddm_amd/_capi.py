@@ -12,7 +12,7 @@ import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 # DDM_AMD_LIB: an alternative build of the same library (e.g. an instrumented one)
 LIB_PATH = os.environ.get("DDM_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 23
+ABI_VERSION = 22
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
@@ -70,8 +70,7 @@ class DdmCtl(ctypes.Structure):
                 ("stage", _vp), ("off", _vp), ("end", _vp), ("state", _vp), ("first", _vp), ("stop", _vp),
                 ("pick", _vp), ("loff", _vp), ("lend", _vp), ("pstall", _vp), ("predict_blocks", _i64),
                 ("status", _vp), ("logs", _vp), ("log_b0", _vp), ("sync", _vp), ("decoupled", _i32),
-                ("long_ok", _i32), ("predict_clock", _vp), ("spec_jobs", _vp), ("spec_gate", _vp),
-                ("spec_flags", _vp), ("spec_k", _i32), ("spec_v", ctypes.c_uint32)]
+                ("long_ok", _i32), ("predict_clock", _vp)]
 
 
 class DdmCtlEpoch(ctypes.Structure):
@@ -82,7 +81,7 @@ class DdmCtlEpoch(ctypes.Structure):
                 ("long_max_rows", _i64), ("long_scratch", _vp), ("dfit_jobs", _vp), ("n_dfit", _i32),
                 ("max_trees", _i32), ("max_W", _i64), ("max_pieces", _i64), ("dfit_max_lf", _i64),
                 ("ev", _vp * 12), ("row_order_delta", _i64), ("decouple", _i32), ("pad_dc", _i32),
-                ("predict_evs", _vp), ("sync_flags", _vp), ("sync_seq", _vp), ("spec_stream", _vp)]
+                ("predict_evs", _vp), ("sync_flags", _vp), ("sync_seq", _vp)]
 
 # name -> (restype, argtypes); every symbol include/ddm_amd.h declares.
 SIGNATURES = {

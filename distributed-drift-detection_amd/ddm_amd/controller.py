@@ -179,14 +179,13 @@ class RunStats:
                  "scan_ms", "scan_rows", "shuffle_ms", "sklearn_refits", "refit_fit_s", "refit_readback_s",
                  "prep_s", "dfit_ms", "device_refits", "long_scans", "preshuffled", "device_epochs", "device_phases",
                  "permute_rows", "device_rows", "predict_dev_ms", "predict_dev_launches", "device_predict_bytes",
-                 "flag_recoveries", "spec_refits")
+                 "flag_recoveries")
 
     def __init__(self):
         self.epochs = self.refits = self.predicted_rows = self.predict_bytes = self.scan_rows = 0
         self.sklearn_refits = self.device_refits = self.long_scans = self.preshuffled = 0
         self.device_epochs = self.device_phases = self.permute_rows = self.device_rows = 0
         self.flag_recoveries = 0       # runs redone with event-ordered fork / join (devctl.FlagTimeout)
-        self.spec_refits = 0           # drifts whose forest came from a speculative refit (devctl.SPEC_K)
         self.predict_dev_ms, self.predict_dev_launches, self.device_predict_bytes = 0.0, 0, 0
         self.refit_s = self.gpu_s = self.host_s = self.predict_ms = self.scan_ms = self.shuffle_ms = 0.0
         self.refit_fit_s = self.refit_readback_s = self.prep_s = self.dfit_ms = 0.0

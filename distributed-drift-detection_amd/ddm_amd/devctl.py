@@ -49,11 +49,6 @@ CTL_GRAPH = os.environ.get("DDM_CTL_GRAPH", "0") not in ("", "0")
 # (ddm_ctl_epoch.sync_flags: a one-wave store / poll kernel pair, ~12 us per epoch) instead
 # of HIP events (~30 us); DDM_CTL_FLAGS=0: events
 CTL_FLAGS = os.environ.get("DDM_CTL_FLAGS", "1") not in ("", "0")
-# Speculative refits (ddm_ctl.spec_k, ABI 23): after every epoch's predict, the SPEC_K
-# batches from the window's first error batch on are staged as candidate changes and refit
-# on a third stream beside the scan and the staging; a change in a candidate batch takes
-# that forest, so its refit leaves the epoch's critical path.  With the flags only.
-SPEC_K = int(os.environ.get("DDM_SPEC_REFIT", "0"))
 
 
 class FlagTimeout(RuntimeError):
@@ -90,37 +85,6 @@ class PredictTimer:
 
     def close(self):
         pass
-
-
-class _SpecTables:
-    """The speculative refits' buffers (ddm_ctl.spec_*): per partition and candidate a
-    training batch, its seeds, a gate word, a refit job and its RefitBuffers; the flags and
-    the stream."""
-
-    def __init__(self, r, K):
-        n, dev, pb, T = len(r.parts), r.device, r.s.per_batch, r.s.n_estimators
-        self.K = K
-        self.bufs, recs = [], []
-        self.gate = torch.full((n * K,), -1, dtype=torch.int64, device=dev)
-        self.res = torch.zeros((n * K, dfit.RESULT_WORDS), dtype=torch.int64, device=dev)
-        self.flags = torch.zeros(4, dtype=torch.int32, device=dev)
-        self.flags_h = torch.zeros(4, dtype=torch.int32, pin_memory=True)
-        self.hits_seen = 0
-        F = max(b.F for b in r.dfit_bufs)
-        self.x = torch.zeros((n * K, pb * F), dtype=torch.float32, device=dev)
-        self.y = torch.zeros((n * K, pb), dtype=torch.int32, device=dev)
-        self.seeds = torch.zeros((n * K, T), dtype=torch.int64, device=dev)
-        for i in range(n):
-            rb = r.dfit_bufs[i]
-            for k in range(K):
-                s = i * K + k
-                b = dfit.RefitBuffers(rb.L, rb.F, rb.T, rb.k_cap, dev)
-                self.bufs.append(b)
-                recs.append(b.record(self.x[s].data_ptr(), self.y[s].data_ptr(), self.seeds[s].data_ptr(),
-                                     self.res[s].data_ptr(), gate=self.gate.data_ptr() + 8 * s, gate2=0, L=pb))
-        self.jobs_d = torch.from_numpy(np.array(recs, dtype=dfit.DFIT_DTYPE).view(np.uint8)).to(dev)
-        self.stream = torch.cuda.Stream(dev)
-        torch.cuda.synchronize(dev)
 
 
 class DeviceController:
@@ -163,10 +127,9 @@ class DeviceController:
         # fork / join numbers: published on the device, enqueued so far on the host (both
         # monotonic for the runner's life), and the device's count of waits that gave up
         self.sync_flags = torch.zeros(4, dtype=torch.int32, device=dev)
-        self.sync_seq = (ctypes.c_uint32 * 5)()
+        self.sync_seq = (ctypes.c_uint32 * 3)()
         self.sync_h = torch.zeros(4, dtype=torch.int32, pin_memory=True)
         self.flags_ok = True         # off for the runner's life after a FlagTimeout
-        self.spec = None             # the speculative refits' tables (SPEC_K > 0), built with E
         self._E = None
 
     # ---------------------------------------------------------------- eligibility
@@ -218,12 +181,6 @@ class DeviceController:
         E.max_pieces = 2 + 64 + r.shuffles[0].window_draws(mw) // 8192
         E.row_order_delta = self.err_rows.data_ptr() - r.err_all.data_ptr()
         E.decouple = 0
-        if SPEC_K > 0:
-            self.spec = _SpecTables(r, SPEC_K)
-            sp = self.spec
-            c.spec_jobs, c.spec_gate, c.spec_flags, c.spec_k = sp.jobs_d.data_ptr(), sp.gate.data_ptr(), \
-                sp.flags.data_ptr(), SPEC_K
-            E.spec_stream = sp.stream.cuda_stream
         self._E = E
         return E
 
@@ -417,8 +374,6 @@ class DeviceController:
         r._mark(f"device loop done ({epochs} epochs enqueued)")
         stream.synchronize()
         r.side_stream.synchronize()
-        if self.spec is not None:
-            self.spec.stream.synchronize()
         if pt is not None:
             ms, n = pt.take(stream)
             st.predict_dev_ms += ms
@@ -459,10 +414,8 @@ class DeviceController:
         give-up count start over should flags be turned back on)."""
         self.flags_ok = False
         self.sync_flags[:3].zero_()
-        for k in range(5):
+        for k in range(3):
             self.sync_seq[k] = 0
-        if self.spec is not None:
-            self.spec.flags.zero_()
         torch.cuda.synchronize(self.r.device)
 
     def close(self):
@@ -541,18 +494,12 @@ class DeviceController:
             r.ctrl_h.copy_(r.ctrl_d, non_blocking=True)        # staging slots and refit results
             r._mark("slab copy enqueued")
             self.sync_h.copy_(self.sync_flags, non_blocking=True)
-            if self.spec is not None:
-                self.spec.flags_h.copy_(self.spec.flags, non_blocking=True)
             r._mark("flags copy enqueued")
         r.stream.synchronize()
         r._mark("records copied")
         if int(self.sync_h[2]):
             raise FlagTimeout(f"{int(self.sync_h[2])} cross-stream flag waits of the device epochs gave up "
                               "(ddm_ctl_epoch.sync_flags): the phase's results are void")
-        if self.spec is not None:
-            hits = int(self.spec.flags_h[2])
-            st.spec_refits += hits - self.spec.hits_seen
-            self.spec.hits_seen = hits
         rec = self.rec
         epochs = int(rec["epochs"].max()) if len(rec) else 0
         # every partition's event log in one read-back

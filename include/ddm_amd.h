@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 23
+#define DDM_AMD_ABI_VERSION 22
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 256) */
@@ -662,26 +662,6 @@ typedef struct ddm_ctl {
                                                       shards), the staging kernel after it adds
                                                       max(end) - min(start) to [16] and 1 to
                                                       [17] and resets the shards              */
-    /* ABI 23: speculative refits (spec_k > 0; only with ddm_ctl_epoch.sync_flags).  After
-     * every epoch's predict, ddm_ctl_epochs enqueues on the epoch stream a staging of spec_k
-     * candidate changes per partition -- the batches c = fb .. fb + spec_k - 1 from the batch
-     * fb of the window's first error, each when batch c + 1 was shuffled by the window: batch
-     * c's rows in shuffled order and the tree seeds drawn after batch c + 1's shuffle, i.e.
-     * exactly what the staging gathers and draws if the change is in batch c
-     * (DDM_Process.py:207-210, :190, :102) -- into spec_jobs[i * spec_k + k] (its X, y and
-     * seeds buffers) with spec_gate[i * spec_k + k] = c (-1: no candidate), and the
-     * candidates' refits (ddm_rf_fit_device, gated by spec_gate) on spec_stream.  The staging
-     * kernel, finding the change in a candidate batch with the same seeds, waits for those
-     * refits and copies the candidate's forest into the partition's refit buffers (ddm_ctl_part
-     * dnodes ... res), and the epoch's own refit of that partition is gated off: the refit
-     * leaves the epoch's critical path.  spec_flags: device words [4], zeroed once: [0] / [1]
-     * the staging's / the refits' sequence numbers, [2] forests taken from a candidate,
-     * [3] the staging's block ticket (left 0).  spec_v: set by ddm_ctl_epochs. */
-    const ddm_dfit_job* spec_jobs;                 /* [n * spec_k] device table               */
-    int64_t* spec_gate;                            /* [n * spec_k]                            */
-    uint32_t* spec_flags;
-    int32_t spec_k;
-    uint32_t spec_v;
 } ddm_ctl;
 
 typedef struct ddm_ctl_epoch {
@@ -718,12 +698,7 @@ typedef struct ddm_ctl_epoch {
     uint32_t* sync_seq;                            /* ABI 21: host words [3], the fork / join
                                                       numbers enqueued so far and the last
                                                       join the epoch stream polled (advanced
-                                                      by ddm_ctl_epochs; zero with the flags);
-                                                      ABI 23: [5] with ctl.spec_k > 0, [3] / [4]
-                                                      the speculative staging's / refits'
-                                                      numbers                                  */
-    ddm_stream_t spec_stream;                      /* ABI 23: the speculative refits' stream
-                                                      (ctl.spec_k > 0)                         */
+                                                      by ddm_ctl_epochs; zero with the flags)  */
 } ddm_ctl_epoch;
 int64_t ddm_ctl_part_bytes(void);
 int64_t ddm_ctl_epoch_bytes(void);

@@ -178,35 +178,3 @@ def test_flag_timeout_voids_and_redoes_the_run(decouple, monkeypatch):
         assert np.array_equal(out[k], host_out[k]), k
     assert runner.stats.flag_recoveries == 1
     runner.close()
-
-
-@pytest.mark.parametrize("case", ["blocks", "jitter", "noise", "tails", "decoupled"])
-@pytest.mark.parametrize("K", [1, 2])
-def test_speculative_refits_equal_host_epochs(case, K, monkeypatch):
-    """Speculative refits (devctl.SPEC_K, ddm_ctl.spec_*): the candidates' forests taken by
-    the staging kernel are the refits the epoch would have run (same batch, same seeds), so
-    events, RNG positions and refit counts equal host epochs (DDM_Process.py:189-210), and
-    some drifts do take a candidate's forest."""
-    from ddm_amd import devctl
-    monkeypatch.setattr(devctl, "SPEC_K", K)
-    if case == "decoupled":
-        monkeypatch.setattr(devctl, "DECOUPLE_ROWS", 0)
-        parts = _parts((60_000,) * 4, 28, 20_011, 3)
-    elif case == "blocks":
-        parts = _parts((60_000,) * 4, 27, 20_011, 3)
-    elif case == "jitter":
-        parts = _parts((24_000,) * 4, 27, 0, 5, jitter=True)
-    elif case == "noise":
-        parts = _parts((30_000, 30_000), 27, 0, 7, flip=0.01, jitter=True)
-    else:
-        parts = _parts((24_037, 17_055, 4_321, 9_999), 27, 6_007, 9)
-    seeds = [300 + k for k in range(len(parts))]
-    dev_out, dev_rng, st = _run(parts, True, seeds)
-    host_out, host_rng, st_h = _run(parts, False, seeds)
-    assert st.device_epochs > 0 and st_h.device_epochs == 0
-    for k in range(len(parts)):
-        assert np.array_equal(dev_out[k], host_out[k]), k
-        assert np.array_equal(dev_rng[k][0], host_rng[k][0]) and dev_rng[k][1] == host_rng[k][1], k
-    assert st.refits == st_h.refits
-    assert st.flag_recoveries == 0
-    assert st.spec_refits > 0
