@@ -162,3 +162,48 @@ def test_prefix_tables_equal_direct_simulation(L):
     assert np.array_equal(got, want)
     tc = sh.Tchunk[:chunks * (L - 1)].cpu().numpy().view(np.uint32).reshape(chunks, L - 1)
     assert np.array_equal(tc, want[:, 63])
+
+
+@pytest.mark.parametrize("L", [100, 2, 7, 256])
+def test_window_batch_small_and_large_windows(L):
+    """ddm_shuffle_window_batch (the controller's batched window shuffles): windows of at most
+    16 batches go through the one-workgroup kernel, longer ones through first / walk /
+    replay / perms, in the same launch sequence; every partition's perm bytes and E equal
+    numpy's permutation stream (DDM_Process.py:187, :190)."""
+    import ctypes
+    from ddm_amd import kernels
+    from ddm_amd._capi import check, lib
+    dev = torch.device("cuda", 0)
+    Ws = [1, 5, 16, 17, 40, 3, 16, 300]
+    shs, hosts, outs, recs = [], [], [], []
+    for k, W in enumerate(Ws):
+        sh = _mk(L, cap=1 << 19, max_window=1024)
+        mt = MTStream.from_seed(500 + k)
+        mt.skip(17 * k)
+        host = mt.copy()
+        sh.reset(mt)
+        P = 0
+        if k % 2:                     # a window that does not start at draw 0
+            pre = np.zeros(3, dtype=np.int64)
+            host.perms(np.full(3, L, np.int32), draws=pre)
+            P = int(pre.sum())
+        sh.ensure(P + sh.window_draws(W))
+        out = torch.zeros(W * L, dtype=torch.uint8, device=dev)
+        rec = np.zeros(1, kernels.JOB_DTYPE)
+        sh.fill_job(rec[0], P, W, out.data_ptr())
+        shs.append(sh)
+        hosts.append((host, P))
+        outs.append(out)
+        recs.append(rec)
+    table = torch.from_numpy(np.concatenate(recs).view(np.uint8)).to(dev)
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream(dev)
+    check(lib.ddm_shuffle_window_batch(table.data_ptr(), len(Ws), max(Ws), 2 + 64 + 300 * L * 2 // 8192 + 2, L,
+                                       ctypes.c_void_p(s.cuda_stream), None, None), "ddm_shuffle_window_batch")
+    torch.cuda.synchronize()
+    for k, W in enumerate(Ws):
+        host, P = hosts[k]
+        draws = np.zeros(W, dtype=np.int64)
+        want = host.perms(np.full(W, L, np.int32), draws=draws)
+        assert np.array_equal(outs[k].cpu().numpy(), want), (k, W)
+        assert np.array_equal(shs[k].E[:W].cpu().numpy(), P + np.cumsum(draws) - 1), (k, W)
