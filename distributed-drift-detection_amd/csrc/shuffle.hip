@@ -423,14 +423,8 @@ __device__ void fsm_first(const Job& j, int L) {
 
 __global__ __launch_bounds__(kFirstThreads) void k_fsm_first(Job j, int L) { fsm_first(j, L); }
 
-#ifndef DDM_SMALL_WINDOW
-#define DDM_SMALL_WINDOW 16
-#endif
-constexpr int kSmallWindow = DDM_SMALL_WINDOW;   // k_shuffle_small_batch's windows (kSmallW); 0: none
-
 __global__ __launch_bounds__(kFirstThreads) void k_fsm_first_batch(const Job* __restrict__ jobs, int L) {
     const Job j = jobs[blockIdx.y];
-    if (j.W <= kSmallWindow) return;
     fsm_first(j, L);
 }
 
@@ -585,7 +579,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fsm_walk(Job j, int L) {
 
 __global__ __launch_bounds__(kWalkThreads) void k_fsm_walk_batch(const Job* __restrict__ jobs, int L) {
     const Job j = jobs[blockIdx.x];
-    if (j.W <= kSmallWindow) return;
+    if (j.W <= 0) return;
     fsm_walk(as_global(j.R), as_global((const uint16_t*)j.first), as_global(j.Tchunk), j.P, j.W, L, j.avail,
              as_global(reinterpret_cast<ChunkStart*>(j.pieces)), as_global(j.info));
 }
@@ -757,7 +751,7 @@ __global__ __launch_bounds__(64) void k_fsm_replay(Job j, int L) {
 
 __global__ __launch_bounds__(64) void k_fsm_replay_batch(const Job* __restrict__ jobs, int L) {
     const Job j = jobs[blockIdx.y];
-    if (j.W <= kSmallWindow) return;
+    if (j.W <= 0) return;
     fsm_replay<true>(as_global(j.R), as_global(j.Tpre), as_global(reinterpret_cast<const ChunkStart*>(j.pieces)),
                      as_global((const int64_t*)j.info), j.W, L, as_global(j.J), as_global(j.E), as_global(j.perm_out),
                      blockIdx.x, gridDim.x);
@@ -788,7 +782,6 @@ __global__ __launch_bounds__(256) void k_fsm_perms(Job j, int L) {
 
 __global__ __launch_bounds__(256) void k_fsm_perms_batch(const Job* __restrict__ jobs, int L) {
     const Job j = jobs[blockIdx.y];
-    if (j.W <= kSmallWindow) return;
     for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < j.W; b0 += (int64_t)gridDim.x * 256)
         fsm_perms(as_global((const uint8_t*)j.J), j.W, L, as_global(j.perm_out), b0);
 }
@@ -805,106 +798,6 @@ __global__ void k_pick_batch(const Job* __restrict__ jobs, int n) {
     if (!j.pick_out) return;
     const int64_t k = (j.stop && j.stop[0] >= 0 ? (int64_t)j.stop[0] : j.pick_last) - j.pick_offset;
     j.pick_out[0] = (j.W > 0 && k >= 0 && k < j.W) ? j.E[k] : -1;
-}
-
-// Windows of at most kSmallW batches in ONE workgroup instead of first / walk / replay /
-// perms (whose fixed grids and four launches are the whole cost of a few-batch window:
-// C5's windows are ~6 batches).  Wave 0 runs the window's Fisher-Yates intervals batch after
-// batch from the stream words (stage_body's speculative interval draws: lane l tries interval
-// i - l on word k + l, the lanes before the first rejection are final, the rejected interval
-// searches on by a ballot over 64 words at a time), recording every interval's j and E[b]
-// (the draw that completes batch b); then every thread of the workgroup follows one
-// (batch, element) pair through its batch's transpositions, and the window's perm bytes go
-// out contiguously.  The other four kernels skip these windows.
-constexpr int kSmallW = kSmallWindow;
-static_assert(kSmallW <= 64, "k_shuffle_small_batch: LDS rows per window batch");
-constexpr int kSmallThreads = 256;
-constexpr int kSmallWords = 1024;      // stream words in LDS (refilled as the window consumes them)
-
-__device__ __forceinline__ void small_fill(gptr<const uint32_t> R, int64_t base, uint32_t* words, int lane) {
-#pragma unroll 4
-    for (int w = lane; w < kSmallWords; w += 64) words[w] = R[base + w];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__global__ __launch_bounds__(kSmallThreads) void k_shuffle_small_batch(const Job* __restrict__ jobs, int L) {
-    const Job j = jobs[blockIdx.x];
-    if (j.W <= 0 || j.W > kSmallW) return;
-    __shared__ uint32_t words[kSmallWords];
-    __shared__ uint8_t js[kSmallW > 0 ? kSmallW : 1][256];
-    __shared__ uint8_t pl[kSmallW > 0 ? kSmallW : 1][256];
-    const int t = threadIdx.x, S = L - 1;
-    const int W = (int)j.W;
-    const gptr<const uint32_t> R = as_global(j.R);
-    if (t < 64) {
-        const int lane = t;
-        int64_t base = j.P;            // words[k] = R[base + k]
-        int k = 0;
-        small_fill(R, base, words, lane);
-        // the window's words run out of the LDS copy: continue from the current draw
-        const auto refill = [&]() {
-            if (k + 64 > kSmallWords) {
-                base += k;
-                k = 0;
-                small_fill(R, base, words, lane);
-            }
-        };
-        for (int b = 0; b < W; ++b) {
-            int i = S;
-            while (i >= 1) {
-                refill();
-                const int il = i - lane;
-                bool acc = false;
-                uint32_t val = 0xffffffffu;
-                if (il >= 1) {
-                    const uint32_t mask = 0xffffffffu >> __builtin_clz((uint32_t)il);
-                    val = words[k + lane] & mask;
-                    acc = val <= (uint32_t)il;
-                }
-                const uint64_t rej = __ballot(!acc);     // lane i (il = 0) always counts
-                const int r = rej ? __builtin_ctzll(rej) : 64;
-                if (lane < r) js[b][il] = (uint8_t)val;
-                i -= r;
-                k += r;
-                if (i < 1 || r == 64) continue;
-                // interval i rejected word k: its first accepted word after it
-                const uint32_t mask = 0xffffffffu >> __builtin_clz((uint32_t)i);
-                ++k;
-                for (;;) {
-                    refill();
-                    const uint32_t v = words[k + lane] & mask;
-                    const uint64_t bb = __ballot(v <= (uint32_t)i);
-                    if (bb) {
-                        const int f = __builtin_ctzll(bb);
-                        const int jv = __builtin_amdgcn_readlane((int)v, f);   // f is wave-uniform
-                        k += f + 1;
-                        if (lane == 0) js[b][i] = (uint8_t)jv;
-                        --i;
-                        break;
-                    }
-                    k += 64;
-                }
-            }
-            if (lane == 0) j.E[b] = base + k - 1;   // the draw of interval 1: the batch's last
-        }
-    }
-    __syncthreads();
-    // element e of batch b starts at e and follows the transpositions i <-> js[b][i],
-    // i = L-1 .. 1; it ends where Fisher-Yates puts it
-    for (int x = t; x < W * L; x += kSmallThreads) {
-        const int b = x / L, e = x - b * L;
-        int q = e;
-        for (int i = S; i >= 1; --i) {
-            const int jv = js[b][i];
-            q = q == i ? jv : (q == jv ? i : q);
-        }
-        pl[b][q] = (uint8_t)e;
-    }
-    __syncthreads();
-    const gptr<uint8_t> dst = as_global(j.perm_out);
-    for (int x = t; x < W * L; x += kSmallThreads) dst[x] = pl[x / L][x % L];
 }
 
 size_t walk_lds_bytes(int L) {
@@ -940,8 +833,6 @@ extern "C" int ddm_shuffle_window_batch(const ddm_shuffle_job* jobs_dev, int32_t
     const Job* jobs = reinterpret_cast<const Job*>(jobs_dev);
     if (ev_begin)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s), "event record")) return rc;
-    hipLaunchKernelGGL(k_shuffle_small_batch, dim3((unsigned)n_jobs), dim3(kSmallThreads), 0, s, jobs, (int)batch_len);
-    if (int rc = ddm::launch_status("ddm_shuffle_window_batch/small")) return rc;
     hipLaunchKernelGGL(k_fsm_first_batch, dim3(kSubPerChunk - 1, (unsigned)n_jobs), dim3(kFirstThreads), 0, s, jobs,
                        (int)batch_len);
     if (int rc = ddm::launch_status("ddm_shuffle_window_batch/first")) return rc;
