@@ -277,7 +277,10 @@ class DeviceController:
             if rec["done"][i] or rec["stall"][i] or rec["park"][i]:
                 continue
             sh = r.shuffles[i]
-            win = int(min(r.max_wins[i], max(1, int(rec["win"][i])) << (2 * GROUP)))
+            # the windows of the next groups, but never past the partition's last batch (the
+            # draws beyond it would be generated at the end of the run and waited for)
+            win = int(min(r.max_wins[i], max(1, int(rec["win"][i])) << (2 * GROUP),
+                          max(1, r.nbs[i] - int(rec["j"][i]))))
             need = int(rec["P"][i]) + sh.window_draws(win) + r.n_words + 8 * CHUNK
             need = min(need, sh.cap - 2 * CHUNK)
             if int(rec["P"][i]) + sh.window_draws(1) + r.n_words + 4 * CHUNK > sh.cap - 2 * CHUNK:
