@@ -35,7 +35,8 @@ from ._capi import DDM_STOP_FAILED, DdmEpoch, check, lib
 from .forest import upload_forests
 from .params import OUTPUT_COLUMNS, DDMSettings, infer_x_features
 from .rng import MTStream
-from .shuffle import CHUNK, GpuShuffle, expected_draws_per_batch, fy_from_words, perm_seeds_from_words, untemper_state
+from .shuffle import (CHUNK, GpuShuffle, expected_draws_per_batch, fy_from_words, perm_seeds_from_words,
+                      untemper_keys)
 from .trainer import BatchForestTrainer
 
 # A window runs on ddm_scan_long when its carried detector is neither fresh nor trivial
@@ -923,14 +924,17 @@ class BatchRunner:
             if need:
                 for ps, start, _ in need:
                     self.shuffles[ps.i].ensure(start + 624)
-                buf = torch.empty((len(need), 624), dtype=torch.int32, pin_memory=True)
+                if getattr(self, "_st_buf", None) is None or self._st_buf.shape[0] < len(need):
+                    self._st_buf = torch.empty((len(self.parts), 624), dtype=torch.int32, pin_memory=True)
+                buf = self._st_buf[:len(need)]     # free: the last run's copy into it has completed
                 with torch.cuda.stream(self.stream):
-                    for k, (ps, start, _) in enumerate(need):
-                        buf[k].copy_(self.shuffles[ps.i].R[start:start + 624], non_blocking=True)
+                    # the windows of every stream gathered on the device: one copy back
+                    buf.copy_(torch.stack([self.shuffles[ps.i].R[start:start + 624] for ps, start, _ in need]),
+                              non_blocking=True)
                 self.stream.synchronize()
-                words = buf.numpy().view(np.uint32)
+                keys = untemper_keys(buf.numpy().view(np.uint32))
                 for k, (ps, _, pos) in enumerate(need):
-                    states[ps.i] = untemper_state(words[k], pos)
+                    states[ps.i] = ("MT19937", keys[k], int(pos), 0, 0.0)
             for ps in started:
                 ns = states[ps.i]
                 rngs[ps.i].key[:] = ns[1]
@@ -965,8 +969,10 @@ class BatchRunner:
             if r is None:                        # rejections ran past the head read-back
                 return False
             plans.append((ps, ps.P + r[2], ps.P + r[2] + r[3]))
+        self._mark("start: seeds drawn")
         n, stream = len(pss), self.stream
         t = self._stream_ptrs(pss)
+        self._mark("start: stream pointers")
         rec = t["stage"][[ps.i for ps in pss]]
         rec["j"], rec["g0"], rec["b_end"] = 0, 1, 1
         rec["p_after_first"] = [ps.P for ps in pss]          # the draw after batch 0's shuffle
@@ -978,8 +984,19 @@ class BatchRunner:
         rec["max_events"], rec["log"], rec["plan_out"], rec["next_job"] = 0, 0, 0, 0
         self.stage_jobs.rec[:n] = rec
         self.dfit_jobs.rec[:n] = self._templates()["dfit"][[ps.i for ps in pss]]
-        for ps in pss:
-            self._upload_perm(ps.i, 0, np.asarray(ps.train_rows, dtype=np.uint8), 0)
+        self._mark("start: records")
+        # batch 0's shuffle of every partition: one host->device copy and one scatter into
+        # the partitions' perm arrays (eight separate copies took ~0.5 ms of the run start)
+        key = tuple(ps.i for ps in pss)
+        if getattr(self, "_p0", None) is None or self._p0[0] != key:
+            idx = np.concatenate([self.bases[i] + np.arange(pb, dtype=np.int64) for i in key])
+            self._p0 = (key, torch.empty((n, pb), dtype=torch.uint8, pin_memory=True),
+                        torch.from_numpy(idx).to(self.device))
+        _, p0_h, p0_idx = self._p0
+        p0_h.numpy()[:] = np.stack([np.asarray(ps.train_rows, dtype=np.uint8) for ps in pss])
+        with torch.cuda.stream(stream):
+            self.perm_all.index_copy_(0, p0_idx, p0_h.view(-1).to(self.device, non_blocking=True))
+        self._mark("start: batch-0 perms uploaded")
         with torch.cuda.stream(stream):
             # the whole host half of the slab, as a host epoch uploads it: the device copy
             # must hold every static table field (the next-window jobs' stream pointers,
@@ -987,6 +1004,7 @@ class BatchRunner:
             # (ctrl_d -> ctrl_h) when it ends
             self.ctrl_d[:self.o_stage].copy_(self.ctrl_h[:self.o_stage], non_blocking=True)
             self.ctrl_d[self.o_stop:self.o_stop + 4 * len(self.parts)].zero_()   # a change in batch 0
+        self._mark("start: slab uploaded")
         kernels.epoch_stage(self.stage_jobs, n, stream, upload=False)
         dfit.fit_device(self.dfit_jobs.d, n, T, stream, self._E.dfit_max_lf)
         for ps, P1, P2 in plans:

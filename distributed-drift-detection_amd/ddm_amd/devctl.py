@@ -301,6 +301,7 @@ class DeviceController:
         # nothing of the host path may still be in flight: the last epoch's refits are read
         # by the device predict itself
         stream.synchronize()
+        r._mark("phase: stream synchronised")
         r._pending_sync = False
         r._pending_forests = []
         E = self._epoch_struct()
@@ -332,12 +333,15 @@ class DeviceController:
         # enqueued (~0.9 ms of host time the first epochs no longer wait for: their windows
         # are planned within the words already tabulated)
         self._write_records(live)
+        r._mark("phase: records written")
         with torch.cuda.stream(stream):
             self.pstall.zero_()
             self.parts_d.copy_(self.parts_h, non_blocking=True)
             r.dfit_jobs.d[:self.n * dfit.DFIT_DTYPE.itemsize].copy_(
                 r.dfit_jobs.h[:self.n * dfit.DFIT_DTYPE.itemsize], non_blocking=True)
+        r._mark("phase: records uploaded")
         self._publish_avail()
+        r._mark("phase: coverage published")
         E.decouple = self._decouple([(ps.win, r.max_wins[ps.i]) for ps in live])
         check(lib.ddm_ctl_enter(ctypes.byref(E)), "ddm_ctl_enter")
         r._mark("device phase entered")

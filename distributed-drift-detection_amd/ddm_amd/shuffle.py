@@ -47,6 +47,11 @@ def _untemper(y):
     return (u & 0xffffffff).astype(np.uint32)
 
 
+def untemper_keys(words):
+    """_untemper over rows of 624 tempered words at once ([n, 624] -> [n, 624] keys)."""
+    return _untemper(np.asarray(words, dtype=np.uint32))
+
+
 def untemper_state(words, pos):
     """numpy's ('MT19937', key, pos) from 624 tempered stream words."""
     return ("MT19937", _untemper(words), int(pos), 0, 0.0)
