@@ -118,16 +118,20 @@ def parse():
                          "by the staging kernel after it); -1: on for c3/c3w, off for the latency-bound c2/c5 "
                          "epochs (a few us of each ~120-us C5 epoch), whose kernel times then come from an "
                          "instrumented step after the timed ones")
-    ap.add_argument("--predict-replays", type=int, default=0,
-                    help="isolated back-to-back replays of the last timed step's predict tables (a side figure; "
-                         "0 for PMC runs, whose rows must be the steps' own)")
+    ap.add_argument("--predict-replays", type=int, default=-1,
+                    help="isolated back-to-back replays of the instrumented step's predict tables, reported as "
+                         "roofline.isolated_replay next to the in-step frac (a side figure; 0 for PMC runs, whose "
+                         "rows must be the steps' own); -1: 2 for c3 / c3w, 0 otherwise")
     ap.add_argument("--gc", default="on", choices=["on", "freeze", "off"],
                     help="Python's cyclic garbage collector during the timed steps: on, frozen after setup "
                          "(gc.freeze: the setup's objects leave the collected generations), or off")
     ap.add_argument("--solo-world", type=int, default=0,
-                    help="measurement aid: run only rank 0's partitions of an N-GPU job (d % N == 0), one "
+                    help="measurement aid: run only rank 0's partitions of an N-GPU job (d %% N == 0), one "
                          "process, no collective (the per-GPU share of the strong-scaling workloads)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.predict_replays < 0:
+        a.predict_replays = 2 if a.workload in ("c3", "c3w") else 0
+    return a
 
 
 def dist_env():
