@@ -232,33 +232,53 @@ constexpr int kClsWords = kClsLoads * 64 / 4;   // the LDS bit image in u64 word
 // A fill's geometry: the first item (wave-uniform, 64-bit) and each lane's batch from it
 // in 32-bit offsets (w stream boundaries lie between them).
 struct FillGeo {
-    int64_t base, a0, f0, s0;
+    int64_t base, a0, f0, s0, j0;
     int ln, w, o, blen, nch;
     bool valid;
 };
 
-__device__ __forceinline__ FillGeo fill_geo(int64_t f, int64_t n_items, int64_t L, int64_t nb, int64_t nbp, int pb,
-                                            int delta, double inv_nb, int lane) {
+// The geometry of the fill whose first item is `base` = batch j0 of stream s0 (wave-uniform):
+// per lane, 32-bit arithmetic only (the batch's stream offset w by a float reciprocal and one
+// correction) while nb < 2^24 -- the general form's 64-bit products and fp64 conversions
+// were a measurable part of the classify pass's VALU work, which bounds it.
+__device__ __forceinline__ FillGeo fill_geo_at(int64_t base, int64_t s0, int64_t j0, int64_t n_items, int64_t L,
+                                               int64_t nb, int64_t nbp, int pb, int delta, double inv_nb, int lane) {
     FillGeo g;
-    g.base = f << 6;
-    g.s0 = item_stream(g.base, nb, inv_nb);
-    const int64_t j0 = g.base - g.s0 * nb;
-    const int64_t b0 = g.s0 * L + j0 * pb;            // the fill's first row
+    g.base = base;
+    g.s0 = s0;
+    g.j0 = j0;
+    const int64_t b0 = s0 * L + j0 * pb;            // the fill's first row
     g.a0 = b0 & ~(int64_t)15;
-    g.f0 = g.s0 * nbp + j0;
-    const int last = (int)min((int64_t)63, n_items - 1 - g.base);
+    g.f0 = s0 * nbp + j0;
+    const int last = (int)min((int64_t)63, n_items - 1 - base);
     g.valid = lane <= last;
     g.ln = min(lane, last);                          // lanes past the end repeat the last item
-    const int jl = (int)j0 + g.ln;
-    int w = (int)((double)jl * inv_nb);
-    if ((int64_t)w * nb > jl) --w;
-    else if ((int64_t)(w + 1) * nb <= jl) ++w;
+    int w, j;
+    if (nb < (1 << 24)) {                            // wave-uniform
+        const int nbi = (int)nb, jl = (int)j0 + g.ln;
+        w = (int)((float)jl * (float)inv_nb);
+        if (w * nbi > jl) --w;
+        else if ((w + 1) * nbi <= jl) ++w;
+        j = jl - w * nbi;
+    } else {
+        const int64_t jl = j0 + g.ln;
+        w = (int)((double)jl * inv_nb);
+        if ((int64_t)w * nb > jl) --w;
+        else if ((int64_t)(w + 1) * nb <= jl) ++w;
+        j = (int)(jl - (int64_t)w * nb);
+    }
     g.w = w;
-    const int j = jl - w * (int)nb;
     g.o = (int)(b0 - g.a0) + g.ln * pb - w * delta;  // the batch's first row - a0
-    g.blen = min(pb, (int)L - j * pb);
+    g.blen = min(pb, (int)L - j * pb);               // L < 2^31 (ddm_scan_batches checks)
     g.nch = __builtin_amdgcn_readfirstlane((__shfl(g.o + g.blen, 63, 64) + 15) >> 4);
     return g;
+}
+
+__device__ __forceinline__ FillGeo fill_geo(int64_t f, int64_t n_items, int64_t L, int64_t nb, int64_t nbp, int pb,
+                                            int delta, double inv_nb, int lane) {
+    const int64_t base = f << 6;
+    const int64_t s0 = item_stream(base, nb, inv_nb);
+    return fill_geo_at(base, s0, base - s0 * nb, n_items, L, nb, nbp, pb, delta, inv_nb, lane);
 }
 
 // The fill's chunks, one coalesced 16-byte load per k, issued back to back (chunks past the
@@ -292,6 +312,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
     // HBM reads back to merge -- 0.12 B/row of extra fetches and 0.1 B/row of extra writes.)
     __shared__ int2 ring_ev[kClsThreads / 64][kRing][64];
     __shared__ uint8_t ring_fl[kClsThreads / 64][kRing][64];
+    __shared__ int64_t ring_sj[kClsThreads / 64][kRing][2];   // the slot's fill: s0, j0
     __shared__ double rcp[kBatchRcp];
     for (int k = threadIdx.x; k < kBatchRcp; k += kClsThreads) rcp[k] = 1.0 / (double)(k > 0 ? k : 1);
     __syncthreads();
@@ -421,8 +442,9 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
     // a ring slot's fill to HBM: its 64 event records (whole lines) and flag bytes
     const auto flush = [&](int64_t fit) {
         const int64_t ff = wave + fit * n_waves;
-        const FillGeo fg = fill_geo(ff, n_items, L, nb, nbp, pb, delta, inv_nb, lane);
         const int sl = (int)(fit % kRing);
+        const FillGeo fg = fill_geo_at(ff << 6, ring_sj[wv][sl][0], ring_sj[wv][sl][1], n_items, L, nb, nbp, pb, delta,
+                                       inv_nb, lane);
         if (fg.valid) {
             ev[fg.base + fg.ln] = ring_ev[wv][sl][lane];
             flags[fg.f0 + fg.ln + fg.w * (int)(nbp - nb)] = ring_fl[wv][sl][lane];
@@ -431,6 +453,8 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
     // software pipeline: the next fill's loads are issued before this fill's decisions
     // and stores, so every wave keeps a fill in flight
     FillGeo g = fill_geo(wave, n_items, L, nb, nbp, pb, delta, inv_nb, lane);
+    // the next fill's first item, stream and batch advance by a constant step (wave-uniform)
+    const int64_t dstep = n_waves << 6, ds = dstep / nb, dj = dstep - ds * nb;
     uint4 v[kLoads];
     if (wave < nfill) fill_load<kLoads>(err, g, lane, v);
     for (int64_t f = wave; f < nfill; f += n_waves) {
@@ -477,7 +501,17 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
         const double4 ppt = pst[pix];
         // C: the next fill's loads (the last iteration reloads its own fill)
         const int64_t fn = f + n_waves;
-        const FillGeo gn = fill_geo(min(fn, nfill - 1), n_items, L, nb, nbp, pb, delta, inv_nb, lane);
+        FillGeo gn;
+        if (fn < nfill) {
+            int64_t sn = g.s0 + ds, jn = g.j0 + dj;
+            if (jn >= nb) {
+                jn -= nb;
+                ++sn;
+            }
+            gn = fill_geo_at(fn << 6, sn, jn, n_items, L, nb, nbp, pb, delta, inv_nb, lane);
+        } else {
+            gn = fill_geo(nfill - 1, n_items, L, nb, nbp, pb, delta, inv_nb, lane);
+        }
         fill_load<kLoads>(err, gn, lane, v);
         // D: decisions and stores
         bool exact = false;
@@ -512,6 +546,11 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
             const int sl = (int)(iter % kRing);
             ring_ev[wv][sl][lane] = make_int2(wp, cp);
             ring_fl[wv][sl][lane] = fl;
+        }
+        if (lane == 0) {
+            const int sl = (int)(iter % kRing);
+            ring_sj[wv][sl][0] = g.s0;
+            ring_sj[wv][sl][1] = g.j0;
         }
         start(ppt);
         uint64_t xm = __ballot(exact);
