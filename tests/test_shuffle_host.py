@@ -44,3 +44,19 @@ def test_word_level_fisher_yates_and_seeds():
 
 def test_expected_draws():
     assert abs(expected_draws_per_batch(100) - 141.3) < 0.2
+
+
+def test_untemper_keys_rows_equal_per_stream_states():
+    """The run end's one-pass read-back (BatchRunner._run: every stream's final 624-word window
+    untempered at once) equals numpy's state of each stream, as untemper_state gives it."""
+    from ddm_amd.shuffle import untemper_keys, untemper_state
+    rows, keys = [], []
+    for seed in (3, 4, 5):
+        mt = MTStream.from_seed(seed)
+        keys.append(mt.key.copy())
+        rows.append(_temper(mt.key))
+    words = np.stack(rows)
+    got = untemper_keys(words)
+    for k in range(3):
+        assert np.array_equal(got[k], keys[k])
+        assert np.array_equal(untemper_state(words[k], 624)[1], keys[k])
