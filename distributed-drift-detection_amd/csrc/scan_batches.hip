@@ -496,7 +496,6 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
         const bool pre = g.valid && !triv && use_pre && blen >= kPre;
         const uint32_t ix = (uint32_t)(m0 & (uint64_t)(kPreN - 1));
         const uint32_t inf = ptab[ix];
-        const double4 pt = pst[ix];
         const uint32_t pix = steps > 0 ? pop() : 0u;
         const double4 ppt = pst[pix];
         // C: the next fill's loads (the last iteration reloads its own fill)
@@ -570,7 +569,11 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
             xm = __ballot(exact);
         }
         if (exact) {
-            // the detector after the prefix rows (no change there) when the batch is longer
+            // the detector after the prefix rows (no change there) when the batch is longer;
+            // its prefix state is loaded only here (the LDS queue's batches look it up at the
+            // pop): an unconditional 32-byte load per batch was 1.3 GB of L2 reads per C4 call
+            // for the few batches that overflow to the global queue
+            const double4 pt = pst[ix];
             QEntry e;
             e.m0 = m0;
             e.m1 = m1;
