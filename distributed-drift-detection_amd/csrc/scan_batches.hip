@@ -489,13 +489,15 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
         // B: fresh + two zero rows = trivial state (n = 3): its first error row is the change
         // (p + s > 0 = p_min + cl * s_min) and zeros raise nothing.  Otherwise the prefix
         // table (and the detector after it, for the exact rows) is looked up now.
-        // Both loads below are issued unconditionally, before the prefetch, so their uses wait
-        // only for them (a popped state loaded under a branch measured 0.5% slower; the pop's
-        // lanes mostly share one address).
+        // Both loads below are issued before the prefetch, so their uses wait only for them.
+        // The table entry is read by the lanes that use it (scattered 4-byte reads; 1.3 %
+        // faster than all 64 lanes); the popped state by every lane (mostly one shared
+        // address; under a branch it measured 0.5 % slower).
         const bool triv = shortcuts && blen >= 2 && (m0 & 3ull) == 0;
         const bool pre = g.valid && !triv && use_pre && blen >= kPre;
         const uint32_t ix = (uint32_t)(m0 & (uint64_t)(kPreN - 1));
-        const uint32_t inf = ptab[ix];
+        uint32_t inf = 0u;
+        if (pre) inf = ptab[ix];
         const uint32_t pix = steps > 0 ? pop() : 0u;
         const double4 ppt = pst[pix];
         // C: the next fill's loads (the last iteration reloads its own fill)
