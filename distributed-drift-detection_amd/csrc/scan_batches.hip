@@ -294,6 +294,22 @@ __device__ __forceinline__ void fill_load(const uint8_t* __restrict__ err, const
     }
 }
 
+// The classify pass's per-wave LDS: the fill's bit image, the LDS queue of batches needing
+// exact rows and the ring of the last kRing fills' events and flag bytes, stored to HBM whole
+// when a fill leaves the ring: by then the batches the pass steps exactly have (nearly all)
+// finished, so every 512-byte event row goes out as full lines.  (Stored as decided, the rows
+// had a hole per exact batch and each exact result was a lone 8-byte store: partial lines,
+// which HBM reads back to merge -- 0.12 B/row of extra fetches and 0.1 B/row of extra writes.)
+struct ClsWaveLds {
+    uint64_t img[kClsWords + 2];
+    uint64_t lq_m0[kLQ], lq_m1[kLQ];
+    int64_t lq_it[kLQ];
+    int2 ring_ev[kRing][64];
+    int64_t ring_sj[kRing][2];   // the slot's fill: s0, j0
+    int32_t lq_hdr[kLQ];
+    uint8_t ring_fl[kRing][64];
+};
+
 template <bool kPmap, int kLoads>
 __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kClsWavesPerEU))) void k_scan_batches_classify(
     const uint8_t* __restrict__ err, int64_t n_items, int64_t L, int64_t nb, int64_t nbp, ddm_params P,
@@ -301,18 +317,9 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
     uint32_t* __restrict__ need, bool use_pre, const uint16_t* __restrict__ ptab, const double4* __restrict__ pst,
     QEntry* __restrict__ q, uint32_t* __restrict__ qcnt, int64_t* __restrict__ q1, uint32_t* __restrict__ q1cnt,
     double2* __restrict__ pend, int steps, int pop_min) {
-    __shared__ uint64_t img[kClsThreads / 64][kClsWords + 2];
-    __shared__ uint64_t lq_m0[kClsThreads / 64][kLQ], lq_m1[kClsThreads / 64][kLQ];
-    __shared__ int64_t lq_it[kClsThreads / 64][kLQ];
-    __shared__ int32_t lq_hdr[kClsThreads / 64][kLQ];
-    // the events and flag bytes of the wave's last kRing fills, stored to HBM whole when a fill
-    // leaves the ring: by then the batches the pass steps exactly have (nearly all) finished,
-    // so every 512-byte event row goes out as full lines.  (Stored as decided, the rows had a
-    // hole per exact batch and each exact result was a lone 8-byte store: partial lines, which
-    // HBM reads back to merge -- 0.12 B/row of extra fetches and 0.1 B/row of extra writes.)
-    __shared__ int2 ring_ev[kClsThreads / 64][kRing][64];
-    __shared__ uint8_t ring_fl[kClsThreads / 64][kRing][64];
-    __shared__ int64_t ring_sj[kClsThreads / 64][kRing][2];   // the slot's fill: s0, j0
+    // one struct per wave: a single LDS base (and immediate offsets) for all of them -- as
+    // separate arrays each had its own base, which the compiler spilled (a v_readlane each)
+    __shared__ ClsWaveLds wlds[kClsThreads / 64];
     __shared__ double rcp[kBatchRcp];
     for (int k = threadIdx.x; k < kBatchRcp; k += kClsThreads) rcp[k] = 1.0 / (double)(k > 0 ? k : 1);
     __syncthreads();
@@ -322,12 +329,13 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
     const bool shortcuts = min_inst == 3;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    ClsWaveLds& W = wlds[wv];
     const uint64_t below = (1ull << lane) - 1;
     const int64_t wave = (int64_t)blockIdx.x * (kClsThreads / 64) + wv;
     const int64_t n_waves = (int64_t)gridDim.x * (kClsThreads / 64);
     const int64_t nfill = (n_items + 63) >> 6;
     int64_t iter = 0;                                   // this wave's fill count (wave-uniform)
-    uint16_t* const img16 = reinterpret_cast<uint16_t*>(img[wv]);
+    uint16_t* const img16 = reinterpret_cast<uint16_t*>(W.img);
     QEntry* const wq = q + wave * qcap;
     const double inv_nb = 1.0 / (double)nb;
     const int delta = (int)(nb * pb - L);            // rows missing from a stream's last batch
@@ -386,8 +394,8 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
                 const int64_t fit = ((eit >> 6) - wave) / n_waves;
                 if (fit > iter - kRing) {
                     const int sl = (int)(fit % kRing);
-                    ring_ev[wv][sl][eit & 63] = make_int2(w, c);
-                    ring_fl[wv][sl][eit & 63] = fl;
+                    W.ring_ev[sl][eit & 63] = make_int2(w, c);
+                    W.ring_fl[sl][eit & 63] = fl;
                 } else {
                     ev[eit] = make_int2(w, c);
                     flags[es * nbp + ej] = fl;
@@ -410,10 +418,10 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
             const uint32_t rank = (uint32_t)__popcll(idle_m & below);
             if (!busy && rank < take) {
                 const uint32_t sl = (lq_head + rank) & (kLQ - 1);
-                em0 = lq_m0[wv][sl];
-                em1 = lq_m1[wv][sl];
-                eit = lq_it[wv][sl];
-                ehdr = lq_hdr[wv][sl];
+                em0 = W.lq_m0[sl];
+                em1 = W.lq_m1[sl];
+                eit = W.lq_it[sl];
+                ehdr = W.lq_hdr[sl];
                 popping = true;
                 ix = (uint32_t)(em0 & (uint64_t)(kPreN - 1));
             }
@@ -443,11 +451,11 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
     const auto flush = [&](int64_t fit) {
         const int64_t ff = wave + fit * n_waves;
         const int sl = (int)(fit % kRing);
-        const FillGeo fg = fill_geo_at(ff << 6, ring_sj[wv][sl][0], ring_sj[wv][sl][1], n_items, L, nb, nbp, pb, delta,
+        const FillGeo fg = fill_geo_at(ff << 6, W.ring_sj[sl][0], W.ring_sj[sl][1], n_items, L, nb, nbp, pb, delta,
                                        inv_nb, lane);
         if (fg.valid) {
-            ev[fg.base + fg.ln] = ring_ev[wv][sl][lane];
-            flags[fg.f0 + fg.ln + fg.w * (int)(nbp - nb)] = ring_fl[wv][sl][lane];
+            ev[fg.base + fg.ln] = W.ring_ev[sl][lane];
+            flags[fg.f0 + fg.ln + fg.w * (int)(nbp - nb)] = W.ring_fl[sl][lane];
         }
     };
     // software pipeline: the next fill's loads are issued before this fill's decisions
@@ -475,7 +483,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
         for (int k = 0; k < kLoads; ++k) img16[k * 64 + lane] = (uint16_t)fold16(v[k]);
         wave_sync_lds();
         const int wo = g.o >> 6, sh = g.o & 63;
-        const uint64_t x0 = img[wv][wo], x1 = img[wv][wo + 1], x2 = img[wv][wo + 2];
+        const uint64_t x0 = W.img[wo], x1 = W.img[wo + 1], x2 = W.img[wo + 2];
         wave_sync_lds();
         uint64_t m0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
         uint64_t m1 = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
@@ -545,13 +553,13 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
             // into the ring (an exact batch's slot is written when it finishes, or by
             // k_scan_batches_exact<0> after the pass when it overflows to the global queue)
             const int sl = (int)(iter % kRing);
-            ring_ev[wv][sl][lane] = make_int2(wp, cp);
-            ring_fl[wv][sl][lane] = fl;
+            W.ring_ev[sl][lane] = make_int2(wp, cp);
+            W.ring_fl[sl][lane] = fl;
         }
         if (lane == 0) {
             const int sl = (int)(iter % kRing);
-            ring_sj[wv][sl][0] = g.s0;
-            ring_sj[wv][sl][1] = g.j0;
+            W.ring_sj[sl][0] = g.s0;
+            W.ring_sj[sl][1] = g.j0;
         }
         start(ppt);
         uint64_t xm = __ballot(exact);
@@ -561,10 +569,10 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
             const uint32_t r = (uint32_t)__popcll(xm & below);
             if (exact && r < room) {
                 const uint32_t sl = (lq_head + lq_count + r) & (kLQ - 1);
-                lq_m0[wv][sl] = m0;
-                lq_m1[wv][sl] = m1;
-                lq_it[wv][sl] = g.base + g.ln;
-                lq_hdr[wv][sl] = (pre && blen > kPre) ? ((wp + 1) | (kPre << 8)) : 0;
+                W.lq_m0[sl] = m0;
+                W.lq_m1[sl] = m1;
+                W.lq_it[sl] = g.base + g.ln;
+                W.lq_hdr[sl] = (pre && blen > kPre) ? ((wp + 1) | (kPre << 8)) : 0;
                 exact = false;
             }
             lq_count += min((uint32_t)__popcll(xm), room);
