@@ -1018,8 +1018,11 @@ struct FixEntry {
 #define DDM_WALK_THREADS 256
 #endif
 constexpr int kWalkThreads = DDM_WALK_THREADS;
+#ifndef DDM_WALK_WAVES
+#define DDM_WALK_WAVES 4
+#endif
 
-__global__ __launch_bounds__(kWalkThreads) void k_scan_batches_walk(
+__global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(DDM_WALK_WAVES))) void k_scan_batches_walk(
     int64_t n_streams, int64_t L, int64_t nb, int64_t nbp, ddm_params P, ddm_state* __restrict__ state,
     int2* __restrict__ ev, const uint8_t* __restrict__ flags, int64_t* __restrict__ nev_out,
     const uint8_t* __restrict__ pmap, const uint32_t* __restrict__ need, uint32_t* __restrict__ ctr,
