@@ -455,7 +455,9 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
                                        inv_nb, lane);
         if (fg.valid) {
             ev[fg.base + fg.ln] = W.ring_ev[sl][lane];
+#if !(defined(DDM_TUNING) && defined(DDM_PROBE_NO_FLAGS))   // timing probe only: results wrong
             flags[fg.f0 + fg.ln + fg.w * (int)(nbp - nb)] = W.ring_fl[sl][lane];
+#endif
         }
     };
     // software pipeline: the next fill's loads are issued before this fill's decisions
