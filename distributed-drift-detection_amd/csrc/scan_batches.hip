@@ -502,7 +502,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
         // Both loads below are issued before the prefetch, so their uses wait only for them.
         // The table entry is read by the lanes that use it (scattered 4-byte reads; 1.3 %
         // faster than all 64 lanes); the popped state by every lane (mostly one shared
-        // address; under a branch it measured 0.5 % slower).
+        // address; under a per-lane or a wave-uniform branch it measured 0.5-0.6 % slower).
         const bool triv = shortcuts && blen >= 2 && (m0 & 3ull) == 0;
         const bool pre = g.valid && !triv && use_pre && blen >= kPre;
         const uint32_t ix = (uint32_t)(m0 & (uint64_t)(kPreN - 1));
