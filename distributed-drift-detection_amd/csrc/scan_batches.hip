@@ -30,6 +30,7 @@ namespace {
 constexpr int kMaxBatch = 128;
 constexpr int kBatchRcp = 2 * kMaxBatch + 2;   // n <= 2 * 128 + 1 in a level-1 rescan
 
+// phase: fold
 // bit k set <=> byte k of w is nonzero
 __device__ __forceinline__ uint32_t nz4(uint32_t w) {
     const uint32_t t = (((w & 0x7f7f7f7fu) + 0x7f7f7f7fu) | w) & 0x80808080u;
@@ -55,6 +56,7 @@ __device__ __forceinline__ uint32_t fold16(uint4 v) {
     return lo | (hi << 8);
 }
 
+// phase: other
 // 128-bit nonzero mask of the rows [bstart, bstart + blen), blen in 1..128, by nine
 // 16-byte loads of this lane (the scattered form: level-1 rescans and the fix-up).
 __device__ __forceinline__ void batch_mask(const uint8_t* __restrict__ err, int64_t bstart, int blen, uint64_t& m0,
@@ -82,6 +84,7 @@ __device__ __forceinline__ void batch_mask(const uint8_t* __restrict__ err, int6
     }
 }
 
+// phase: decide
 __device__ __forceinline__ int mask_bit(uint64_t m0, uint64_t m1, int i) {
     return (int)((i < 64 ? m0 >> i : m1 >> (i - 64)) & 1ull);
 }
@@ -98,6 +101,7 @@ __device__ __forceinline__ int mask_next(uint64_t m0, uint64_t m1, int i) {
     return t ? 64 + __builtin_ctzll(t) : 128;
 }
 
+// phase: step_rows
 struct SmallDet {          // a detector inside one or two batches: n <= 2 * kMaxBatch + 1
     double p, s, pmin, smin, psmin;
     int n;
@@ -135,6 +139,7 @@ __device__ __forceinline__ int small_add(SmallDet& d, int x, int min_inst, doubl
     return small_test(d, p, s, min_inst, wl, cl);
 }
 
+// phase: other
 // Prefix table: a fresh detector's first kPre rows depend only on their kPre error bits.
 // Entry m (bit t = row t is an error): ptab[m] = (first warning row + 1) | (change row + 1)
 // << 5 inside the prefix (0 = none), and, without a change, pst[m] = the detector after
@@ -178,6 +183,7 @@ __device__ __forceinline__ bool state_fresh(const ddm_state& st) {
 // is that row; bit 4: row 1), else the change is the batch's first error row, as the fresh
 // speculation found.  Level-1 flag bytes (flags1): bit 0 change, bit 1 event, bit 2 end
 // state stored (pend1).
+// phase: decide
 constexpr uint8_t kFlagLead01 = 8, kFlagLeadRow1 = 16, kFlagNoError = 32;
 
 __device__ __forceinline__ uint8_t lead_bits(uint64_t m0, uint64_t m1) {
@@ -186,6 +192,7 @@ __device__ __forceinline__ uint8_t lead_bits(uint64_t m0, uint64_t m1) {
     return 0;
 }
 
+// phase: item_stream
 // item -> (stream, batch in stream): a float quotient corrected by one
 __device__ __forceinline__ int64_t item_stream(int64_t it, int64_t nb, double inv_nb) {
     int64_t s = (int64_t)((double)it * inv_nb);
@@ -194,6 +201,7 @@ __device__ __forceinline__ int64_t item_stream(int64_t it, int64_t nb, double in
     return s;
 }
 
+// phase: sync
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -237,6 +245,7 @@ struct FillGeo {
     bool valid;
 };
 
+// phase: geometry
 // The geometry of the fill whose first item is `base` = batch j0 of stream s0 (wave-uniform):
 // per lane, 32-bit arithmetic only (the batch's stream offset w by a float reciprocal and one
 // correction) while nb < 2^24 -- the general form's 64-bit products and fp64 conversions
@@ -281,6 +290,7 @@ __device__ __forceinline__ FillGeo fill_geo(int64_t f, int64_t n_items, int64_t 
     return fill_geo_at(base, s0, base - s0 * nb, n_items, L, nb, nbp, pb, delta, inv_nb, lane);
 }
 
+// phase: loads
 // The fill's chunks, one coalesced 16-byte load per k, issued back to back (chunks past the
 // fill repeat its last one: no branch between them).
 template <int kLoads, bool kNt = true>
@@ -317,6 +327,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
     uint32_t* __restrict__ need, bool use_pre, const uint16_t* __restrict__ ptab, const double4* __restrict__ pst,
     QEntry* __restrict__ q, uint32_t* __restrict__ qcnt, int64_t* __restrict__ q1, uint32_t* __restrict__ q1cnt,
     double2* __restrict__ pend, int steps, int pop_min) {
+    // phase: prologue
     // one struct per wave: a single LDS base (and immediate offsets) for all of them -- as
     // separate arrays each had its own base, which the compiler spilled (a v_readlane each)
     __shared__ ClsWaveLds wlds[kClsThreads / 64];
@@ -350,6 +361,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
     int ei = 0, eblen = 0, ewp = -1, ehdr = 0;
     uint64_t em0 = 0, em1 = 0;
     int64_t eit = 0;
+    // phase: step_rows
     const auto step_rows = [&]() {
         // two exact rows of this lane's batch (as k_scan_batches_exact); a finished batch
         // writes its result
@@ -370,6 +382,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
                 if (r == 1 && ewp < 0) ewp = ei;
                 ++ei;
             }
+            // phase: step_finish
             if (r == 2 || ei >= eblen) {
                 const bool chg = r == 2;
                 const int64_t es = item_stream(eit, nb, inv_nb);
@@ -403,10 +416,12 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
                 busy = false;
             }
         }
+        // phase: step_rows
         const uint64_t qm = __ballot(enq);
         if (enq) wq1[nq + __popcll(qm & below)] = eit;
         nq += (uint32_t)__popcll(qm);
     };
+    // phase: pop
     // idle lanes take queued batches (lane order); returns the prefix-table index to look up
     const auto pop = [&]() -> uint32_t {
         popping = false;
@@ -430,6 +445,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
         }
         return ix;
     };
+    // phase: start
     // a popped batch's starting detector (after the prefix rows when hdr says so)
     const auto start = [&](const double4& t) {
         if (popping) {
@@ -447,6 +463,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
             eblen = (int)min((int64_t)pb, L - (eit - es * nb) * pb);
         }
     };
+    // phase: flush
     // a ring slot's fill to HBM: its 64 event records (whole lines) and flag bytes
     const auto flush = [&](int64_t fit) {
         const int64_t ff = wave + fit * n_waves;
@@ -460,6 +477,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
 #endif
         }
     };
+    // phase: prologue
     // software pipeline: the next fill's loads are issued before this fill's decisions
     // and stores, so every wave keeps a fill in flight
     FillGeo g = fill_geo(wave, n_items, L, nb, nbp, pb, delta, inv_nb, lane);
@@ -468,6 +486,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
     uint4 v[kLoads];
     if (wave < nfill) fill_load<kLoads>(err, g, lane, v);
     for (int64_t f = wave; f < nfill; f += n_waves) {
+        // phase: fold
         // A: the fill's bytes -> the LDS bit image -> this lane's 128 row bits
         uint32_t odd = 0;
 #pragma unroll
@@ -484,6 +503,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
 #pragma unroll
         for (int k = 0; k < kLoads; ++k) img16[k * 64 + lane] = (uint16_t)fold16(v[k]);
         wave_sync_lds();
+        // phase: cut
         const int wo = g.o >> 6, sh = g.o & 63;
         const uint64_t x0 = W.img[wo], x1 = W.img[wo + 1], x2 = W.img[wo + 2];
         wave_sync_lds();
@@ -496,6 +516,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
         } else if (blen < 128) {
             m1 &= (1ull << (blen - 64)) - 1;
         }
+        // phase: decide
         // B: fresh + two zero rows = trivial state (n = 3): its first error row is the change
         // (p + s > 0 = p_min + cl * s_min) and zeros raise nothing.  Otherwise the prefix
         // table (and the detector after it, for the exact rows) is looked up now.
@@ -508,8 +529,10 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
         const uint32_t ix = (uint32_t)(m0 & (uint64_t)(kPreN - 1));
         uint32_t inf = 0u;
         if (pre) inf = ptab[ix];
+        // phase: pop
         const uint32_t pix = steps > 0 ? pop() : 0u;
         const double4 ppt = pst[pix];
+        // phase: geometry
         // C: the next fill's loads (the last iteration reloads its own fill)
         const int64_t fn = f + n_waves;
         FillGeo gn;
@@ -524,6 +547,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
             gn = fill_geo(nfill - 1, n_items, L, nb, nbp, pb, delta, inv_nb, lane);
         }
         fill_load<kLoads>(err, gn, lane, v);
+        // phase: decide
         // D: decisions and stores
         bool exact = false;
         int wp = -1, cp = -1;
@@ -552,6 +576,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
                     if (cp >= 0) cp = pmap[g.a0 + g.o + cp];
                 }
             }
+            // phase: ring
             // into the ring (an exact batch's slot is written when it finishes, or by
             // k_scan_batches_exact<0> after the pass when it overflows to the global queue)
             const int sl = (int)(iter % kRing);
@@ -563,7 +588,9 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
             W.ring_sj[sl][0] = g.s0;
             W.ring_sj[sl][1] = g.j0;
         }
+        // phase: start
         start(ppt);
+        // phase: queue
         uint64_t xm = __ballot(exact);
         if (steps > 0 && xm) {
             // into the LDS queue while it has room (the prefix state is looked up at the pop)
@@ -600,11 +627,13 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
             wq[count + __popcll(xm & below)] = e;
         }
         count += (uint32_t)__popcll(xm);
+        // phase: step_rows
         // E: exact rows of the queued batches
         for (int k = 0; k < steps; ++k) {
             if (__ballot(busy) == 0ull) break;
             step_rows();
         }
+        // phase: flush
         g = gn;
         ++iter;
         if (iter >= kRing) {                            // the slot the next fill takes
@@ -612,6 +641,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
             flush(iter - kRing);
         }
     }
+    // phase: drain
     // drain the LDS queue (finished batches still land in the ring), then the ring
     if (steps > 0) {
         for (;;) {
@@ -629,6 +659,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
     }
 }
 
+// phase: other
 #ifdef DDM_TUNING
 // Timing probe (DDM_SCAN_PROBE=1, tuning builds only; results are NOT the scan's): the classify pass's reads,
 // LDS image and bit extraction with one 8-byte store per batch and nothing else, to price

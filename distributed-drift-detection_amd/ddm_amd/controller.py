@@ -76,7 +76,10 @@ EARLY_PIECES = int(os.environ.get("DDM_EARLY_PIECES", "1"))
 # The side stream (the next windows' shuffles, beside the refits and the next predict) on
 # every SIDE_CU_STRIDE-th CU only (ddm_stream_create_cu_stride; 1: all CUs): its fused replay
 # holds ~17 KB of LDS per one-wave workgroup, so on every CU it left no room for the
-# predict's workgroups, which then ran at 0.50 of HBM instead of 0.71.
+# predict's workgroups, which then ran at 0.50 of HBM instead of 0.71.  Note for reading the
+# A/B in profiles/r05/refit: a CU-masked stream (hipExtStreamCreateWithCUMask) is a blocking
+# stream at normal priority, while the stream it replaces is a non-blocking torch stream at
+# priority -1, so stride > 1 changes the mask, the priority and the null-stream sync at once.
 SIDE_CU_STRIDE = int(os.environ.get("DDM_SIDE_CU_STRIDE", "1"))
 
 
@@ -780,6 +783,7 @@ class BatchRunner:
         if len(rngs) != len(self.parts):
             raise ValueError("one MT19937 stream per partition")
         snaps = [r.snapshot() for r in rngs]
+        stats0 = {k: getattr(self.stats, k) for k in RunStats.__slots__}
         try:
             return self._run(rngs)
         except FlagTimeout as e:
@@ -788,8 +792,12 @@ class BatchRunner:
             self._mark(f"flag timeout: {e}; run redone with event-ordered fork / join")
             for r, snap in zip(rngs, snaps):
                 r.restore(snap)
+            # the voided attempt's counts are dropped: the redo counts its own
+            recoveries = self.stats.flag_recoveries + 1
+            for k, v in stats0.items():
+                setattr(self.stats, k, v)
             self.devctl.flags_off()
-            self.stats.flag_recoveries += 1
+            self.stats.flag_recoveries = recoveries
             return self._run(rngs)
 
     def _run(self, rngs):

@@ -393,7 +393,7 @@ class DeviceController:
             st.scan_ms += s_ms
             st.dfit_ms += f_ms
             st.shuffle_ms += sh_ms
-        out = self._take_back(live)
+        out = self._take_back(live, flags)
         r._mark("records taken back")
         return out
 
@@ -418,8 +418,10 @@ class DeviceController:
 
     def flags_off(self):
         """After a FlagTimeout: fork / join by HIP events from now on (the numbers and the
-        give-up count start over should flags be turned back on)."""
+        give-up count start over should flags be turned back on).  Every stream is drained
+        first: a fork poll still queued on the side stream must not see the zeroed numbers."""
         self.flags_ok = False
+        torch.cuda.synchronize(self.r.device)
         self.sync_flags[:3].zero_()
         for k in range(3):
             self.sync_seq[k] = 0
@@ -492,8 +494,9 @@ class DeviceController:
                                              ctypes.c_void_p(stream.cuda_stream), None, None),
                   "ddm_forest_predict_dev")
 
-    def _take_back(self, live):
-        """Device records -> the partitions' host state (and their events)."""
+    def _take_back(self, live, flags=True):
+        """Device records -> the partitions' host state (and their events).  `flags`: the
+        phase forked / joined by device flags, so their give-up count is read."""
         r, st, pb = self.r, self.r.stats, self.r.s.per_batch
         with torch.cuda.stream(r.stream):
             self.parts_h.copy_(self.parts_d, non_blocking=True)
@@ -504,7 +507,7 @@ class DeviceController:
             r._mark("flags copy enqueued")
         r.stream.synchronize()
         r._mark("records copied")
-        if int(self.sync_h[2]):
+        if flags and int(self.sync_h[2]):
             raise FlagTimeout(f"{int(self.sync_h[2])} cross-stream flag waits of the device epochs gave up "
                               "(ddm_ctl_epoch.sync_flags): the phase's results are void")
         rec = self.rec

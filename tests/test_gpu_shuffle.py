@@ -166,10 +166,10 @@ def test_prefix_tables_equal_direct_simulation(L):
 
 @pytest.mark.parametrize("L", [100, 2, 7, 256])
 def test_window_batch_small_and_large_windows(L):
-    """ddm_shuffle_window_batch (the controller's batched window shuffles): windows of at most
-    16 batches go through the one-workgroup kernel, longer ones through first / walk /
-    replay / perms, in the same launch sequence; every partition's perm bytes and E equal
-    numpy's permutation stream (DDM_Process.py:187, :190)."""
+    """ddm_shuffle_window_batch (the controller's batched window shuffles): short and long
+    windows in one call, every one through the first / walk / replay / perms kernels; every
+    partition's perm bytes and E equal numpy's permutation stream (DDM_Process.py:187,
+    :190)."""
     import ctypes
     from ddm_amd import kernels
     from ddm_amd._capi import check, lib
