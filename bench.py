@@ -629,8 +629,7 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
              "device_allocs_in_timed_steps": timed_allocs,
              "kernel_ms_from": "one instrumented step after the timed ones (HIP events around each launch)",
              "gather_ms_per_step": gather_s[0] / args.steps * 1e3 if world > 1 else None,
-             "gather_backend": (None if world == 1 else "rccl (ctypes ncclAllGather, HBM to HBM)" if args.comm
-                                else "torch.distributed all_gather"),
+             "gather_backend": args.gather_backend,
              "checks": checks}
     dec_frac = agg["permute_rows"] / max(1, agg["device_rows"])
     kname = "k_cforest_predict_dev" if dec_frac < 0.5 else "k_cforest_predict_dev (row order)"
@@ -694,6 +693,14 @@ def c2_fixture_check(mult, instances, c2parts, results):
     if not os.path.exists(path):
         return None
     cfg = np.load(path, allow_pickle=False)
+    # the stream itself first: its row order (the fixture's order, or for the published
+    # cell the sha1 of its 2,048,000 int32 entries) == the one this run built
+    order = outdoor_stream(mult, instances)[1].astype(np.int32)
+    if "order_sha1" in cfg.files:
+        if hashlib.sha1(np.ascontiguousarray(order).tobytes()).hexdigest() != str(cfg["order_sha1"]):
+            raise RuntimeError(f"c2 stream order differs from the reference fixture {os.path.basename(path)}")
+    elif not np.array_equal(order, cfg["order"]):
+        raise RuntimeError(f"c2 stream order differs from the reference fixture {os.path.basename(path)}")
     for d, r in results.items():
         rn = c2parts[d].row_number
         ev = np.full((len(r), 4), -1, dtype=np.int64)
@@ -704,7 +711,9 @@ def c2_fixture_check(mult, instances, c2parts, results):
         want = cfg[f"events/{d}"]
         if not np.array_equal(ev, want):
             raise RuntimeError(f"c2 partition {d}: events differ from the reference fixture {os.path.basename(path)}")
-    return f"all {len(results)} partitions == tests/golden/{os.path.basename(path)} (reference-executed)"
+    n_ev = sum(len(r) for r in results.values())
+    return (f"all {len(results)} partitions ({n_ev} batch records, every event) and the stream order == "
+            f"tests/golden/{os.path.basename(path)} (reference-executed)")
 
 
 def run_c1(args, world, rank, dev, torch, dist, cpu):
@@ -856,7 +865,7 @@ def run_c4(args, world, rank, dev, torch, dist, cpu):
     alg = S * L * 1.0 + S * nb * 8
     achieved = alg / (avg_ms * 1e-3) / 1e9
     cpu_res = None
-    if rank == 0 and world == 1 and args.cpu_baseline:
+    if rank == 0 and args.cpu_baseline:
         from oracle.ddm import scan_stream
         e = err[:2000 * L].cpu().numpy()
         t = time.perf_counter()
@@ -956,6 +965,35 @@ def keep_freed_outputs_in_heap():
     return ok and libc.mallopt(M_TRIM_THRESHOLD, 1 << 30) == 1
 
 
+def bench_line(args, world, rows_total, elapsed, info, extra, roofline, cpu_res, scaling):
+    """The driver's JSON line (rank 0): whole-job rows/s over the max-over-ranks time.  At
+    N > 1 it carries the same roofline (rank 0's own launches) and CPU baseline (rank 0's
+    pool) as at N = 1 and names the collect's backend; a line missing one of them is refused."""
+    value = rows_total / elapsed
+    pub = published_cell(args.workload, args)
+    out = {"metric": "stream rows/sec through predict+DDM (node, 1/2/4/8 GPU) + % HBM roofline",
+           "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+           "scaling": scaling, "vs_baseline": value / pub[0] if pub else None,
+           "vs_baseline_basis": pub[1] if pub else "no published reference number for this workload (the "
+                                                   "reference publishes outdoorStream only: --workload c2)",
+           "dtype": "f64",
+           "data": ("the reference's outdoorStream.csv (parsed, tests/golden/outdoor.npz), resident in HBM "
+                    "before the timed region" if args.workload == "c2" else
+                    "synthetic (rialto.csv not shipped), generated before the timed region"),
+           "config": dict(info, parallelism=f"partitions over {world} GPU(s), partition d on GPU d % {world}, "
+                                            f"no data-path collective"),
+           "roofline": roofline, "cpu_baseline": cpu_res, "breakdown": extra}
+    if world > 1 and args.workload != "c4":
+        out["gather_backend"] = extra.get("gather_backend")
+    missing = [k for k in ("roofline", "cpu_baseline") if out[k] is None and (k != "cpu_baseline" or args.cpu_baseline)]
+    if world > 1 and args.workload != "c4" and not out.get("gather_backend"):
+        missing.append("gather_backend")
+    if missing:
+        raise RuntimeError(f"bench.py: the N={world} line lacks {missing}")
+    return out
+
+
 def main():
     args = parse()
     keep_freed_outputs_in_heap()
@@ -972,7 +1010,9 @@ def main():
     if args.workload == "c1":
         c1_stream()
     cpu = None
-    if args.cpu_baseline and rank == 0 and world == 1 and args.workload in ("c1", "c2", "c3", "c3w", "c5"):
+    # rank 0's CPU baseline at every N: its pool forks here, before any HIP call, and runs
+    # after the timed region while the other ranks wait at the timing reduction
+    if args.cpu_baseline and rank == 0 and args.workload in ("c1", "c2", "c3", "c3w", "c5"):
         procs = {"c1": 1, "c2": min(args.cpu_procs, args.c2_instances)}.get(args.workload, args.cpu_procs)
         cpu = CpuBaseline(procs, args.cpu_cores)              # forked before any HIP call
     import torch
@@ -983,19 +1023,23 @@ def main():
     dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     comm = None
+    args.gather_backend = None
     if world > 1:
+        # ONE GPU communicator per rank: torch.distributed runs on gloo (host memory: the
+        # rendezvous, the barriers and the max-over-ranks timing), and the event collect on
+        # RCCL itself (ctypes ncclCommInitRank / ncclAllGather, its id through gloo's store)
+        dist.init_process_group("gloo")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-            # the event collect runs on RCCL itself (ctypes), torch.distributed only for the
-            # rendezvous, the barrier and the timing reduction
             try:
                 from ddm_amd.rccl import RcclComm
                 comm = RcclComm.from_default_group(dev)
-            except Exception as e:      # noqa: BLE001  (reported in the JSON line)
-                print(f"rank {rank}: RCCL ctypes communicator unavailable ({e}); gathering over torch.distributed",
+                args.gather_backend = "rccl (ctypes ncclAllGather, HBM to HBM over xGMI)"
+            except Exception as e:      # noqa: BLE001  (reported in the JSON line, loudly)
+                args.gather_backend = f"gloo (host all_gather): the RCCL communicator failed to initialise: {e}"
+                print(f"rank {rank}: RCCL communicator failed ({e}); the events are gathered over gloo",
                       file=sys.stderr)
         else:
-            dist.init_process_group(backend)
+            args.gather_backend = f"{backend} (torch.distributed all_gather, host memory: a rehearsal)"
     args.comm = comm
     if args.workload == "c1":
         res = run_c1(args, world, rank, dev, torch, dist, cpu if rank == 0 and args.cpu_baseline else None)
@@ -1005,31 +1049,16 @@ def main():
         res = run_partition_workload(args, world, rank, dev, torch, dist, args.workload, cpu)
     rows_rank, elapsed, info, extra, roofline, cpu_res, scaling = res
     if world > 1:
-        rdev = dev if backend == "nccl" else torch.device("cpu")
-        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        r = torch.tensor([rows_rank], dtype=torch.float64, device=rdev)
+        r = torch.tensor([rows_rank], dtype=torch.float64)
         dist.all_reduce(r)
         rows_total = float(r.item())
     else:
         rows_total = float(rows_rank)
     if rank == 0:
-        value = rows_total / elapsed
-        pub = published_cell(args.workload, args)
-        out = {"metric": "stream rows/sec through predict+DDM (node, 1/2/4/8 GPU) + % HBM roofline",
-               "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
-               "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-               "scaling": scaling, "vs_baseline": value / pub[0] if pub else None,
-               "vs_baseline_basis": pub[1] if pub else "no published reference number for this workload (the "
-                                                       "reference publishes outdoorStream only: --workload c2)",
-               "dtype": "f64",
-               "data": ("the reference's outdoorStream.csv (parsed, tests/golden/outdoor.npz), resident in HBM "
-                        "before the timed region" if args.workload == "c2" else
-                        "synthetic (rialto.csv not shipped), generated before the timed region"),
-               "config": dict(info, parallelism=f"partitions over {world} GPU(s), partition d on GPU d % {world}, "
-                                                f"no data-path collective"),
-               "roofline": roofline, "cpu_baseline": cpu_res, "breakdown": extra}
+        out = bench_line(args, world, rows_total, elapsed, info, extra, roofline, cpu_res, scaling)
         if args.workload == "c3" and args.companion and world == 1 and not args.solo_world:
             out["companion"] = {"c2_published_cell": companion_c2(args, rank, dev, torch, dist)}
         print(json.dumps(out), flush=True)

@@ -241,7 +241,7 @@ constexpr int kClsWords = kClsLoads * 64 / 4;   // the LDS bit image in u64 word
 // in 32-bit offsets (w stream boundaries lie between them).
 struct FillGeo {
     int64_t base, a0, f0, s0, j0;
-    int ln, w, o, blen, nch;
+    int ln, w, j, o, blen, nch;
     bool valid;
 };
 
@@ -277,6 +277,7 @@ __device__ __forceinline__ FillGeo fill_geo_at(int64_t base, int64_t s0, int64_t
         j = (int)(jl - (int64_t)w * nb);
     }
     g.w = w;
+    g.j = j;
     g.o = (int)(b0 - g.a0) + g.ln * pb - w * delta;  // the batch's first row - a0
     g.blen = min(pb, (int)L - j * pb);               // L < 2^31 (ddm_scan_batches checks)
     g.nch = __builtin_amdgcn_readfirstlane((__shfl(g.o + g.blen, 63, 64) + 15) >> 4);
@@ -304,6 +305,25 @@ __device__ __forceinline__ void fill_load(const uint8_t* __restrict__ err, const
     }
 }
 
+// The same chunks through a buffer descriptor over the fill's bytes (wave-uniform base and
+// size): the lane offset is one constant VGPR and the chunk offset a scalar, so the loads
+// take no VALU address work; chunks past the fill are out of the descriptor's range and read
+// as zeros without a memory access.  Non-temporal (aux 2: nt).
+template <int kLoads>
+__device__ __forceinline__ void fill_load_buf(const uint8_t* __restrict__ err, const FillGeo& g, int lane,
+                                              uint4 (&v)[kLoads]) {
+    const uint64_t a = reinterpret_cast<uint64_t>(err) + (uint64_t)g.a0;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const int nbytes = __builtin_amdgcn_readfirstlane(g.nch * 16);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, nbytes, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < kLoads; ++k) {
+        const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, k * 1024, 2);
+        v[k] = make_uint4(t.x, t.y, t.z, t.w);
+    }
+}
+
 // The classify pass's per-wave LDS: the fill's bit image, the LDS queue of batches needing
 // exact rows and the ring of the last kRing fills' events and flag bytes, stored to HBM whole
 // when a fill leaves the ring: by then the batches the pass steps exactly have (nearly all)
@@ -313,10 +333,10 @@ __device__ __forceinline__ void fill_load(const uint8_t* __restrict__ err, const
 struct ClsWaveLds {
     uint64_t img[kClsWords + 2];
     uint64_t lq_m0[kLQ], lq_m1[kLQ];
-    int64_t lq_it[kLQ];
+    int2 lq_sj[kLQ];             // the batch's stream and its batch in the stream
     int2 ring_ev[kRing][64];
-    int64_t ring_sj[kRing][2];   // the slot's fill: s0, j0
-    int32_t lq_hdr[kLQ];
+    int64_t ring_f0[kRing];      // the slot's fill: its first batch's flag-byte index
+    uint32_t lq_hdr[kLQ];
     uint8_t ring_fl[kRing][64];
 };
 
@@ -358,14 +378,22 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
     bool busy = false, popping = false;
     SmallDet d;
     small_fresh(d);
-    int ei = 0, eblen = 0, ewp = -1, ehdr = 0;
+    // the lane's exact batch: stream es, batch ej in it, and the queue entry's header
+    // (first warning row + 1) | rows from the prefix table << 8 | its fill's count << 16
+    int ei = 0, eblen = 0, ewp = -1, es = 0, ej = 0;
+    uint32_t ehdr = 0;
     uint64_t em0 = 0, em1 = 0;
-    int64_t eit = 0;
+    const uint32_t nb32 = (uint32_t)nb;              // nb < 2^31 (ddm_scan_batches checks)
+    // the stream offset w of every lane's batch in the ring's fills, a byte per fill
+    // (slots 0-3 in wr0, 4-7 in wr1): the flag-byte index of a flushed fill without its
+    // geometry recomputed
+    uint32_t wr0 = 0, wr1 = 0;
     // phase: step_rows
     const auto step_rows = [&]() {
         // two exact rows of this lane's batch (as k_scan_batches_exact); a finished batch
         // writes its result
         bool enq = false;
+        int64_t eit = 0;
         if (busy) {
             const bool two = ei + 1 < eblen;
             const int n0 = d.n;
@@ -385,11 +413,10 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
             // phase: step_finish
             if (r == 2 || ei >= eblen) {
                 const bool chg = r == 2;
-                const int64_t es = item_stream(eit, nb, inv_nb);
-                const int64_t ej = eit - es * nb;
-                const int64_t eb = es * L + ej * pb;
+                eit = (int64_t)((uint64_t)(uint32_t)es * nb32) + ej;
                 int w = ewp, c = chg ? ei - 1 : -1;
                 if (kPmap) {
+                    const int64_t eb = (int64_t)es * L + (int64_t)ej * pb;
                     if (w >= 0) w = pmap[eb + w];
                     if (c >= 0) c = pmap[eb + c];
                 }
@@ -403,15 +430,22 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
                 }
                 const uint8_t fl = (uint8_t)((chg ? 1 : 0) | ((chg || w >= 0) ? 2 : 0) | (chg ? 0 : 4) |
                                              lead_bits(em0, em1));
-                // the fill of this batch, if still in the ring (fills iter - kRing + 1 .. iter)
-                const int64_t fit = ((eit >> 6) - wave) / n_waves;
-                if (fit > iter - kRing) {
-                    const int sl = (int)(fit % kRing);
+                // the fill of this batch, if still in the ring (fills iter - kRing + 1 .. iter):
+                // its fill count mod 2^16 rides in the header (a queued batch waits a few
+                // hundred fills at most: 128 entries ahead of it, <= 64 steps per batch).
+                // A fill that left the ring stored a placeholder here from another lane of
+                // this wave (flush); this later store of the same wave to the same address
+                // lands after it, as a wave's vector memory operations issue in order and
+                // one address's requests stay in order through its L2 channel (the full-size
+                // C4 test checks every such batch: all unchanged exact batches outlive the ring)
+                const uint32_t fit = ehdr >> 16;
+                if ((((uint32_t)iter - fit) & 0xffffu) < (uint32_t)kRing) {
+                    const int sl = (int)(fit & (kRing - 1));
                     W.ring_ev[sl][eit & 63] = make_int2(w, c);
                     W.ring_fl[sl][eit & 63] = fl;
                 } else {
                     ev[eit] = make_int2(w, c);
-                    flags[es * nbp + ej] = fl;
+                    flags[(int64_t)es * nbp + ej] = fl;
                 }
                 busy = false;
             }
@@ -435,7 +469,9 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
                 const uint32_t sl = (lq_head + rank) & (kLQ - 1);
                 em0 = W.lq_m0[sl];
                 em1 = W.lq_m1[sl];
-                eit = W.lq_it[sl];
+                const int2 sj = W.lq_sj[sl];
+                es = sj.x;
+                ej = sj.y;
                 ehdr = W.lq_hdr[sl];
                 popping = true;
                 ix = (uint32_t)(em0 & (uint64_t)(kPreN - 1));
@@ -451,29 +487,28 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
         if (popping) {
             busy = true;
             popping = false;
-            ei = ehdr >> 8;
-            ewp = (ehdr & 255) - 1;
+            ei = (int)((ehdr >> 8) & 255u);
+            ewp = (int)(ehdr & 255u) - 1;
             d.p = ei ? t.x : 1.0;
             d.s = 0.0;
             d.pmin = ei ? t.y : __builtin_huge_val();
             d.smin = ei ? t.z : __builtin_huge_val();
             d.psmin = ei ? t.w : __builtin_huge_val();
             d.n = ei + 1;
-            const int64_t es = item_stream(eit, nb, inv_nb);
-            eblen = (int)min((int64_t)pb, L - (eit - es * nb) * pb);
+            eblen = min(pb, (int)L - ej * pb);
         }
     };
     // phase: flush
     // a ring slot's fill to HBM: its 64 event records (whole lines) and flag bytes
     const auto flush = [&](int64_t fit) {
-        const int64_t ff = wave + fit * n_waves;
-        const int sl = (int)(fit % kRing);
-        const FillGeo fg = fill_geo_at(ff << 6, W.ring_sj[sl][0], W.ring_sj[sl][1], n_items, L, nb, nbp, pb, delta,
-                                       inv_nb, lane);
-        if (fg.valid) {
-            ev[fg.base + fg.ln] = W.ring_ev[sl][lane];
+        const int64_t base = (wave + fit * n_waves) << 6;
+        const int sl = (int)(fit & (kRing - 1));
+        const int last = (int)min((int64_t)63, n_items - 1 - base);
+        const int w = (int)(((sl < 4 ? wr0 : wr1) >> (8 * (sl & 3))) & 255u);
+        if (lane <= last) {
+            ev[base + lane] = W.ring_ev[sl][lane];
 #if !(defined(DDM_TUNING) && defined(DDM_PROBE_NO_FLAGS))   // timing probe only: results wrong
-            flags[fg.f0 + fg.ln + fg.w * (int)(nbp - nb)] = W.ring_fl[sl][lane];
+            flags[W.ring_f0[sl] + lane + w * (int)(nbp - nb)] = W.ring_fl[sl][lane];
 #endif
         }
     };
@@ -484,7 +519,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
     // the next fill's first item, stream and batch advance by a constant step (wave-uniform)
     const int64_t dstep = n_waves << 6, ds = dstep / nb, dj = dstep - ds * nb;
     uint4 v[kLoads];
-    if (wave < nfill) fill_load<kLoads>(err, g, lane, v);
+    if (wave < nfill) fill_load_buf<kLoads>(err, g, lane, v);
     for (int64_t f = wave; f < nfill; f += n_waves) {
         // phase: fold
         // A: the fill's bytes -> the LDS bit image -> this lane's 128 row bits
@@ -546,7 +581,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
         } else {
             gn = fill_geo(nfill - 1, n_items, L, nb, nbp, pb, delta, inv_nb, lane);
         }
-        fill_load<kLoads>(err, gn, lane, v);
+        fill_load_buf<kLoads>(err, gn, lane, v);
         // phase: decide
         // D: decisions and stores
         bool exact = false;
@@ -579,14 +614,16 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
             // phase: ring
             // into the ring (an exact batch's slot is written when it finishes, or by
             // k_scan_batches_exact<0> after the pass when it overflows to the global queue)
-            const int sl = (int)(iter % kRing);
+            const int sl = (int)(iter & (kRing - 1));
             W.ring_ev[sl][lane] = make_int2(wp, cp);
             W.ring_fl[sl][lane] = fl;
         }
-        if (lane == 0) {
-            const int sl = (int)(iter % kRing);
-            W.ring_sj[sl][0] = g.s0;
-            W.ring_sj[sl][1] = g.j0;
+        {
+            const int sl = (int)(iter & (kRing - 1));
+            if (lane == 0) W.ring_f0[sl] = g.f0;
+            const uint32_t sh = 8u * (uint32_t)(sl & 3), keep = ~(255u << sh), wb = (uint32_t)g.w << sh;
+            if (sl < 4) wr0 = (wr0 & keep) | wb;
+            else wr1 = (wr1 & keep) | wb;
         }
         // phase: start
         start(ppt);
@@ -600,8 +637,8 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
                 const uint32_t sl = (lq_head + lq_count + r) & (kLQ - 1);
                 W.lq_m0[sl] = m0;
                 W.lq_m1[sl] = m1;
-                W.lq_it[sl] = g.base + g.ln;
-                W.lq_hdr[sl] = (pre && blen > kPre) ? ((wp + 1) | (kPre << 8)) : 0;
+                W.lq_sj[sl] = make_int2((int)(g.s0 + g.w), g.j);
+                W.lq_hdr[sl] = ((pre && blen > kPre) ? (uint32_t)((wp + 1) | (kPre << 8)) : 0u) | ((uint32_t)iter << 16);
                 exact = false;
             }
             lq_count += min((uint32_t)__popcll(xm), room);

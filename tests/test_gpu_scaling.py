@@ -56,6 +56,8 @@ def test_events_do_not_depend_on_gpu_count(workload, extra):
     assert one["breakdown"]["drifts_per_step"] > 0
     assert two["config"]["partitions_this_rank"] == 4 and one["config"]["partitions_this_rank"] == 8
     assert one["scaling"] == two["scaling"] == "strong"
+    assert two["gather_backend"] and "gather_backend" not in one
+    assert two["roofline"]["frac"] > 0
     if workload == "c5":
         assert two["breakdown"]["gather_ms_per_step"] is not None
 
@@ -72,14 +74,18 @@ def test_bench_launches_its_own_ranks():
     assert two["breakdown"]["checks"]["events_sha1"] == one["breakdown"]["checks"]["events_sha1"]
 
 
-@pytest.mark.parametrize("mult,inst", [(2, 16), (2, 1), (4, 4)])
+@pytest.mark.parametrize("mult,inst", [(2, 16), (2, 1), (4, 4), (512, 16)])
 def test_bench_c2_matches_reference_fixtures(mult, inst):
     """configs[1] (outdoorStream) as the bench times it: every partition's events == the
-    reference-executed fixture, and vs_baseline against the matching published cell."""
+    reference-executed fixture, and vs_baseline against the matching published cell.
+    (512, 16) is the published cell itself (`Plot Results.ipynb:572`): all 16 partitions,
+    20,464 batch records, against tests/golden/make_golden_cell.py's fixture, the stream
+    order by its sha1."""
     import torch
     assert not torch.cuda.is_initialized()
     r = _bench(1, ["--workload", "c2", "--c2-mult", str(mult), "--c2-instances", str(inst)])
     assert "fixtures" in r["breakdown"]["checks"]
+    assert "oracle_prefix" not in r["breakdown"]["checks"]
     assert r["config"]["rows_per_step"] == 4000 * mult
     assert r["vs_baseline"] is not None and r["vs_baseline"] > 1
     assert r["roofline"]["kernel"].startswith("k_cforest_predict_dev")

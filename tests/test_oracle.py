@@ -223,3 +223,23 @@ def test_mt_replay_matches_oracle_controller_rng():
         changes = [k + 1 for k in np.nonzero(expect[:, 2] >= 0)[0]]
         _, key, pos = mt_replay(1000 + d, len(part), changes)
         assert np.array_equal(key, st[1]) and pos == st[2], d
+
+
+def test_oracle_controller_matches_published_cell_partition():
+    """The published cell (outdoorStream x512, 16 instances; tests/golden/make_golden_cell.py,
+    the reference's own run_DDM_loop on every partition): the stream order the product's
+    loader builds has the fixture's sha1, and the oracle controller reproduces partition 0's
+    1,279 batch records (the GPU side compares all 16 through bench.py, test_gpu_scaling)."""
+    import hashlib
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), "..", "distributed-drift-detection_amd"))
+    from ddm_amd import loader
+    data = load_npz("outdoor.npz")
+    cfg = load_npz("outdoor_cfg_m512_i16.npz")
+    X, target = data["X"], data["target"].astype(np.int64)
+    order = loader.prepare_order(len(target), target, 512, np.random.RandomState(123), "stable")
+    assert hashlib.sha1(np.ascontiguousarray(order.astype(np.int32)).tobytes()).hexdigest() == str(cfg["order_sha1"])
+    sel = order[order % 16 == 0]
+    np.random.seed(1000)
+    got = run_partition(X[sel], target[sel], np.arange(len(sel)), sel)
+    assert np.array_equal(got, cfg["events/0"])
