@@ -376,6 +376,8 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
     uint32_t lq_head = 0, lq_count = 0, nq = 0;
     int64_t* const wq1 = q1 + wave * qcap;
     bool busy = false, popping = false;
+    bool fin = false;                                 // the lane's batch finished in this fill's steps
+    int fr = 0;                                       // ... with this test result of its last row
     SmallDet d;
     small_fresh(d);
     // the lane's exact batch: stream es, batch ej in it, and the queue entry's header
@@ -390,10 +392,10 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
     uint32_t wr0 = 0, wr1 = 0;
     // phase: step_rows
     const auto step_rows = [&]() {
-        // two exact rows of this lane's batch (as k_scan_batches_exact); a finished batch
-        // writes its result
-        bool enq = false;
-        int64_t eit = 0;
+        // two exact rows of this lane's batch (as k_scan_batches_exact); a finished batch is
+        // marked and written by finish() once per fill (a lane that finishes idles until the
+        // next fill's pop anyway; per step, the compiler hoisted the result's addressing out
+        // of its branch into every step)
         if (busy) {
             const bool two = ei + 1 < eblen;
             const int n0 = d.n;
@@ -410,8 +412,22 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
                 if (r == 1 && ewp < 0) ewp = ei;
                 ++ei;
             }
-            // phase: step_finish
             if (r == 2 || ei >= eblen) {
+                busy = false;
+                fin = true;
+                fr = r;
+            }
+        }
+    };
+    // phase: step_finish
+    // the results of the batches that finished in this fill's steps
+    const auto finish = [&]() {
+        bool enq = false;
+        int64_t eit = 0;
+        if (fin) {
+            fin = false;
+            {
+                const int r = fr;
                 const bool chg = r == 2;
                 eit = (int64_t)((uint64_t)(uint32_t)es * nb32) + ej;
                 int w = ewp, c = chg ? ei - 1 : -1;
@@ -447,10 +463,8 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
                     ev[eit] = make_int2(w, c);
                     flags[(int64_t)es * nbp + ej] = fl;
                 }
-                busy = false;
             }
         }
-        // phase: step_rows
         const uint64_t qm = __ballot(enq);
         if (enq) wq1[nq + __popcll(qm & below)] = eit;
         nq += (uint32_t)__popcll(qm);
@@ -670,6 +684,8 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
             if (__ballot(busy) == 0ull) break;
             step_rows();
         }
+        // phase: step_finish
+        if (__ballot(fin)) finish();
         // phase: flush
         g = gn;
         ++iter;
@@ -686,6 +702,7 @@ __global__ __launch_bounds__(kClsThreads) __attribute__((amdgpu_waves_per_eu(kCl
             start(pst[pix]);
             if (__ballot(busy) == 0ull && lq_count == 0) break;
             step_rows();
+            if (__ballot(fin)) finish();
         }
     }
     wave_sync_lds();
@@ -1177,7 +1194,7 @@ __global__ __launch_bounds__(kChainThreads) void k_scan_batches_chain(
     ddm_state* __restrict__ state, int2* __restrict__ ev, const uint8_t* __restrict__ flags,
     int64_t* __restrict__ nev_out, const uint8_t* __restrict__ pmap, const FixEntry* __restrict__ coop,
     const uint32_t* __restrict__ ctr, const double2* __restrict__ pend, const int2* __restrict__ ev1,
-    const uint8_t* __restrict__ flags1, const double2* __restrict__ pend1) {
+    const uint8_t* __restrict__ flags1, const double2* __restrict__ pend1, uint64_t* __restrict__ cprof) {
     __shared__ uint64_t img[kChainThreads / 64][kClsWords + 2];
     __shared__ double s_tile[kChainThreads / 64][kTileScratch];
     const int64_t pb = P.per_batch;
@@ -1190,7 +1207,16 @@ __global__ __launch_bounds__(kChainThreads) void k_scan_batches_chain(
     double* const tw = s_tile[wv];
     const uint32_t n_list = __atomic_load_n(ctr + 2, __ATOMIC_RELAXED);
     const uint32_t n_waves = gridDim.x * (kChainThreads / 64);
+#ifdef DDM_TUNING
+    // per-wave profile (tuning builds, DDM_CHAIN_PROF): start / end on the 100 MHz clock,
+    // streams taken, rows run through wave_tile
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    uint64_t p_streams = 0, p_rows = 0;
+#endif
     for (uint32_t k = blockIdx.x * (kChainThreads / 64) + wv; k < n_list; k += n_waves) {
+#ifdef DDM_TUNING
+        ++p_streams;
+#endif
         const FixEntry e = coop[k];
         Walk W;
         W.d = e.d;
@@ -1238,6 +1264,9 @@ __global__ __launch_bounds__(kChainThreads) void k_scan_batches_chain(
                 const int cnt = min(64, blen - ci);
                 const uint64_t m = ci < 64 ? m0_shift(a0, a1, ci) : (a1 >> (ci - 64));
                 const TileOut to = wave_tile(c, m, cnt, min_inst, wl, cl, tw);
+#ifdef DDM_TUNING
+                p_rows += (uint64_t)cnt;
+#endif
                 const uint64_t upto = to.last >= 63 ? ~0ull : ((1ull << (to.last + 1)) - 1);
                 const uint64_t wb = to.warn & upto;
                 if (cw < 0 && wb) cw = ci + __builtin_ctzll(wb);
@@ -1263,6 +1292,19 @@ __global__ __launch_bounds__(kChainThreads) void k_scan_batches_chain(
             if (nev_out) nev_out[W.sid] = W.nev;
         }
     }
+#ifdef DDM_TUNING
+    if (cprof) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        const uint32_t wid = blockIdx.x * (kChainThreads / 64) + wv;
+        if (lane == 0) {
+            uint64_t* const r = cprof + 4 * (uint64_t)wid;
+            r[0] = t_start;
+            r[1] = t_end;
+            r[2] = p_streams;
+            r[3] = p_rows;
+        }
+    }
+#endif
 }
 
 // Scratch: counters, the fix-up list, flag bytes, the per-wave queues and the end states /
@@ -1284,8 +1326,10 @@ struct BatchScratch {
     uint32_t* q1cnt;    // [kMaxWaves]
     double4* pst;       // [kPreN]
     uint16_t* ptab;     // [kPreN]
+    uint64_t* cprof;    // tuning builds: the chain kernel's per-wave profile [kChainProfWaves][4] (the scratch's end)
     int64_t bytes;
 };
+constexpr int64_t kChainProfWaves = 2048 * 4;
 
 BatchScratch batch_scratch(void* base, int64_t n_streams, int64_t nb) {
     const auto up = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
@@ -1303,6 +1347,9 @@ BatchScratch batch_scratch(void* base, int64_t n_streams, int64_t nb) {
     const int64_t o_pend1 = take(48 * n_items), o_q = take((int64_t)sizeof(QEntry) * nq), o_q1 = take(8 * nq);
     const int64_t o_qcnt = take(4 * kMaxWaves), o_q1cnt = take(4 * kMaxWaves), o_pst = take(32 * (int64_t)kPreN);
     const int64_t o_ptab = take(2 * (int64_t)kPreN);
+#ifdef DDM_TUNING
+    const int64_t o_cprof = take(32 * kChainProfWaves);
+#endif
     uint8_t* b = static_cast<uint8_t*>(base);
     BatchScratch sc;
     sc.ctr = reinterpret_cast<uint32_t*>(b);
@@ -1319,6 +1366,11 @@ BatchScratch batch_scratch(void* base, int64_t n_streams, int64_t nb) {
     sc.q1cnt = reinterpret_cast<uint32_t*>(b + o_q1cnt);
     sc.pst = reinterpret_cast<double4*>(b + o_pst);
     sc.ptab = reinterpret_cast<uint16_t*>(b + o_ptab);
+#ifdef DDM_TUNING
+    sc.cprof = getenv("DDM_CHAIN_PROF") ? reinterpret_cast<uint64_t*>(b + o_cprof) : nullptr;
+#else
+    sc.cprof = nullptr;
+#endif
     sc.bytes = o;
     return sc;
 }
@@ -1432,10 +1484,11 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
                        sc.flags, nev_out, perm_map, sc.need, sc.ctr, sc.pend, sc.ev1, sc.flags1, sc.pend1, sc.coop);
     if (int rc = ddm::launch_status("ddm_scan_batches/walk")) return rc;
     const int64_t fix_blocks =
-        std::max<int64_t>(1, std::min<int64_t>(fix_blocks_max, ddm::ceil_div(n_streams, kChainThreads / 64)));
+        std::max<int64_t>(1, std::min<int64_t>(sc.cprof ? std::min(fix_blocks_max, 2048) : fix_blocks_max,
+                                               ddm::ceil_div(n_streams, kChainThreads / 64)));
     hipLaunchKernelGGL(k_scan_batches_chain, dim3((unsigned)fix_blocks), dim3(kChainThreads), 0, s, err, stream_len,
                        nb, nbp, *prm, state_io, reinterpret_cast<int2*>(ev_out), sc.flags, nev_out, perm_map,
-                       sc.coop, sc.ctr, sc.pend, sc.ev1, sc.flags1, sc.pend1);
+                       sc.coop, sc.ctr, sc.pend, sc.ev1, sc.flags1, sc.pend1, sc.cprof);
     if (ev_end)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
     return ddm::launch_status("ddm_scan_batches");

@@ -16,7 +16,8 @@ def test_manifest_versions():
     man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
     import sklearn
     assert man["sklearn"] == sklearn.__version__, "fixtures depend on sklearn's RF; regenerate"
-    assert set(man["configs"]) == {f"m{m}_i{i}" for m, i in golden_configs()}
+    # the small grid (make_golden.py) and the published cell (make_golden_cell.py)
+    assert set(man["configs"]) == {f"m{m}_i{i}" for m, i in golden_configs()} | {"m512_i16"}
 
 
 def test_ddm_known_answers():

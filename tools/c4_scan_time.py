@@ -45,6 +45,21 @@ def child(a):
         torch.cuda.synchronize()
         if r >= 2:
             times.append(e0.elapsed_time(e1))
+    if os.environ.get("DDM_CHAIN_PROF"):   # tuning build: the chain kernel's per-wave profile (last call)
+        cp = scratch[-32 * 8192:].cpu().numpy().view(np.uint64).reshape(8192, 4).astype(np.int64)
+        cp = cp[cp[:, 0] > 0]
+        t0 = cp[:, 0].min()
+        dur = (cp[:, 1] - cp[:, 0]) / 100.0          # us (100 MHz)
+        order = np.argsort(-dur)
+        prof_out = {"waves": int(len(cp)), "span_us": float((cp[:, 1].max() - t0) / 100.0),
+                    "start_spread_us": float((cp[:, 0].max() - t0) / 100.0),
+                    "dur_us_pct": {str(q): float(np.percentile(dur, q)) for q in (50, 90, 99, 99.9, 100)},
+                    "rows_total": int(cp[:, 3].sum()), "streams_total": int(cp[:, 2].sum()),
+                    "top": [{"dur_us": float(dur[i]), "start_us": float((cp[i, 0] - t0) / 100.0),
+                             "streams": int(cp[i, 2]), "rows": int(cp[i, 3])} for i in order[:12]],
+                    "hist_dur_us": np.histogram(dur, bins=[0, 5, 10, 20, 40, 60, 80, 100, 120, 160, 200, 400])[0].tolist()}
+        with open(os.environ["DDM_CHAIN_PROF"], "w") as f:
+            json.dump(prof_out, f, indent=1)
     prof = scratch[64:128].cpu().numpy().view(np.uint64)
     h = hashlib.sha1()
     h.update(ev.cpu().numpy().tobytes())
