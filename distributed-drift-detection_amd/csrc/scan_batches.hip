@@ -69,8 +69,7 @@ __device__ __forceinline__ void batch_mask(const uint8_t* __restrict__ err, int6
     const int off = (int)(bstart & 15);
     const int nch = (off + blen + 15) >> 4;
     // 16 bytes -> 16 bits by four v_dot4 (fold16) once bytes other than 0/1 are made 1
-    // (rare: a ballot decides for the lanes loading together); nz16's byte tests took
-    // ~300 VALU per batch, most of a level-1 refill
+    // (rare: a ballot decides for the lanes loading together) instead of nz16's byte tests
     uint32_t odd = 0;
 #pragma unroll
     for (int k = 0; k < 9; ++k) odd |= v[k].x | v[k].y | v[k].z | v[k].w;
@@ -1124,38 +1123,19 @@ constexpr int kWalkThreads = DDM_WALK_THREADS;
 #define DDM_WALK_WAVES 4
 #endif
 
-__device__ __forceinline__ void chain_stream(const FixEntry& e, const uint8_t* __restrict__ err, int64_t L, int64_t nb,
-                                             int64_t nbp, int64_t pb, bool shortcuts, int min_inst, double wl,
-                                             double cl, ddm_state* __restrict__ state, int2* __restrict__ ev,
-                                             const uint8_t* __restrict__ flags, int64_t* __restrict__ nev_out,
-                                             const uint8_t* __restrict__ pmap, const double2* __restrict__ pend,
-                                             const int2* __restrict__ ev1, const uint8_t* __restrict__ flags1,
-                                             const double2* __restrict__ pend1, uint64_t* img, double* tw,
-                                             uint64_t& p_rows);
-
-constexpr int kDefMax = 16;      // deferred streams a walker block runs itself
-[[maybe_unused]] constexpr int64_t kChainProfWaves = 16384;   // tuning builds: waves profiled (DDM_CHAIN_PROF)
-
 __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(DDM_WALK_WAVES))) void k_scan_batches_walk(
-    const uint8_t* __restrict__ err, int64_t n_streams, int64_t L, int64_t nb, int64_t nbp, ddm_params P,
-    ddm_state* __restrict__ state, int2* __restrict__ ev, const uint8_t* __restrict__ flags,
-    int64_t* __restrict__ nev_out, const uint8_t* __restrict__ pmap, const uint32_t* __restrict__ need,
-    uint32_t* __restrict__ ctr, const double2* __restrict__ pend, const int2* __restrict__ ev1,
-    const uint8_t* __restrict__ flags1, const double2* __restrict__ pend1, FixEntry* __restrict__ coop,
-    uint64_t* __restrict__ cprof) {
+    int64_t n_streams, int64_t L, int64_t nb, int64_t nbp, ddm_params P, ddm_state* __restrict__ state,
+    int2* __restrict__ ev, const uint8_t* __restrict__ flags, int64_t* __restrict__ nev_out,
+    const uint8_t* __restrict__ pmap, const uint32_t* __restrict__ need, uint32_t* __restrict__ ctr,
+    const double2* __restrict__ pend, const int2* __restrict__ ev1, const uint8_t* __restrict__ flags1,
+    const double2* __restrict__ pend1, FixEntry* __restrict__ coop) {
     const int64_t pb = P.per_batch;
     const bool shortcuts = P.min_num_instances == 3;
     const int lane = threadIdx.x & 63;
     const uint64_t below = (1ull << lane) - 1;
     __shared__ int32_t s_list[kWalkThreads];
-    __shared__ uint32_t s_cnt, s_ndef;
-    __shared__ FixEntry s_def[kDefMax];
-    __shared__ uint64_t img[kWalkThreads / 64][kClsWords + 2];
-    __shared__ double s_tile[kWalkThreads / 64][kTileScratch];
-#ifdef DDM_TUNING
-    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-#endif
-    if (threadIdx.x == 0) s_cnt = s_ndef = 0;
+    __shared__ uint32_t s_cnt;
+    if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
     const int64_t t = (int64_t)blockIdx.x * kWalkThreads + threadIdx.x;
     if (t < n_streams) {
@@ -1181,174 +1161,46 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(DD
     __syncthreads();
     // the block's other streams, packed onto its first lanes
     const uint32_t cnt = s_cnt;
-    if ((threadIdx.x & ~63u) < cnt) {
-        bool defer = false;
-        Walk W;
-        if (threadIdx.x < cnt) {
-            const int64_t u = (int64_t)blockIdx.x * kWalkThreads + s_list[threadIdx.x];
-            W.sid = u;
-            load_det(W.d, state[u]);
-            W.j = W.wbase = W.nev = 0;
-            W.chg_m = nb > 0 ? change_window(flags + u * nbp, 0, nb, W.st_m, W.ev_m, W.lm) : 0;
-            walk_open(W, L, nb, nbp, pb, shortcuts, ev, flags, pmap, pend, ev1, flags1, pend1);
-            if (W.j >= nb) {
-                state[u] = store_det(W.d);
-                if (nev_out) nev_out[u] = W.nev;
-            } else {
-                defer = true;
-            }
+    if ((threadIdx.x & ~63u) >= cnt) return;
+    bool defer = false;
+    Walk W;
+    if (threadIdx.x < cnt) {
+        const int64_t u = (int64_t)blockIdx.x * kWalkThreads + s_list[threadIdx.x];
+        W.sid = u;
+        load_det(W.d, state[u]);
+        W.j = W.wbase = W.nev = 0;
+        W.chg_m = nb > 0 ? change_window(flags + u * nbp, 0, nb, W.st_m, W.ev_m, W.lm) : 0;
+        walk_open(W, L, nb, nbp, pb, shortcuts, ev, flags, pmap, pend, ev1, flags1, pend1);
+        if (W.j >= nb) {
+            state[u] = store_det(W.d);
+            if (nev_out) nev_out[u] = W.nev;
+        } else {
+            defer = true;
         }
-        // a stream that needs carried rows: this block's waves run it right after the walk
-        // (up to kDefMax of them), the rest goes to the fix-up list of k_scan_batches_chain
+    }
+    const uint64_t dm = __ballot(defer);
+    if (dm) {
+        uint32_t base = 0;
+        const int lead = __builtin_ctzll(dm);
+        if (lane == lead) base = atomicAdd(ctr + 2, (uint32_t)__popcll(dm));
+        base = __shfl(base, lead);
         if (defer) {
             FixEntry e;
             e.d = W.d;
             e.sid = W.sid;
             e.j = W.j;
             e.nev = W.nev;
-            const uint32_t k = atomicAdd(&s_ndef, 1u);
-            if (k < (uint32_t)kDefMax) {
-                s_def[k] = e;
-                defer = false;
-            }
+            coop[base + __popcll(dm & below)] = e;
         }
-        const uint64_t dm = __ballot(defer);
-        if (dm) {
-            uint32_t base = 0;
-            const int lead = __builtin_ctzll(dm);
-            if (lane == lead) base = atomicAdd(ctr + 2, (uint32_t)__popcll(dm));
-            base = __shfl(base, lead);
-            if (defer) {
-                FixEntry e;
-                e.d = W.d;
-                e.sid = W.sid;
-                e.j = W.j;
-                e.nev = W.nev;
-                coop[base + __popcll(dm & below)] = e;
-            }
-        }
-    }
-    __syncthreads();
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t ndef = min(s_ndef, (uint32_t)kDefMax);
-    uint64_t p_rows = 0, p_streams = 0;
-    for (uint32_t k = wv; k < ndef; k += kWalkThreads / 64) {
-        ++p_streams;
-        chain_stream(s_def[k], err, L, nb, nbp, pb, shortcuts, P.min_num_instances, P.warning_level,
-                     P.out_control_level, state, ev, flags, nev_out, pmap, pend, ev1, flags1, pend1, img[wv],
-                     s_tile[wv], p_rows);
-    }
-#ifdef DDM_TUNING
-    // per-wave profile (tuning builds, DDM_CHAIN_PROF): start / end on the 100 MHz clock,
-    // carried streams run, their rows through wave_tile
-    if (cprof) {
-        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-        const uint32_t wid = blockIdx.x * (kWalkThreads / 64) + wv;
-        if (lane == 0 && wid < (uint32_t)kChainProfWaves) {
-            uint64_t* const r = cprof + 4 * (uint64_t)wid;
-            r[0] = t_start;
-            r[1] = t_end;
-            r[2] = p_streams;
-            r[3] = p_rows;
-        }
-    }
-#else
-    (void)cprof;
-    (void)p_streams;
-#endif
-}
-
-// 4b. A stream the walker handed over, by one wave.  The stream's bytes are read 64 batches
-// at a time by coalesced loads into the wave's LDS bit image (as the classify pass does), so
-// a carried detector's rows never wait on memory batch by batch; the walk (walk_open, uniform
-// over the wave) skips what the flag bytes and records decide, and a batch that needs rows
-// runs through wave_tile tiles (the p chain once, the rest lane-parallel) from the carried
-// detector.
-__device__ __forceinline__ void chain_stream(const FixEntry& e, const uint8_t* __restrict__ err, int64_t L, int64_t nb,
-                                             int64_t nbp, int64_t pb, bool shortcuts, int min_inst, double wl,
-                                             double cl, ddm_state* __restrict__ state, int2* __restrict__ ev,
-                                             const uint8_t* __restrict__ flags, int64_t* __restrict__ nev_out,
-                                             const uint8_t* __restrict__ pmap, const double2* __restrict__ pend,
-                                             const int2* __restrict__ ev1, const uint8_t* __restrict__ flags1,
-                                             const double2* __restrict__ pend1, uint64_t* img, double* tw,
-                                             uint64_t& p_rows) {
-    const int lane = threadIdx.x & 63;
-    uint16_t* const img16 = reinterpret_cast<uint16_t*>(img);
-    Walk W;
-    W.d = e.d;
-    W.sid = e.sid;
-    W.j = e.j;
-    W.nev = e.nev;
-    W.wbase = W.j & ~(int64_t)63;
-    W.chg_m = change_window(flags + W.sid * nbp, W.wbase, nb, W.st_m, W.ev_m, W.lm);
-    int64_t ib = -((int64_t)1 << 40), ia0 = 0;     // the image: batches [ib, ib + 64), first byte ia0
-    const int64_t srow = W.sid * L;
-    for (;;) {
-        walk_open(W, L, nb, nbp, pb, shortcuts, ev, flags, pmap, pend, ev1, flags1, pend1);
-        if (W.j >= nb) break;
-        const int64_t j = W.j;
-        if (j < ib || j >= ib + 64) {
-            // batches [j & ~63, +64) of the stream into the image
-            ib = j & ~(int64_t)63;
-            ia0 = (srow + ib * pb) & ~(int64_t)15;
-            const int64_t iend = srow + min(L, (ib + 64) * pb);
-            const int nch = (int)((iend - ia0 + 15) >> 4);
-            wave_sync_lds();
-            for (int c0 = 0; c0 < nch; c0 += 64) {
-                const int c = min(c0 + lane, nch - 1);
-                uint4 v = *reinterpret_cast<const uint4*>(err + ia0 + 16 * (int64_t)c);
-                v.x = nzbytes(v.x);
-                v.y = nzbytes(v.y);
-                v.z = nzbytes(v.z);
-                v.w = nzbytes(v.w);
-                img16[c] = (uint16_t)fold16(v);
-            }
-            wave_sync_lds();
-        }
-        const int64_t bstart = srow + j * pb;
-        const int blen = (int)min(pb, L - j * pb);
-        const int o = (int)(bstart - ia0);
-        const int wo = o >> 6, sh = o & 63;
-        const uint64_t x0 = img[wo], x1 = img[wo + 1], x2 = img[wo + 2];
-        const uint64_t a0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
-        const uint64_t a1 = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
-        // the batch's rows from the carried detector, one tile after the other
-        Det c = W.d;
-        c.chg = 0;
-        int ci = 0, cw = -1, cp = -1;
-        while (ci < blen) {
-            const int cnt = min(64, blen - ci);
-            const uint64_t m = ci < 64 ? m0_shift(a0, a1, ci) : (a1 >> (ci - 64));
-            const TileOut to = wave_tile(c, m, cnt, min_inst, wl, cl, tw);
-            p_rows += (uint64_t)cnt;
-            const uint64_t upto = to.last >= 63 ? ~0ull : ((1ull << (to.last + 1)) - 1);
-            const uint64_t wb = to.warn & upto;
-            if (cw < 0 && wb) cw = ci + __builtin_ctzll(wb);
-            if (to.kc >= 0) {
-                cp = ci + to.kc;
-                break;
-            }
-            ci += cnt;
-        }
-        int w = cw, cc = cp;
-        if (pmap) {
-            if (w >= 0) w = pmap[bstart + w];
-            if (cc >= 0) cc = pmap[bstart + cc];
-        }
-        if (lane == 0) ev[W.sid * nb + j] = make_int2(w, cc);
-        W.nev += (w >= 0 || cc >= 0);
-        if (cp >= 0) det_reset(c);             // DDM dropped (DDM_Process.py:209)
-        W.d = c;
-        W.j = j + 1;
-    }
-    if (lane == 0) {
-        state[W.sid] = store_det(W.d);
-        if (nev_out) nev_out[W.sid] = W.nev;
     }
 }
 
-// 4c. The fix-up list's overflow (a walker block with more than kDefMax deferred streams):
-// one wave per stream, grid-stride.
+// 4b. The chain kernel: one wave per stream the walker handed over.  The stream's bytes
+// are read 64 batches at a time by coalesced loads into the wave's LDS bit image (as the
+// classify pass does), so a carried detector's rows never wait on memory batch by batch;
+// the walk (walk_open, uniform over the wave) skips what the flag bytes and records decide,
+// and a batch that needs rows runs through wave_tile tiles (the p chain once, the rest
+// lane-parallel) from the carried detector.
 constexpr int kChainThreads = 256;
 
 __global__ __launch_bounds__(kChainThreads) void k_scan_batches_chain(
@@ -1356,17 +1208,117 @@ __global__ __launch_bounds__(kChainThreads) void k_scan_batches_chain(
     ddm_state* __restrict__ state, int2* __restrict__ ev, const uint8_t* __restrict__ flags,
     int64_t* __restrict__ nev_out, const uint8_t* __restrict__ pmap, const FixEntry* __restrict__ coop,
     const uint32_t* __restrict__ ctr, const double2* __restrict__ pend, const int2* __restrict__ ev1,
-    const uint8_t* __restrict__ flags1, const double2* __restrict__ pend1) {
+    const uint8_t* __restrict__ flags1, const double2* __restrict__ pend1, uint64_t* __restrict__ cprof) {
     __shared__ uint64_t img[kChainThreads / 64][kClsWords + 2];
     __shared__ double s_tile[kChainThreads / 64][kTileScratch];
+    const int64_t pb = P.per_batch;
+    const int min_inst = P.min_num_instances;
+    const double wl = P.warning_level, cl = P.out_control_level;
+    const bool shortcuts = min_inst == 3;
+    const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint16_t* const img16 = reinterpret_cast<uint16_t*>(img[wv]);
+    double* const tw = s_tile[wv];
     const uint32_t n_list = __atomic_load_n(ctr + 2, __ATOMIC_RELAXED);
     const uint32_t n_waves = gridDim.x * (kChainThreads / 64);
-    uint64_t rows = 0;
-    for (uint32_t k = blockIdx.x * (kChainThreads / 64) + wv; k < n_list; k += n_waves)
-        chain_stream(coop[k], err, L, nb, nbp, P.per_batch, P.min_num_instances == 3, P.min_num_instances,
-                     P.warning_level, P.out_control_level, state, ev, flags, nev_out, pmap, pend, ev1, flags1, pend1,
-                     img[wv], s_tile[wv], rows);
+#ifdef DDM_TUNING
+    // per-wave profile (tuning builds, DDM_CHAIN_PROF): start / end on the 100 MHz clock,
+    // streams taken, rows run through wave_tile
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    uint64_t p_streams = 0, p_rows = 0;
+#endif
+    for (uint32_t k = blockIdx.x * (kChainThreads / 64) + wv; k < n_list; k += n_waves) {
+#ifdef DDM_TUNING
+        ++p_streams;
+#endif
+        const FixEntry e = coop[k];
+        Walk W;
+        W.d = e.d;
+        W.sid = e.sid;
+        W.j = e.j;
+        W.nev = e.nev;
+        W.wbase = W.j & ~(int64_t)63;
+        W.chg_m = change_window(flags + W.sid * nbp, W.wbase, nb, W.st_m, W.ev_m, W.lm);
+        int64_t ib = -((int64_t)1 << 40), ia0 = 0; // the image: batches [ib, ib + 64), first byte ia0
+        const int64_t srow = W.sid * L;
+        for (;;) {
+            walk_open(W, L, nb, nbp, pb, shortcuts, ev, flags, pmap, pend, ev1, flags1, pend1);
+            if (W.j >= nb) break;
+            const int64_t j = W.j;
+            if (j < ib || j >= ib + 64) {
+                // batches [j & ~63, +64) of the stream into the image
+                ib = j & ~(int64_t)63;
+                ia0 = (srow + ib * pb) & ~(int64_t)15;
+                const int64_t iend = srow + min(L, (ib + 64) * pb);
+                const int nch = (int)((iend - ia0 + 15) >> 4);
+                wave_sync_lds();
+                for (int c0 = 0; c0 < nch; c0 += 64) {
+                    const int c = min(c0 + lane, nch - 1);
+                    uint4 v = *reinterpret_cast<const uint4*>(err + ia0 + 16 * (int64_t)c);
+                    v.x = nzbytes(v.x);
+                    v.y = nzbytes(v.y);
+                    v.z = nzbytes(v.z);
+                    v.w = nzbytes(v.w);
+                    img16[c] = (uint16_t)fold16(v);
+                }
+                wave_sync_lds();
+            }
+            const int64_t bstart = srow + j * pb;
+            const int blen = (int)min(pb, L - j * pb);
+            const int o = (int)(bstart - ia0);
+            const int wo = o >> 6, sh = o & 63;
+            const uint64_t x0 = img[wv][wo], x1 = img[wv][wo + 1], x2 = img[wv][wo + 2];
+            const uint64_t a0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
+            const uint64_t a1 = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
+            // the batch's rows from the carried detector, one tile after the other
+            Det c = W.d;
+            c.chg = 0;
+            int ci = 0, cw = -1, cp = -1;
+            while (ci < blen) {
+                const int cnt = min(64, blen - ci);
+                const uint64_t m = ci < 64 ? m0_shift(a0, a1, ci) : (a1 >> (ci - 64));
+                const TileOut to = wave_tile(c, m, cnt, min_inst, wl, cl, tw);
+#ifdef DDM_TUNING
+                p_rows += (uint64_t)cnt;
+#endif
+                const uint64_t upto = to.last >= 63 ? ~0ull : ((1ull << (to.last + 1)) - 1);
+                const uint64_t wb = to.warn & upto;
+                if (cw < 0 && wb) cw = ci + __builtin_ctzll(wb);
+                if (to.kc >= 0) {
+                    cp = ci + to.kc;
+                    break;
+                }
+                ci += cnt;
+            }
+            int w = cw, cc = cp;
+            if (pmap) {
+                if (w >= 0) w = pmap[bstart + w];
+                if (cc >= 0) cc = pmap[bstart + cc];
+            }
+            if (lane == 0) ev[W.sid * nb + j] = make_int2(w, cc);
+            W.nev += (w >= 0 || cc >= 0);
+            if (cp >= 0) det_reset(c);             // DDM dropped (DDM_Process.py:209)
+            W.d = c;
+            W.j = j + 1;
+        }
+        if (lane == 0) {
+            state[W.sid] = store_det(W.d);
+            if (nev_out) nev_out[W.sid] = W.nev;
+        }
+    }
+#ifdef DDM_TUNING
+    if (cprof) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        const uint32_t wid = blockIdx.x * (kChainThreads / 64) + wv;
+        if (lane == 0) {
+            uint64_t* const r = cprof + 4 * (uint64_t)wid;
+            r[0] = t_start;
+            r[1] = t_end;
+            r[2] = p_streams;
+            r[3] = p_rows;
+        }
+    }
+#endif
 }
 
 // Scratch: counters, the fix-up list, flag bytes, the per-wave queues and the end states /
@@ -1391,7 +1343,7 @@ struct BatchScratch {
     uint64_t* cprof;    // tuning builds: the chain kernel's per-wave profile [kChainProfWaves][4] (the scratch's end)
     int64_t bytes;
 };
-
+constexpr int64_t kChainProfWaves = 2048 * 4;
 
 BatchScratch batch_scratch(void* base, int64_t n_streams, int64_t nb) {
     const auto up = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
@@ -1490,7 +1442,7 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
     const BatchScratch sc = batch_scratch(scratch, n_streams, nb);
     hipStream_t s = ddm::as_hip(stream);
     static const int ex_refill = std::max(1, std::min(64, env_int("DDM_EXACT_REFILL", 24)));
-    static const int fix_blocks_max = env_int("DDM_FIX_BLOCKS", 256);
+    static const int fix_blocks_max = env_int("DDM_FIX_BLOCKS", 2048);
     static const bool use_pre = env_int("DDM_SCAN_PRE", 1) != 0;
     static const int cls_steps = std::max(0, env_int("DDM_SCAN_STEPS", 2));
     static const int cls_pop = std::max(1, std::min(64, env_int("DDM_SCAN_POP", 16)));
@@ -1542,16 +1494,15 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
         if (int rc = ddm::launch_status("ddm_scan_batches/exact1")) return rc;
     }
     hipLaunchKernelGGL(k_scan_batches_walk, dim3((unsigned)ddm::ceil_div(n_streams, kWalkThreads)), dim3(kWalkThreads),
-                       0, s, err, n_streams, stream_len, nb, nbp, *prm, state_io, reinterpret_cast<int2*>(ev_out),
-                       sc.flags, nev_out, perm_map, sc.need, sc.ctr, sc.pend, sc.ev1, sc.flags1, sc.pend1, sc.coop,
-                       sc.cprof);
+                       0, s, n_streams, stream_len, nb, nbp, *prm, state_io, reinterpret_cast<int2*>(ev_out),
+                       sc.flags, nev_out, perm_map, sc.need, sc.ctr, sc.pend, sc.ev1, sc.flags1, sc.pend1, sc.coop);
     if (int rc = ddm::launch_status("ddm_scan_batches/walk")) return rc;
-    // the fix-up list's overflow (usually empty: its waves read the count and return)
     const int64_t fix_blocks =
-        std::max<int64_t>(1, std::min<int64_t>(fix_blocks_max, ddm::ceil_div(n_streams, 64 * (kChainThreads / 64))));
+        std::max<int64_t>(1, std::min<int64_t>(sc.cprof ? std::min(fix_blocks_max, 2048) : fix_blocks_max,
+                                               ddm::ceil_div(n_streams, kChainThreads / 64)));
     hipLaunchKernelGGL(k_scan_batches_chain, dim3((unsigned)fix_blocks), dim3(kChainThreads), 0, s, err, stream_len,
                        nb, nbp, *prm, state_io, reinterpret_cast<int2*>(ev_out), sc.flags, nev_out, perm_map,
-                       sc.coop, sc.ctr, sc.pend, sc.ev1, sc.flags1, sc.pend1);
+                       sc.coop, sc.ctr, sc.pend, sc.ev1, sc.flags1, sc.pend1, sc.cprof);
     if (ev_end)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
     return ddm::launch_status("ddm_scan_batches");

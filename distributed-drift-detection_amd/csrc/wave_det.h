@@ -54,11 +54,7 @@ struct TileOut {
 // sc: this wave's LDS scratch of kTileScratch doubles (n, RN(1/n), x and p of every row).
 // d must be uniform over the wave and not in a pending change (the caller resets it first);
 // rows >= cnt are ignored.
-#ifdef DDM_TILE_LDS_CHAIN
 constexpr int kTileScratch = 4 * 64;
-#else
-constexpr int kTileScratch = 64;     // the p of every row (the chain's operands are in SGPRs)
-#endif
 
 __device__ __forceinline__ TileOut wave_tile(Det& d, uint64_t m, int cnt, int min_inst, double wl, double cl,
                                              double* sc) {
@@ -69,47 +65,12 @@ __device__ __forceinline__ TileOut wave_tile(Det& d, uint64_t m, int cnt, int mi
         d.warn = 0;
         return {-1, cnt - 1, 0ull};
     }
-    const double nl = (double)d.n + (double)lane;   // divisor of row lane
-    const double rl = 1.0 / nl;                     // RN(1/n), as det_add_fast's rcp[] / 1.0 / n
-#ifndef DDM_TILE_LDS_CHAIN
-    // the chain with its operands in SGPRs: row k's RN(1/n) by v_readlane from the lane that
-    // computed it, n as a uniform register stepped by 1, x from the scalar bits; only the p
-    // values go through LDS (lane 0 writes each group of 8).  None of that depends on p, so it
-    // issues in the chain's dependency stalls (a dependent fp64 operation takes ~11 cycles on
-    // gfx950, tools/lat_bench.hip): a row costs its 5 dependent operations.  (The LDS form
-    // below staged n, 1/n and x in LDS behind a wave barrier and read them back by broadcast
-    // loads ahead of each group.)  Rows past cnt take 1/n = 0: their step adds exactly 0.
-    double* const s_p = sc;
-    const uint64_t mu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(m >> 32)) << 32) |
-                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)m);
-    const int cu = __builtin_amdgcn_readfirstlane(cnt);
-    const double rz = lane < cnt ? rl : 0.0;
-    double p = d.p;
-    double nk = (double)d.n;
-    for (int k0 = 0; k0 < cu; k0 += 8) {
-        double ps[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const double rk = readlane_d(rz, k0 + u);
-            const double xk = ((mu >> (k0 + u)) & 1ull) ? 1.0 : 0.0;
-            p = p + div_rn(xk - p, nk, rk);
-            nk = nk + 1.0;
-            ps[u] = p;
-        }
-        if (lane == 0) {
-#pragma unroll
-            for (int u = 0; u < 8; ++u) s_p[k0 + u] = ps[u];
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const double myp = lane < cnt ? s_p[lane] : 0.0;
-#else
     double* const s_n = sc;
     double* const s_r = sc + 64;
     double* const s_x = sc + 128;
     double* const s_p = sc + 192;
+    const double nl = (double)d.n + (double)lane;   // divisor of row lane
+    const double rl = 1.0 / nl;                     // RN(1/n), as det_add_fast's rcp[] / 1.0 / n
     // rows past cnt get n = 1, 1/n = 0: their step adds exactly 0 to p
     s_n[lane] = lane < cnt ? nl : 1.0;
     s_r[lane] = lane < cnt ? rl : 0.0;
@@ -142,7 +103,6 @@ __device__ __forceinline__ TileOut wave_tile(Det& d, uint64_t m, int cnt, int mi
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const double myp = lane < cnt ? s_p[lane] : 0.0;
-#endif
     const double s = sqrt_q(div_rn(myp * (1.0 - myp), nl, rl));
     const bool gated = lane < cnt && (d.n + lane + 1 >= (int64_t)min_inst);
     const double ps = myp + s;
