@@ -235,8 +235,15 @@ struct QEntry {
 };
 
 constexpr int kClsThreads = 256;
-constexpr int kRing = 8;                        // fills whose results the classify pass holds in LDS
-constexpr int kLQ = 128;                        // per-wave LDS queue of batches needing exact rows
+#ifndef DDM_RING
+#define DDM_RING 8
+#endif
+#ifndef DDM_LQ
+#define DDM_LQ 128
+#endif
+constexpr int kRing = DDM_RING;                 // fills whose results the classify pass holds in LDS (power of 2)
+constexpr int kLQ = DDM_LQ;                     // per-wave LDS queue of batches needing exact rows (power of 2)
+static_assert((kRing & (kRing - 1)) == 0 && kRing <= 8 && (kLQ & (kLQ - 1)) == 0, "ring / queue sizes");
 #ifndef DDM_CLS_WAVES
 #define DDM_CLS_WAVES 4
 #endif
