@@ -810,7 +810,8 @@ __global__ __launch_bounds__(kExThreads) void k_scan_batches_exact(
     uint32_t* __restrict__ need, const QEntry* __restrict__ q, const uint32_t* __restrict__ qcnt,
     int64_t* __restrict__ q1,
     uint32_t* __restrict__ q1cnt, double2* __restrict__ pend, int2* __restrict__ ev1, uint8_t* __restrict__ flags1,
-    double2* __restrict__ pend1, int refill) {
+    double2* __restrict__ pend1, int refill, uint32_t* __restrict__ ctr, int64_t* __restrict__ spec_list,
+    int32_t* __restrict__ sidx, uint32_t spec_cap) {
     __shared__ double rcp[kBatchRcp];
     for (int k = threadIdx.x; k < kBatchRcp; k += kExThreads) rcp[k] = 1.0 / (double)(k > 0 ? k : 1);
     __syncthreads();
@@ -885,7 +886,7 @@ __global__ __launch_bounds__(kExThreads) void k_scan_batches_exact(
             if (head >= n) break;
             continue;
         }
-        bool enq = false;
+        bool enq = false, spec = false;
         if (busy) {
             const bool two = i + 1 < blen;
             const int n0 = d.n;
@@ -926,8 +927,25 @@ __global__ __launch_bounds__(kExThreads) void k_scan_batches_exact(
                 } else {
                     ev1[it] = make_int2(w, c);
                     flags1[it] = fl;
+                    spec = !chg && j + 1 < nb;   // a carried run from here on: the spec list
                 }
                 busy = false;
+            }
+        }
+        if (kLevel == 1) {
+            // an unchanged level-1 batch t: the run carried on from pend1[t] is computed ahead
+            // by k_scan_batches_walk's spec blocks (beside the walk), its index in sidx[t]
+            const uint64_t sm = __ballot(spec);
+            if (sm) {
+                uint32_t base = 0;
+                const int lead = __builtin_ctzll(sm);
+                if (lane == lead) base = atomicAdd(ctr + 3, (uint32_t)__popcll(sm));
+                base = __shfl(base, lead);
+                if (spec) {
+                    const uint32_t k = base + (uint32_t)__popcll(sm & below);
+                    if (k < spec_cap) spec_list[k] = it;
+                    sidx[it] = k < spec_cap ? (int32_t)k : -1;
+                }
             }
         }
         if (kLevel == 0) {
@@ -1028,6 +1046,7 @@ __device__ __forceinline__ uint64_t change_window(const uint8_t* __restrict__ fl
 struct Walk {
     Det d;
     int64_t sid, j, wbase, nev;
+    int64_t lvl1;       // where walk_open stopped: the unchanged level-1 batch t it carries on from, or -1
     uint64_t chg_m, st_m, ev_m;
     LeadMasks lm;
 };
@@ -1046,6 +1065,7 @@ __device__ __forceinline__ void walk_open(Walk& W, int64_t L, int64_t nb, int64_
     uint64_t& st_m = W.st_m;
     uint64_t& ev_m = W.ev_m;
     LeadMasks& lm = W.lm;
+    W.lvl1 = -1;
     for (;;) {
         if (j >= nb) break;
         if (j >= wbase + 64) {          // next 64-batch window (nb > 64 only)
@@ -1108,6 +1128,7 @@ __device__ __forceinline__ void walk_open(Walk& W, int64_t L, int64_t nb, int64_
             continue;
         }
         load_end_state(d, pend1 + 3 * t);
+        W.lvl1 = t;
         break;
     }
 }
@@ -1116,12 +1137,96 @@ __device__ __forceinline__ void walk_open(Walk& W, int64_t L, int64_t nb, int64_
 struct FixEntry {
     Det d;
     int64_t sid, j, nev;
+    int64_t lvl1;       // Walk::lvl1 where the walker stopped
 };
+
+// The carried run after an unchanged level-1 batch t, computed ahead (spec blocks of
+// k_scan_batches_walk): batches t + 1 .. end_j of the stream from pend1[t], one event record
+// each in spec_ev[k][...], kSpecBatches at most.  status 1: the run changed in batch end_j
+// (the detector resets after it); 2: it reached the stream's end without a change, d the
+// final detector; 3: cut after kSpecBatches batches, d the detector before batch end_j.
+// Whether the run is the stream's (t's predecessor reached with a fresh detector) only the
+// walk knows: the fix-up takes it where the walk stopped at t, ignores it elsewhere.
+constexpr int kSpecBatches = 64;
+struct SpecRes {
+    Det d;
+    int64_t end_j;
+    int32_t status, nev;
+};
+
+// One batch of a stream from a carried detector c, by the wave: its bytes through the wave's
+// LDS bit image (batches [ib, ib + 64) of the stream, refilled by coalesced loads when j
+// leaves it), its rows through wave_tile tiles.  Returns the batch's event record (pmap
+// applied); c is left as it stands after the batch (in a pending change when cp >= 0).
+struct ChainImg {
+    int64_t ib, ia0;
+};
+
+__device__ __forceinline__ int2 chain_batch(Det& c, int64_t sid, int64_t j, const uint8_t* __restrict__ err,
+                                            int64_t L, int64_t pb, int min_inst, double wl, double cl,
+                                            const uint8_t* __restrict__ pmap, uint64_t* img, double* tw,
+                                            ChainImg& im, int& cp_out) {
+    const int lane = threadIdx.x & 63;
+    uint16_t* const img16 = reinterpret_cast<uint16_t*>(img);
+    const int64_t srow = sid * L;
+    if (j < im.ib || j >= im.ib + 64) {
+        // batches [j & ~63, +64) of the stream into the image
+        im.ib = j & ~(int64_t)63;
+        im.ia0 = (srow + im.ib * pb) & ~(int64_t)15;
+        const int64_t iend = srow + min(L, (im.ib + 64) * pb);
+        const int nch = (int)((iend - im.ia0 + 15) >> 4);
+        wave_sync_lds();
+        for (int c0 = 0; c0 < nch; c0 += 64) {
+            const int ch = min(c0 + lane, nch - 1);
+            uint4 v = *reinterpret_cast<const uint4*>(err + im.ia0 + 16 * (int64_t)ch);
+            v.x = nzbytes(v.x);
+            v.y = nzbytes(v.y);
+            v.z = nzbytes(v.z);
+            v.w = nzbytes(v.w);
+            img16[ch] = (uint16_t)fold16(v);
+        }
+        wave_sync_lds();
+    }
+    const int64_t bstart = srow + j * pb;
+    const int blen = (int)min(pb, L - j * pb);
+    const int o = (int)(bstart - im.ia0);
+    const int wo = o >> 6, sh = o & 63;
+    const uint64_t x0 = img[wo], x1 = img[wo + 1], x2 = img[wo + 2];
+    const uint64_t a0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
+    const uint64_t a1 = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
+    c.chg = 0;
+    int ci = 0, cw = -1, cp = -1;
+    while (ci < blen) {
+        const int cnt = min(64, blen - ci);
+        const uint64_t m = ci < 64 ? m0_shift(a0, a1, ci) : (a1 >> (ci - 64));
+        const TileOut to = wave_tile(c, m, cnt, min_inst, wl, cl, tw);
+        const uint64_t upto = to.last >= 63 ? ~0ull : ((1ull << (to.last + 1)) - 1);
+        const uint64_t wb = to.warn & upto;
+        if (cw < 0 && wb) cw = ci + __builtin_ctzll(wb);
+        if (to.kc >= 0) {
+            cp = ci + to.kc;
+            break;
+        }
+        ci += cnt;
+    }
+    int w = cw, cc = cp;
+    if (pmap) {
+        if (w >= 0) w = pmap[bstart + w];
+        if (cc >= 0) cc = pmap[bstart + cc];
+    }
+    cp_out = cp;
+    return make_int2(w, cc);
+}
 
 // 4a. The walker: one lane per listed stream (no cooperation, few registers, many lanes in
 // flight), walk_open over its flag bytes from the carried-in state.  Most streams end here;
 // a stream that needs rows with a carried detector (a chain longer than the level-1 records,
 // or a carried-in state) goes to the fix-up list with its position.
+//
+// The same launch's first spec_blocks workgroups (dispatched first) run the speculative
+// carried runs instead, one wave per spec-list entry t (an unchanged level-1 batch): the
+// batches after t from pend1[t] until a change, into spec_ev / spec_res.  They need nothing
+// of the walk, so the longest carried runs start with it instead of after it.
 #ifndef DDM_WALK_THREADS
 #define DDM_WALK_THREADS 256
 #endif
@@ -1131,20 +1236,67 @@ constexpr int kWalkThreads = DDM_WALK_THREADS;
 #endif
 
 __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(DDM_WALK_WAVES))) void k_scan_batches_walk(
-    int64_t n_streams, int64_t L, int64_t nb, int64_t nbp, ddm_params P, ddm_state* __restrict__ state,
-    int2* __restrict__ ev, const uint8_t* __restrict__ flags, int64_t* __restrict__ nev_out,
-    const uint8_t* __restrict__ pmap, const uint32_t* __restrict__ need, uint32_t* __restrict__ ctr,
-    const double2* __restrict__ pend, const int2* __restrict__ ev1, const uint8_t* __restrict__ flags1,
-    const double2* __restrict__ pend1, FixEntry* __restrict__ coop) {
+    const uint8_t* __restrict__ err, int64_t n_streams, int64_t L, int64_t nb, int64_t nbp, ddm_params P,
+    ddm_state* __restrict__ state, int2* __restrict__ ev, const uint8_t* __restrict__ flags,
+    int64_t* __restrict__ nev_out, const uint8_t* __restrict__ pmap, const uint32_t* __restrict__ need,
+    uint32_t* __restrict__ ctr, const double2* __restrict__ pend, const int2* __restrict__ ev1,
+    const uint8_t* __restrict__ flags1, const double2* __restrict__ pend1, FixEntry* __restrict__ coop,
+    int spec_blocks, const int64_t* __restrict__ spec_list, uint32_t spec_cap, SpecRes* __restrict__ spec_res,
+    int2* __restrict__ spec_ev) {
     const int64_t pb = P.per_batch;
     const bool shortcuts = P.min_num_instances == 3;
     const int lane = threadIdx.x & 63;
     const uint64_t below = (1ull << lane) - 1;
     __shared__ int32_t s_list[kWalkThreads];
     __shared__ uint32_t s_cnt;
+    __shared__ uint64_t img[kWalkThreads / 64][kClsWords + 2];
+    __shared__ double s_tile[kWalkThreads / 64][kTileScratch];
+    if ((int)blockIdx.x < spec_blocks) {
+        // ---- spec role
+        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const uint32_t n_spec = min(__atomic_load_n(ctr + 3, __ATOMIC_RELAXED), spec_cap);
+        const uint32_t n_waves = (uint32_t)spec_blocks * (kWalkThreads / 64);
+        const double inv_nb = 1.0 / (double)nb;
+        for (uint32_t k = blockIdx.x * (kWalkThreads / 64) + wv; k < n_spec; k += n_waves) {
+            const int64_t t = spec_list[k];
+            const int64_t sid = item_stream(t, nb, inv_nb);
+            const int64_t j0 = t - sid * nb + 1;
+            Det c;
+            load_end_state(c, pend1 + 3 * t);
+            ChainImg im{-((int64_t)1 << 40), 0};
+            int32_t status = 3, nev = 0;
+            int64_t j = j0;
+            for (; j < nb && j < j0 + kSpecBatches; ++j) {
+                int cp = -1;
+                const int2 e = chain_batch(c, sid, j, err, L, pb, P.min_num_instances, P.warning_level,
+                                           P.out_control_level, pmap, img[wv], s_tile[wv], im, cp);
+                if (lane == 0) spec_ev[(int64_t)k * kSpecBatches + (j - j0)] = e;
+                nev += (e.x >= 0 || e.y >= 0) ? 1 : 0;
+                if (cp >= 0) {
+                    status = 1;
+                    break;
+                }
+            }
+            if (status != 1 && j >= nb) {
+                status = 2;
+                j = nb - 1;
+            }
+            if (lane == 0) {
+                SpecRes r;
+                r.d = c;
+                r.end_j = j;
+                r.status = status;
+                r.nev = nev;
+                spec_res[k] = r;
+            }
+        }
+        return;
+    }
+    // ---- walk role
+    const int64_t wblk = (int64_t)blockIdx.x - spec_blocks;
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
-    const int64_t t = (int64_t)blockIdx.x * kWalkThreads + threadIdx.x;
+    const int64_t t = wblk * kWalkThreads + threadIdx.x;
     if (t < n_streams) {
         const ddm_state st = state[t];
         if (need[t] == 0u && state_fresh(st)) {
@@ -1162,7 +1314,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(DD
             }
             if (nev_out) nev_out[t] = nb;
         } else {
-            s_list[atomicAdd(&s_cnt, 1u)] = (int32_t)(t - (int64_t)blockIdx.x * kWalkThreads);
+            s_list[atomicAdd(&s_cnt, 1u)] = (int32_t)(t - wblk * kWalkThreads);
         }
     }
     __syncthreads();
@@ -1172,7 +1324,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(DD
     bool defer = false;
     Walk W;
     if (threadIdx.x < cnt) {
-        const int64_t u = (int64_t)blockIdx.x * kWalkThreads + s_list[threadIdx.x];
+        const int64_t u = wblk * kWalkThreads + s_list[threadIdx.x];
         W.sid = u;
         load_det(W.d, state[u]);
         W.j = W.wbase = W.nev = 0;
@@ -1197,17 +1349,18 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(DD
             e.sid = W.sid;
             e.j = W.j;
             e.nev = W.nev;
+            e.lvl1 = W.lvl1;
             coop[base + __popcll(dm & below)] = e;
         }
     }
 }
 
-// 4b. The chain kernel: one wave per stream the walker handed over.  The stream's bytes
-// are read 64 batches at a time by coalesced loads into the wave's LDS bit image (as the
-// classify pass does), so a carried detector's rows never wait on memory batch by batch;
-// the walk (walk_open, uniform over the wave) skips what the flag bytes and records decide,
-// and a batch that needs rows runs through wave_tile tiles (the p chain once, the rest
-// lane-parallel) from the carried detector.
+// 4b. The fix-up: one wave per stream the walker handed over.  Where a carried run starts
+// after an unchanged level-1 batch t (the walk stopped there, or got there again after a
+// change), the spec blocks' run for t is taken as it stands (its event records copied);
+// otherwise, or past a cut run, the batches run from the carried detector here (chain_batch:
+// the stream's bytes 64 batches at a time in the wave's LDS image, rows through wave_tile),
+// and walk_open skips what the flag bytes and records decide in between.
 constexpr int kChainThreads = 256;
 
 __global__ __launch_bounds__(kChainThreads) void k_scan_batches_chain(
@@ -1215,7 +1368,8 @@ __global__ __launch_bounds__(kChainThreads) void k_scan_batches_chain(
     ddm_state* __restrict__ state, int2* __restrict__ ev, const uint8_t* __restrict__ flags,
     int64_t* __restrict__ nev_out, const uint8_t* __restrict__ pmap, const FixEntry* __restrict__ coop,
     const uint32_t* __restrict__ ctr, const double2* __restrict__ pend, const int2* __restrict__ ev1,
-    const uint8_t* __restrict__ flags1, const double2* __restrict__ pend1, uint64_t* __restrict__ cprof) {
+    const uint8_t* __restrict__ flags1, const double2* __restrict__ pend1, const int32_t* __restrict__ sidx,
+    const SpecRes* __restrict__ spec_res, const int2* __restrict__ spec_ev, uint64_t* __restrict__ cprof) {
     __shared__ uint64_t img[kChainThreads / 64][kClsWords + 2];
     __shared__ double s_tile[kChainThreads / 64][kTileScratch];
     const int64_t pb = P.per_batch;
@@ -1224,13 +1378,11 @@ __global__ __launch_bounds__(kChainThreads) void k_scan_batches_chain(
     const bool shortcuts = min_inst == 3;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint16_t* const img16 = reinterpret_cast<uint16_t*>(img[wv]);
-    double* const tw = s_tile[wv];
     const uint32_t n_list = __atomic_load_n(ctr + 2, __ATOMIC_RELAXED);
     const uint32_t n_waves = gridDim.x * (kChainThreads / 64);
 #ifdef DDM_TUNING
     // per-wave profile (tuning builds, DDM_CHAIN_PROF): start / end on the 100 MHz clock,
-    // streams taken, rows run through wave_tile
+    // streams taken, rows run through wave_tile here (spec runs taken count none)
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     uint64_t p_streams = 0, p_rows = 0;
 #endif
@@ -1246,67 +1398,49 @@ __global__ __launch_bounds__(kChainThreads) void k_scan_batches_chain(
         W.nev = e.nev;
         W.wbase = W.j & ~(int64_t)63;
         W.chg_m = change_window(flags + W.sid * nbp, W.wbase, nb, W.st_m, W.ev_m, W.lm);
-        int64_t ib = -((int64_t)1 << 40), ia0 = 0; // the image: batches [ib, ib + 64), first byte ia0
-        const int64_t srow = W.sid * L;
+        ChainImg im{-((int64_t)1 << 40), 0};
+        int64_t lv = e.lvl1;                   // the walk stopped after this level-1 batch
         for (;;) {
-            walk_open(W, L, nb, nbp, pb, shortcuts, ev, flags, pmap, pend, ev1, flags1, pend1);
-            if (W.j >= nb) break;
+            if (lv < 0) {
+                walk_open(W, L, nb, nbp, pb, shortcuts, ev, flags, pmap, pend, ev1, flags1, pend1);
+                if (W.j >= nb) break;
+                lv = W.lvl1;
+            }
+            const int32_t sk = lv >= 0 ? sidx[lv] : -1;
+            lv = -1;
+            if (sk >= 0) {
+                // the run carried on after the level-1 batch, computed ahead from the same
+                // detector (pend1[t]): its records, then where it ended
+                const SpecRes r = spec_res[sk];
+                const int64_t j0 = W.j;
+                const int64_t last = r.status == 3 ? r.end_j - 1 : r.end_j;
+                for (int64_t b = j0 + lane; b <= last; b += 64)
+                    ev[W.sid * nb + b] = spec_ev[(int64_t)sk * kSpecBatches + (b - j0)];
+                W.nev += r.nev;
+                if (r.status == 1) {
+                    det_reset(W.d);            // DDM dropped (DDM_Process.py:209)
+                    W.j = r.end_j + 1;
+                } else {
+                    W.d = r.d;
+                    W.j = r.status == 2 ? nb : r.end_j;
+                }
+                if (W.j >= nb) break;
+                if (r.status == 1) continue;   // fresh again: walk_open from there
+            }
+            // the batch W.j from the carried detector, here
             const int64_t j = W.j;
-            if (j < ib || j >= ib + 64) {
-                // batches [j & ~63, +64) of the stream into the image
-                ib = j & ~(int64_t)63;
-                ia0 = (srow + ib * pb) & ~(int64_t)15;
-                const int64_t iend = srow + min(L, (ib + 64) * pb);
-                const int nch = (int)((iend - ia0 + 15) >> 4);
-                wave_sync_lds();
-                for (int c0 = 0; c0 < nch; c0 += 64) {
-                    const int c = min(c0 + lane, nch - 1);
-                    uint4 v = *reinterpret_cast<const uint4*>(err + ia0 + 16 * (int64_t)c);
-                    v.x = nzbytes(v.x);
-                    v.y = nzbytes(v.y);
-                    v.z = nzbytes(v.z);
-                    v.w = nzbytes(v.w);
-                    img16[c] = (uint16_t)fold16(v);
-                }
-                wave_sync_lds();
-            }
-            const int64_t bstart = srow + j * pb;
-            const int blen = (int)min(pb, L - j * pb);
-            const int o = (int)(bstart - ia0);
-            const int wo = o >> 6, sh = o & 63;
-            const uint64_t x0 = img[wv][wo], x1 = img[wv][wo + 1], x2 = img[wv][wo + 2];
-            const uint64_t a0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
-            const uint64_t a1 = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
-            // the batch's rows from the carried detector, one tile after the other
             Det c = W.d;
-            c.chg = 0;
-            int ci = 0, cw = -1, cp = -1;
-            while (ci < blen) {
-                const int cnt = min(64, blen - ci);
-                const uint64_t m = ci < 64 ? m0_shift(a0, a1, ci) : (a1 >> (ci - 64));
-                const TileOut to = wave_tile(c, m, cnt, min_inst, wl, cl, tw);
+            int cp = -1;
+            const int2 evj = chain_batch(c, W.sid, j, err, L, pb, min_inst, wl, cl, pmap, img[wv], s_tile[wv], im, cp);
 #ifdef DDM_TUNING
-                p_rows += (uint64_t)cnt;
+            p_rows += (uint64_t)min(pb, L - j * pb);
 #endif
-                const uint64_t upto = to.last >= 63 ? ~0ull : ((1ull << (to.last + 1)) - 1);
-                const uint64_t wb = to.warn & upto;
-                if (cw < 0 && wb) cw = ci + __builtin_ctzll(wb);
-                if (to.kc >= 0) {
-                    cp = ci + to.kc;
-                    break;
-                }
-                ci += cnt;
-            }
-            int w = cw, cc = cp;
-            if (pmap) {
-                if (w >= 0) w = pmap[bstart + w];
-                if (cc >= 0) cc = pmap[bstart + cc];
-            }
-            if (lane == 0) ev[W.sid * nb + j] = make_int2(w, cc);
-            W.nev += (w >= 0 || cc >= 0);
+            if (lane == 0) ev[W.sid * nb + j] = evj;
+            W.nev += (evj.x >= 0 || evj.y >= 0);
             if (cp >= 0) det_reset(c);             // DDM dropped (DDM_Process.py:209)
             W.d = c;
             W.j = j + 1;
+            if (W.j >= nb) break;
         }
         if (lane == 0) {
             state[W.sid] = store_det(W.d);
@@ -1325,6 +1459,8 @@ __global__ __launch_bounds__(kChainThreads) void k_scan_batches_chain(
             r[3] = p_rows;
         }
     }
+#else
+    (void)cprof;
 #endif
 }
 
@@ -1333,7 +1469,7 @@ __global__ __launch_bounds__(kChainThreads) void k_scan_batches_chain(
 constexpr int64_t kMaxWaves = 1 << 14;
 
 struct BatchScratch {
-    uint32_t* ctr;      // [2] streams handed to the chain kernel
+    uint32_t* ctr;      // [2] streams handed to the chain kernel, [3] spec-list entries
     uint32_t* need;     // [n_streams]
     FixEntry* coop;     // [n_streams] streams the walker hands to the fix-up kernel
     uint8_t* flags;     // [n_streams * nbp], 64-byte aligned rows
@@ -1347,6 +1483,11 @@ struct BatchScratch {
     uint32_t* q1cnt;    // [kMaxWaves]
     double4* pst;       // [kPreN]
     uint16_t* ptab;     // [kPreN]
+    int64_t* spec_list; // [spec_cap] unchanged level-1 batches whose carried run is computed ahead
+    int32_t* sidx;      // [n_items] spec-list index of an unchanged level-1 batch (-1: none, list full)
+    SpecRes* spec_res;  // [spec_cap]
+    int2* spec_ev;      // [spec_cap][kSpecBatches]
+    uint32_t spec_cap;
     uint64_t* cprof;    // tuning builds: the chain kernel's per-wave profile [kChainProfWaves][4] (the scratch's end)
     int64_t bytes;
 };
@@ -1368,6 +1509,9 @@ BatchScratch batch_scratch(void* base, int64_t n_streams, int64_t nb) {
     const int64_t o_pend1 = take(48 * n_items), o_q = take((int64_t)sizeof(QEntry) * nq), o_q1 = take(8 * nq);
     const int64_t o_qcnt = take(4 * kMaxWaves), o_q1cnt = take(4 * kMaxWaves), o_pst = take(32 * (int64_t)kPreN);
     const int64_t o_ptab = take(2 * (int64_t)kPreN);
+    const int64_t spec_cap = std::min<int64_t>((int64_t)1 << 17, std::max<int64_t>(1, n_items));
+    const int64_t o_slist = take(8 * spec_cap), o_sidx = take(4 * std::max<int64_t>(1, n_items));
+    const int64_t o_sres = take((int64_t)sizeof(SpecRes) * spec_cap), o_sev = take(8 * kSpecBatches * spec_cap);
 #ifdef DDM_TUNING
     const int64_t o_cprof = take(32 * kChainProfWaves);
 #endif
@@ -1387,6 +1531,11 @@ BatchScratch batch_scratch(void* base, int64_t n_streams, int64_t nb) {
     sc.q1cnt = reinterpret_cast<uint32_t*>(b + o_q1cnt);
     sc.pst = reinterpret_cast<double4*>(b + o_pst);
     sc.ptab = reinterpret_cast<uint16_t*>(b + o_ptab);
+    sc.spec_list = reinterpret_cast<int64_t*>(b + o_slist);
+    sc.sidx = reinterpret_cast<int32_t*>(b + o_sidx);
+    sc.spec_res = reinterpret_cast<SpecRes*>(b + o_sres);
+    sc.spec_ev = reinterpret_cast<int2*>(b + o_sev);
+    sc.spec_cap = (uint32_t)spec_cap;
 #ifdef DDM_TUNING
     sc.cprof = getenv("DDM_CHAIN_PROF") ? reinterpret_cast<uint64_t*>(b + o_cprof) : nullptr;
 #else
@@ -1450,6 +1599,7 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
     hipStream_t s = ddm::as_hip(stream);
     static const int ex_refill = std::max(1, std::min(64, env_int("DDM_EXACT_REFILL", 24)));
     static const int fix_blocks_max = env_int("DDM_FIX_BLOCKS", 2048);
+    static const int spec_blocks_max = std::max(0, env_int("DDM_SPEC_BLOCKS", 2048));
     static const bool use_pre = env_int("DDM_SCAN_PRE", 1) != 0;
     static const int cls_steps = std::max(0, env_int("DDM_SCAN_STEPS", 2));
     static const int cls_pop = std::max(1, std::min(64, env_int("DDM_SCAN_POP", 16)));
@@ -1493,23 +1643,28 @@ extern "C" int ddm_scan_batches(const uint8_t* err, int64_t n_streams, int64_t s
         const auto ex1 = perm_map ? k_scan_batches_exact<1, true> : k_scan_batches_exact<1, false>;
         hipLaunchKernelGGL(ex0, dim3((unsigned)blocks), dim3(kExThreads), 0, s, err, n_items, stream_len, nb, nbp, *prm, ev,
                            sc.flags, perm_map, qcap, sc.need, sc.q, sc.qcnt, sc.q1, sc.q1cnt,
-                           sc.pend, sc.ev1, sc.flags1, sc.pend1, ex_refill);
+                           sc.pend, sc.ev1, sc.flags1, sc.pend1, ex_refill, sc.ctr, sc.spec_list, sc.sidx, sc.spec_cap);
         if (int rc = ddm::launch_status("ddm_scan_batches/exact")) return rc;
         hipLaunchKernelGGL(ex1, dim3((unsigned)blocks), dim3(kExThreads), 0, s, err, n_items, stream_len, nb, nbp, *prm, ev,
                            sc.flags, perm_map, qcap, sc.need, sc.q, sc.qcnt, sc.q1, sc.q1cnt,
-                           sc.pend, sc.ev1, sc.flags1, sc.pend1, ex_refill);
+                           sc.pend, sc.ev1, sc.flags1, sc.pend1, ex_refill, sc.ctr, sc.spec_list, sc.sidx, sc.spec_cap);
         if (int rc = ddm::launch_status("ddm_scan_batches/exact1")) return rc;
     }
-    hipLaunchKernelGGL(k_scan_batches_walk, dim3((unsigned)ddm::ceil_div(n_streams, kWalkThreads)), dim3(kWalkThreads),
-                       0, s, n_streams, stream_len, nb, nbp, *prm, state_io, reinterpret_cast<int2*>(ev_out),
-                       sc.flags, nev_out, perm_map, sc.need, sc.ctr, sc.pend, sc.ev1, sc.flags1, sc.pend1, sc.coop);
+    // the speculative carried runs' workgroups first in the grid (dispatched first), then the walk's
+    const int spec_blocks =
+        n_items > 0 ? (int)std::min<int64_t>(spec_blocks_max, ddm::ceil_div((int64_t)sc.spec_cap, kWalkThreads / 64)) : 0;
+    hipLaunchKernelGGL(k_scan_batches_walk, dim3((unsigned)(spec_blocks + ddm::ceil_div(n_streams, kWalkThreads))),
+                       dim3(kWalkThreads), 0, s, err, n_streams, stream_len, nb, nbp, *prm, state_io,
+                       reinterpret_cast<int2*>(ev_out), sc.flags, nev_out, perm_map, sc.need, sc.ctr, sc.pend, sc.ev1,
+                       sc.flags1, sc.pend1, sc.coop, spec_blocks, sc.spec_list, sc.spec_cap, sc.spec_res, sc.spec_ev);
     if (int rc = ddm::launch_status("ddm_scan_batches/walk")) return rc;
     const int64_t fix_blocks =
         std::max<int64_t>(1, std::min<int64_t>(sc.cprof ? std::min(fix_blocks_max, 2048) : fix_blocks_max,
                                                ddm::ceil_div(n_streams, kChainThreads / 64)));
     hipLaunchKernelGGL(k_scan_batches_chain, dim3((unsigned)fix_blocks), dim3(kChainThreads), 0, s, err, stream_len,
                        nb, nbp, *prm, state_io, reinterpret_cast<int2*>(ev_out), sc.flags, nev_out, perm_map,
-                       sc.coop, sc.ctr, sc.pend, sc.ev1, sc.flags1, sc.pend1, sc.cprof);
+                       sc.coop, sc.ctr, sc.pend, sc.ev1, sc.flags1, sc.pend1, sc.sidx, sc.spec_res, sc.spec_ev,
+                       sc.cprof);
     if (ev_end)
         if (int rc = ddm::hip_status(hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s), "event record")) return rc;
     return ddm::launch_status("ddm_scan_batches");

@@ -60,6 +60,7 @@ def child(a):
                     "hist_dur_us": np.histogram(dur, bins=[0, 5, 10, 20, 40, 60, 80, 100, 120, 160, 200, 400])[0].tolist()}
         with open(os.environ["DDM_CHAIN_PROF"], "w") as f:
             json.dump(prof_out, f, indent=1)
+    ctr = scratch[:16].cpu().numpy().view(np.uint32)
     prof = scratch[64:128].cpu().numpy().view(np.uint64)
     h = hashlib.sha1()
     h.update(ev.cpu().numpy().tobytes())
@@ -67,7 +68,8 @@ def child(a):
     med = float(np.median(times))
     alg = S * L * 1.08
     out = {"label": a.label, "median_ms": med, "min_ms": min(times), "frac_8TBs": alg / (med * 1e-3) / 8e12,
-           "sha1_ok": h.hexdigest() == EXPECT_SHA1 if S == 1_000_000 else None, "sha1": h.hexdigest()}
+           "sha1_ok": h.hexdigest() == EXPECT_SHA1 if S == 1_000_000 else None, "sha1": h.hexdigest(),
+           "fixup_streams": int(ctr[2]), "spec_runs": int(ctr[3])}
     if prof.any():      # a -DDDM_OP_PROFILE build: one-pass phase cycles summed over the waves (last call)
         names = ["load", "decide", "drain", "walk", "write", "tail", "-", "chunks"]
         tot = float(prof[:6].sum())
