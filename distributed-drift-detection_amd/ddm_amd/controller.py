@@ -1117,11 +1117,18 @@ class BatchRunner:
         upto, total, pss = self._gen_rest
         pb = self.s.per_batch
         # two pieces per epoch: the epochs' own coverage requests (_ensure_all with wait)
-        # enqueue whatever a window needs first, so this only keeps generation ahead
+        # enqueue whatever a window needs first, so this only keeps generation ahead.
+        # A piece's latency is one jump + one <= 2^20-draw segment per workgroup whatever its
+        # size, so with fewer partitions on this GPU the pieces grow faster and larger (about
+        # 256 segments per launch at most, the CUs' count): with one partition (N = 8) the
+        # doubling from 1M left ~20 epochs waiting behind ~8 pieces one after the other
+        # (profiles/r06/c3s8); with 8 (N = 1) the sizes are as before.
+        grow = max(1, 8 // max(1, len(pss)))
+        piece_max = max(GEN_PIECE_MAX, (256 << 20) // max(1, len(pss)))
         for _ in range(2):
             if upto >= total:
                 break
-            upto = min(total, upto + min(max(upto, GEN_PIECE_MIN), GEN_PIECE_MAX))
+            upto = min(total, upto + min(max(upto * grow, GEN_PIECE_MIN), piece_max))
             self._ensure_all([(ps.i, min(upto, int(ps.nb * expected_draws_per_batch(pb) * 1.02))) for ps in pss],
                              wait=False)
             self._mark(f"piece to {upto}")
