@@ -620,6 +620,7 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
              agg["predict_ms"] / args.steps,
              "scan_kernel_ms_per_step": agg["scan_ms"] / args.steps,
              "shuffle_kernels_ms_per_step": agg["shuffle_ms"] / args.steps,
+             "stream_generation": stream_generation(st_kern),
              "device_refit_kernels_ms_per_step": agg["dfit_ms"] / args.steps,
              "host_s_per_step": agg["host_s"] / args.steps, "gpu_wait_s_per_step": agg["gpu_s"] / args.steps,
              "stream_prep_s_per_step": agg["prep_s"] / args.steps,
@@ -682,6 +683,22 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
                               f"partition rows)")
     scaling = "weak" if kind == "c3w" else "strong"
     return rows_rank, elapsed, info, extra, roofline, cpu_res, scaling
+
+
+def stream_generation(st):
+    """Per step (the instrumented one): the MT19937 stream generation's batched launches on
+    their own streams -- k_mt_jump, k_mt_generate_batch, k_fsm_prefix_batch -- with their
+    algorithmic bytes (ddm_amd/shuffle.py JUMP_BYTES, GEN_STATE_BYTES, table_bytes_per_chunk)
+    and the rate those bytes make over the launches' HIP-event spans, which run beside the
+    epochs (so the rates are in-pipeline figures, not the kernels alone)."""
+    out = {}
+    for kind, units_key, unit in (("jump", "jumps", "jumps"), ("generate", "generate_draws", "draws"),
+                                  ("tables", "tables_chunks", "chunks of 8192 draws")):
+        ms, nb, units = getattr(st, kind + "_ms"), getattr(st, kind + "_bytes"), getattr(st, units_key)
+        out[kind] = {"ms": round(ms, 3), unit: units, "alg_bytes": nb,
+                     "GB_per_s": round(nb / (ms * 1e-3) / 1e9, 1) if ms > 0 else None}
+    out["kernels"] = {"jump": "k_mt_jump", "generate": "k_mt_generate_batch", "tables": "k_fsm_prefix_batch"}
+    return out
 
 
 def c2_fixture_check(mult, instances, c2parts, results):

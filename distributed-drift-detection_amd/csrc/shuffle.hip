@@ -113,12 +113,15 @@ __global__ __launch_bounds__(256) void k_mt_generate(uint32_t* __restrict__ stat
 
 // g(T) * key on the device.  T^i(key) is the window (x_i .. x_{i+623}) of the MT19937
 // word sequence that starts with key (x_{k+624} = f(x_k, x_{k+1}, x_{k+397})), so by
-// linearity g(T) * key = XOR over the set coefficients i of g of those windows:
-//   1. the sequence x_0 .. x_{623 + deg g} (untempered) is generated in LDS (85 KB: one
-//      workgroup per CU), a 624-word block per three barrier phases;
-//   2. thread j accumulates out[j] = XOR_i x_{i+j} over the ~10k set bits of g, every read
-//      an LDS read (consecutive threads, consecutive words: no bank conflict), so a jump
-//      costs ~10k x 2.5 KB of LDS bandwidth instead of as much L2 traffic.
+// linearity g(T) * key = XOR over the set coefficients i of g of those windows.  Thread j
+// accumulates out[j] = XOR_i x_{i+j}, block by block of 624 exponents: the coefficients
+// i in [624c, 624c + 624) read x_{624c} .. x_{624c + 1246}, i.e. sequence blocks c and
+// c + 1, so only three blocks live in LDS (a ring; slot 3 mirrors slot 0 so that blocks c,
+// c + 1 are always contiguous), block c + 2 is generated (three barrier phases) once block
+// c's coefficients are done, and a workgroup takes ~12 KB of LDS instead of the whole
+// ~85 KB sequence (several jumps share a CU, beside the epochs' kernels).  The
+// coefficients are wave-uniform: their bits are walked on the scalar unit (readfirstlane,
+// find-first-set), so a set bit costs the lanes one address add, one LDS read and a XOR.
 struct JumpJob {
     const uint32_t* key;
     const uint64_t* poly;
@@ -127,61 +130,90 @@ struct JumpJob {
 };
 
 constexpr int kJumpThreads = 640;    // >= 624 outputs, a multiple of 64
-constexpr int kJumpZero = DDM_MT_JUMP_SCRATCH_WORDS;   // 624 zero words after the sequence
+
+// block n of the sequence into ring slot n % 3 (and its mirror, slot 3, when n % 3 == 0)
+// from block n - 1; three dependency phases, a barrier after each
+__device__ __forceinline__ void jump_block(uint32_t* x, int n, int t) {
+    const uint32_t* prev = x + ((n - 1) % 3) * kN;
+    uint32_t* cur = x + (n % 3) * kN;
+    uint32_t* mir = (n % 3 == 0) ? x + 3 * kN : nullptr;
+    if (t < 227) {
+        const uint32_t v = mt_word(prev[t], prev[t + 1], prev[t + 397]);
+        cur[t] = v;
+        if (mir) mir[t] = v;
+    }
+    __syncthreads();
+    if (t < 227) {
+        const int i = 227 + t;
+        const uint32_t v = mt_word(prev[i], prev[i + 1], cur[t]);
+        cur[i] = v;
+        if (mir) mir[i] = v;
+    }
+    __syncthreads();
+    if (t < 170) {
+        const int i = 454 + t;
+        const uint32_t v = mt_word(prev[i], i + 1 < kN ? prev[i + 1] : cur[0], cur[i - 227]);
+        cur[i] = v;
+        if (mir) mir[i] = v;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
 
 __global__ __launch_bounds__(kJumpThreads) void k_mt_jump(const JumpJob* __restrict__ jobs) {
     __shared__ uint64_t P[DDM_MT_POLY_WORDS];
-    __shared__ uint32_t x[DDM_MT_JUMP_SCRATCH_WORDS + kN];
+    __shared__ uint32_t x[4 * kN];
     __shared__ int top_s;
     const JumpJob jb = jobs[blockIdx.x];
     const int t = threadIdx.x;
     if (t == 0) top_s = -1;
     for (int k = t; k < DDM_MT_POLY_WORDS; k += kJumpThreads) P[k] = jb.poly[k];
-    if (t < kN) x[t] = jb.key[t];
+    if (t < kN) {
+        const uint32_t v = jb.key[t];
+        x[t] = v;
+        x[3 * kN + t] = v;
+    }
     __syncthreads();
     for (int k = t; k < DDM_MT_POLY_WORDS; k += kJumpThreads)
         if (P[k]) atomicMax(&top_s, 64 * k + 63 - __builtin_clzll(P[k]));
     __syncthreads();
     const int top = top_s;
-    // 1. x_624 .. x_{623 + top}: whole blocks, x_k = f(x_{k-624}, x_{k-623}, x_{k-227})
-    for (int base = kN; base < kN + top; base += kN) {
-        if (t < 227) x[base + t] = mt_word(x[base + t - kN], x[base + t - kN + 1], x[base + t - 227]);
-        __syncthreads();
-        if (t < 227) {
-            const int i = base + 227 + t;
-            x[i] = mt_word(x[i - kN], x[i - kN + 1], x[i - 227]);
-        }
-        __syncthreads();
-        if (t < 170) {
-            const int i = base + 454 + t;
-            x[i] = mt_word(x[i - kN], x[i - kN + 1], x[i - 227]);
-        }
-        __syncthreads();
-    }
-    // 2. out[j] = XOR over set bits i of x_{i+j}: eight set bits per round, their eight LDS
-    //    reads in flight together (a missing bit reads the zero block after the sequence)
-    for (int k = t; k < kN; k += kJumpThreads) x[kJumpZero + k] = 0u;
-    __syncthreads();
+    if (top >= 0) jump_block(x, 1, t);
     uint32_t a = 0;
-    if (t < kN) {
-        for (int wd = 0; wd * 64 <= top; ++wd) {
-            uint64_t bits = P[wd];
-            const int b0 = 64 * wd + t;
-            while (bits) {
-                int i[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    i[u] = bits ? b0 + __builtin_ctzll(bits) : kJumpZero + t;
-                    bits &= bits - 1;
-                }
+    const int tt = t < kN ? t : 0;       // lanes past the state read a valid word, store nothing
+    for (int c = 0; c * kN <= top; ++c) {
+        const int lo = c * kN, hi = min(lo + kN, top + 1);
+        const uint32_t* xc = x + (c % 3) * kN + tt;   // x_{lo + r + t} == xc[r], r + t < 1248
+        for (int wd = lo >> 6; wd * 64 < hi; ++wd) {
+            uint64_t bits = uniform_u64(P[wd]);
+            const int b_lo = lo - 64 * wd, b_hi = hi - 64 * wd;
+            if (b_lo > 0) bits &= ~0ull << b_lo;
+            if (b_hi < 64) bits &= (1ull << b_hi) - 1;
+            const int base = 64 * wd - lo;
+            int n = __builtin_popcountll(bits);
+            for (; n >= 8; n -= 8) {
                 uint32_t v[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = x[i[u]];
+                for (int u = 0; u < 8; ++u) {
+                    v[u] = xc[base + __builtin_ctzll(bits)];
+                    bits &= bits - 1;
+                }
                 a ^= (v[0] ^ v[1]) ^ (v[2] ^ v[3]) ^ (v[4] ^ v[5]) ^ (v[6] ^ v[7]);
             }
+            for (; n > 0; --n) {
+                a ^= xc[base + __builtin_ctzll(bits)];
+                bits &= bits - 1;
+            }
         }
-        jb.out[t] = top >= 0 ? a : 0u;
+        // block c + 2 into block c - 1's slot; its barriers also close block c's reads
+        if ((c + 1) * kN <= top) jump_block(x, c + 2, t);
     }
+    if (t < kN) jb.out[t] = top >= 0 ? a : 0u;
     if (t == 0) jb.out[kN] = kN;
 }
 
@@ -265,13 +297,28 @@ __device__ void fsm_prefix(gptr<const uint32_t> __restrict__ R, int64_t chunk0, 
         off[e] = 0;
     }
     if (tid == 0) n_sh = ns;
+    // the sub-chunk's draws of all nc chunks: kPreLoads 16-byte loads per thread, the next
+    // sub-chunk's issued right after this one's are in LDS so that they land while the
+    // trajectories are stepped (the loop was waiting on a dependent HBM load 64 times)
+    constexpr int kPreLoads = kPreChunks * (kSub / 4) / kPreThreads;
+    static_assert(kPreLoads * kPreThreads == kPreChunks * (kSub / 4), "whole loads per thread");
+    u32x4 nxt[kPreLoads];
+    auto load_sub = [&](int k) {
+#pragma unroll
+        for (int u = 0; u < kPreLoads; ++u) {
+            const int e = tid + u * kPreThreads, c = e / (kSub / 4), q = e % (kSub / 4);
+            if (c < nc) nxt[u] = *(gptr<const u32x4>)(R + (cb + c) * kChunk + (int64_t)k * kSub + 4 * q);
+        }
+    };
+    load_sub(0);
     for (int k = 0; k < kSubPerChunk; ++k) {
         __syncthreads();
-        for (int e = tid; e < nc * (kSub / 4); e += kPreThreads) {
-            const int c = e / (kSub / 4), q = e % (kSub / 4);
-            *reinterpret_cast<u32x4*>(draws + c * kPreRow + 4 * q) =
-                *(gptr<const u32x4>)(R + (cb + c) * kChunk + (int64_t)k * kSub + 4 * q);
+#pragma unroll
+        for (int u = 0; u < kPreLoads; ++u) {
+            const int e = tid + u * kPreThreads, c = e / (kSub / 4), q = e % (kSub / 4);
+            if (c < nc) *reinterpret_cast<u32x4*>(draws + c * kPreRow + 4 * q) = nxt[u];
         }
+        if (k + 1 < kSubPerChunk) load_sub(k + 1);
         __syncthreads();
         const int n = n_sh;
         for (int p = tid; p < n; p += kPreThreads) {
@@ -890,8 +937,6 @@ extern "C" int ddm_mt_jump(const ddm_jump_job* jobs_dev, int32_t n_jobs, ddm_str
     }
     if (n_jobs == 0) return 0;
     static_assert(sizeof(JumpJob) == sizeof(ddm_jump_job), "JumpJob must mirror ddm_jump_job");
-    static_assert(DDM_MT_JUMP_SCRATCH_WORDS >= kN * ((kN + 64 * DDM_MT_POLY_WORDS + kN - 1) / kN + 1),
-                  "the LDS sequence holds the whole blocks of x_0 .. x_{623 + deg}");
     hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)n_jobs), dim3(kJumpThreads), 0, ddm::as_hip(stream),
                        reinterpret_cast<const JumpJob*>(jobs_dev));
     return ddm::launch_status("ddm_mt_jump");

@@ -35,8 +35,8 @@ from ._capi import DDM_STOP_FAILED, DdmEpoch, check, lib
 from .forest import upload_forests
 from .params import OUTPUT_COLUMNS, DDMSettings, infer_x_features
 from .rng import MTStream
-from .shuffle import (CHUNK, GpuShuffle, expected_draws_per_batch, fy_from_words, perm_seeds_from_words,
-                      untemper_keys)
+from .shuffle import (CHUNK, GEN_STATE_BYTES, JUMP_BYTES, GpuShuffle, expected_draws_per_batch, fy_from_words,
+                      perm_seeds_from_words, table_bytes_per_chunk, untemper_keys)
 from .trainer import BatchForestTrainer
 
 # A window runs on ddm_scan_long when its carried detector is neither fresh nor trivial
@@ -183,7 +183,8 @@ class RunStats:
                  "scan_ms", "scan_rows", "shuffle_ms", "sklearn_refits", "refit_fit_s", "refit_readback_s",
                  "prep_s", "dfit_ms", "device_refits", "long_scans", "preshuffled", "device_epochs", "device_phases",
                  "permute_rows", "device_rows", "predict_dev_ms", "predict_dev_launches", "device_predict_bytes",
-                 "flag_recoveries")
+                 "flag_recoveries", "jump_ms", "jumps", "jump_bytes", "generate_ms", "generate_draws",
+                 "generate_bytes", "tables_ms", "tables_chunks", "tables_bytes")
 
     def __init__(self):
         self.epochs = self.refits = self.predicted_rows = self.predict_bytes = self.scan_rows = 0
@@ -193,6 +194,11 @@ class RunStats:
         self.predict_dev_ms, self.predict_dev_launches, self.device_predict_bytes = 0.0, 0, 0
         self.refit_s = self.gpu_s = self.host_s = self.predict_ms = self.scan_ms = self.shuffle_ms = 0.0
         self.refit_fit_s = self.refit_readback_s = self.prep_s = self.dfit_ms = 0.0
+        # the stream generation's batched launches (_ensure_all), HIP events around each on its
+        # own stream while kernel timing is on: time, units, algorithmic bytes per kind
+        self.jump_ms = self.generate_ms = self.tables_ms = 0.0
+        self.jumps = self.jump_bytes = self.generate_draws = self.generate_bytes = 0
+        self.tables_chunks = self.tables_bytes = 0
 
     def as_dict(self):
         return {k: getattr(self, k) for k in self.__slots__}
@@ -385,6 +391,7 @@ class BatchRunner:
             self.shuffles.append(GpuShuffle(dev, pb, cap, mw, self.stream, self.gen_stream, self.tab_stream))
         self.stats = RunStats()
         self._gen_rest = None
+        self._gen_evs = []            # (kind, begin, end, units, bytes) of timed generation launches
         self._forked = False          # the last epoch shuffled the next windows it planned
         self._pending_sync = False    # the last epoch's refit results are still on their way
         self._pending_forests = []
@@ -438,14 +445,19 @@ class BatchRunner:
             rec = np.concatenate(jumps)
             jt = kernels.PinnedTable(kernels.JUMP_DTYPE, len(rec), self.device)
             jt.rec[:len(rec)] = rec
+            e0 = self._gen_ev(self.gen_stream)
             kernels.mt_jump(jt, len(rec), self.gen_stream)
+            self._gen_done(e0, "jump", self.gen_stream, len(rec), len(rec) * JUMP_BYTES)
             self.gen_tables.append(jt)
         self._mark("jumps")
         if reqs:
             reqs = np.concatenate(reqs)
             table = kernels.PinnedTable(kernels.GEN_DTYPE, len(reqs), self.device)   # read by the async copy
             table.rec[:len(reqs)] = reqs
+            e0 = self._gen_ev(self.gen_stream)
             kernels.shuffle_generate_batch(table, len(reqs), self.gen_stream)
+            draws = int(reqs["n"].sum())
+            self._gen_done(e0, "generate", self.gen_stream, draws, 4 * draws + len(reqs) * GEN_STATE_BYTES)
             self.gen_tables.append(table)
         if tabs:
             g = torch.cuda.Event()
@@ -458,8 +470,11 @@ class BatchRunner:
                 # every partition's new chunks: one ddm_shuffle_tables_batch launch
                 tt = kernels.PinnedTable(kernels.TAB_DTYPE, len(recs), self.device)
                 tt.rec[:len(recs)] = np.array(recs, dtype=kernels.TAB_DTYPE)
+                e0 = self._gen_ev(self.tab_stream)
                 kernels.shuffle_tables_batch(tt, len(recs), max(r[2] for r in recs), self.s.per_batch,
                                              self.tab_stream)
+                chunks = sum(r[2] for r in recs)
+                self._gen_done(e0, "tables", self.tab_stream, chunks, chunks * table_bytes_per_chunk(self.s.per_batch))
                 self.gen_tables.append(tt)
             ev = torch.cuda.Event()
             ev.record(self.tab_stream)
@@ -468,6 +483,40 @@ class BatchRunner:
         if wait:
             for i, upto in wants:
                 self.shuffles[i].wait_for(upto)
+
+    def _gen_ev(self, stream):
+        """A timing event on `stream` ahead of a generation launch, while kernel timing is on."""
+        if not self.timing or self.t_shuf is None:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        return e
+
+    def _gen_done(self, e0, kind, stream, units, nbytes):
+        if e0 is None:
+            return
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record(stream)
+        self._gen_evs.append((kind, e0, e1, int(units), int(nbytes)))
+
+    def _gen_collect(self):
+        """Fold the drained generation launches' times and bytes into the stats."""
+        st = self.stats
+        for kind, e0, e1, units, nbytes in self._gen_evs:
+            ms = e0.elapsed_time(e1)
+            if kind == "jump":
+                st.jump_ms += ms
+                st.jumps += units
+                st.jump_bytes += nbytes
+            elif kind == "generate":
+                st.generate_ms += ms
+                st.generate_draws += units
+                st.generate_bytes += nbytes
+            else:
+                st.tables_ms += ms
+                st.tables_chunks += units
+                st.tables_bytes += nbytes
+        self._gen_evs = []
 
     def _upload_perm(self, i, b, perm, slot):
         pb = self.s.per_batch
@@ -804,6 +853,7 @@ class BatchRunner:
         s, st, pb = self.s, self.stats, self.s.per_batch
         self._t_run = time.perf_counter()
         self._gen_rest = None
+        self._gen_evs = []
         self._forked = False
         self._pending_sync = False
         self._pending_forests = []
@@ -952,6 +1002,7 @@ class BatchRunner:
             # streams: nothing may write into this runner's buffers once the caller can free them
             self.gen_stream.synchronize()
             self.tab_stream.synchronize()
+            self._gen_collect()
             self._mark("side streams drained")
 
     def _device_start(self, pss):

@@ -25,6 +25,17 @@ SUB, CHUNK = 128, 8192
 # draws D_0 = 0, D_s = (624 - pos0) + s * JUMP, and segment s >= 1 starts from the state
 # T^(s * JUMP)(key0) (ddm_mt_jump), so all segments of a piece are generated at once.
 JUMP = 1 << 20
+# Algorithmic HBM bytes of the generation kernels (csrc/shuffle.hip), for the bench's
+# stream-generation figures: a jump reads its key (624 words + pos) and its polynomial
+# (312 u64) and writes the segment's start state; a generate job reads and writes its
+# 625-word state and writes 4 B per draw; the tables read a chunk's 8192 draws and write
+# 64 sub-chunk entries plus the chunk entry per interval state (S = L - 1, 4 B each).
+JUMP_BYTES = 625 * 4 + 312 * 8 + 625 * 4
+GEN_STATE_BYTES = 2 * 625 * 4
+
+
+def table_bytes_per_chunk(L):
+    return CHUNK * 4 + (CHUNK // SUB + 1) * (L - 1) * 4
 
 
 @functools.lru_cache(maxsize=None)

@@ -417,8 +417,9 @@ int ddm_shuffle_generate_batch(const ddm_gen_job* jobs_dev, int32_t n_jobs, ddm_
  * ddm_mt_jump (device): per job, out[0..623] = the MT19937 state (numpy key layout,
  *   pos 624) T^e(key) for the polynomial x^e mod phi in poly, and out[624] = 624.  The
  *   lower 31 bits of out[0] are not part of the state (never read by the generator).
- *   scratch: unused, may be NULL (the word sequence x_0 .. x_{623 + deg} of
- *   DDM_MT_JUMP_SCRATCH_WORDS words lives in the workgroup's LDS).
+ *   scratch: unused, may be NULL (the word sequence x_0 .. x_{623 + deg} is generated in
+ *   the workgroup's LDS, three 624-word blocks at a time since round 6; the sequence's
+ *   whole length, DDM_MT_JUMP_SCRATCH_WORDS, is kept for callers sizing scratch).
  *   Replaces nothing in the reference: the streams are those of DDM_Process.py:187,190,102. */
 #define DDM_MT_POLY_WORDS 312
 #define DDM_MT_JUMP_SCRATCH_WORDS 21216
