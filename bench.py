@@ -465,7 +465,9 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
         if getattr(runner, "trace", None) and os.environ.get("DDM_HOST_TRACE_OUT"):
             step.n = getattr(step, "n", 0) + 1
             with open(f"{os.environ['DDM_HOST_TRACE_OUT']}.{step.n}", "w") as f:    # every run's host phases
-                json.dump(runner.trace, f)
+                # t_run: the run's start on CLOCK_MONOTONIC (perf_counter), to align the marks
+                # with a kernel trace's timestamps
+                json.dump({"t_run": getattr(runner, "_t_run", None), "marks": runner.trace}, f)
         if world > 1:
             # the collect of DDM_Process.py:258: the drift/warning positions of every
             # partition on every rank, one all_gather of the batches with an event

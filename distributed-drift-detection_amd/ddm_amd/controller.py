@@ -80,6 +80,9 @@ EARLY_PIECES = int(os.environ.get("DDM_EARLY_PIECES", "1"))
 # A/B in profiles/r05/refit: a CU-masked stream (hipExtStreamCreateWithCUMask) is a blocking
 # stream at normal priority, while the stream it replaces is a non-blocking torch stream at
 # priority -1, so stride > 1 changes the mask, the priority and the null-stream sync at once.
+# Round 6 (tools/cu_probe.hip): the MI355X pool's runtime does not apply the CU mask at all
+# (a stride-2 / 4 / 8 stream's workgroups ran on all 256 CUs), so those A/Bs measured the
+# priority and sync change only.
 SIDE_CU_STRIDE = int(os.environ.get("DDM_SIDE_CU_STRIDE", "1"))
 
 

@@ -325,8 +325,11 @@ int ddm_event_elapsed_ms(ddm_event_t begin, ddm_event_t end, float* ms);
 
 /* ABI 22: a stream on a subset of the current device's CUs (hipExtStreamCreateWithCUMask):
  * CU i belongs to it when i % stride == offset % stride; *n_cus (nullable) = their count.
- * The device epochs put the next windows' shuffles on such a stream so that they leave the
- * other CUs to the predict (DDM_Process.py:110-128 beside :187/:190's shuffles). */
+ * The device epochs can put the next windows' shuffles on such a stream so that they leave
+ * the other CUs to the predict (DDM_Process.py:110-128 beside :187/:190's shuffles; off by
+ * default).  Measured in round 6 (tools/cu_probe.hip, profiles/r06/cu_probe.txt): on the
+ * MI355X pool the runtime accepts the mask but does not apply it -- the workgroups of a
+ * stride-2 / 4 / 8 stream still ran on all 256 CUs -- so *n_cus is the requested count. */
 int ddm_stream_create_cu_stride(int32_t stride, int32_t offset, ddm_stream_t* out, int32_t* n_cus);
 /* ABI 22: the number of CUs a stream may run on (hipExtStreamGetCUMask). */
 int ddm_stream_cu_count(ddm_stream_t stream, int32_t* n_cus);

@@ -62,4 +62,28 @@ for nchunk in (256, 2048):
     ms = float(np.median(times[1:]))
     out[f"tables_{nchunk}"] = {"ms": round(ms, 4), "GB_per_s": round(nchunk * (8192 * 4 + 65 * S * 4) / ms / 1e6, 1),
                                "sha1": hashlib.sha1(Tpre.cpu().numpy().tobytes()).hexdigest()[:16]}
+# the batched form the runner uses: 8 partitions' pieces of 1,024 chunks in one launch
+nj, nchunk, L, S = 8, 1024, 100, 99
+Rs = [torch.from_numpy(np.random.default_rng(100 + k).integers(0, 2**32, nchunk * 8192, dtype=np.uint64)
+                       .astype(np.uint32).view(np.int32)).to(dev) for k in range(nj)]
+Tps = [torch.zeros(nchunk * 64 * S, dtype=torch.int32, device=dev) for _ in range(nj)]
+Tcs = [torch.zeros(nchunk * S + 4, dtype=torch.int32, device=dev) for _ in range(nj)]
+tt = kernels.PinnedTable(kernels.TAB_DTYPE, nj, dev)
+tt.rec[:nj] = np.array([(R.data_ptr(), 0, nchunk, Tp.data_ptr(), Tc.data_ptr()) for R, Tp, Tc in zip(Rs, Tps, Tcs)],
+                       dtype=kernels.TAB_DTYPE)
+torch.cuda.synchronize()
+times = []
+for rep in range(4):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    kernels.shuffle_tables_batch(tt, nj, nchunk, L, stream)
+    e1.record(stream)
+    e1.synchronize()
+    times.append(e0.elapsed_time(e1))
+ms = float(np.median(times[1:]))
+h = hashlib.sha1()
+for Tp in Tps:
+    h.update(Tp.cpu().numpy().tobytes())
+out["tables_batch_8x1024"] = {"ms": round(ms, 4), "GB_per_s": round(nj * nchunk * (8192 * 4 + 65 * S * 4) / ms / 1e6, 1),
+                              "sha1": h.hexdigest()[:16]}
 print(json.dumps(out))
