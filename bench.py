@@ -455,9 +455,21 @@ def run_partition_workload(args, world, rank, dev, torch, dist, kind, cpu):
 
     def step():
         streams = [MTStream.from_seed(seed_base + d) for d, _ in parts]
+        step.calls = getattr(step, "calls", 0) + 1
+        prof = None
+        if os.environ.get("DDM_CPROFILE_OUT") and step.calls == 2:
+            # developer knob: the second run under cProfile (host-time breakdown of a run)
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         tr = time.perf_counter()
         outs = runner.run(streams)
         tr = time.perf_counter() - tr
+        if prof is not None:
+            prof.disable()
+            import pstats
+            with open(os.environ["DDM_CPROFILE_OUT"], "w") as f:
+                pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(60)
         for (d, _), o, g in zip(parts, outs, streams):
             results[d] = o
             rngs[d] = g

@@ -86,6 +86,17 @@ EARLY_PIECES = int(os.environ.get("DDM_EARLY_PIECES", "1"))
 SIDE_CU_STRIDE = int(os.environ.get("DDM_SIDE_CU_STRIDE", "1"))
 
 
+class _Done:
+    """An already computed result with a Future's result() (the small-output fills)."""
+    __slots__ = ("value",)
+
+    def __init__(self, value):
+        self.value = value
+
+    def result(self):
+        return self.value
+
+
 def _round_up(n, m):
     return (n + m - 1) // m * m
 
@@ -225,6 +236,7 @@ class _Part:
 
 _HOST_TRACE = os.environ.get("DDM_HOST_TRACE", "") not in ("", "0")
 _FRESH = kernels.fresh_states(1)[0]
+_FRESH1 = kernels.fresh_states(1)
 
 
 class BatchRunner:
@@ -940,7 +952,7 @@ class BatchRunner:
                     raise ValueError("No objects to concatenate")  # pd.concat([]) (:212)
                 ps.train_rows = perm0.astype(np.int64)
                 ps.ev = []                       # (batch rows, column, positions) of every event
-                ps.state = kernels.fresh_states(1)
+                ps.state = _FRESH1.copy()
                 ps.forest, ps.retrain, ps.j, ps.done = None, True, 1, False
                 ps.staged = None
                 ps.win = max(1, s.window_batches)
@@ -948,8 +960,10 @@ class BatchRunner:
             # the dense per-batch result (DDM_Process.py:212 concatenates one row per batch:
             # 1.25M rows per C3 partition) is filled with -1 on pool threads while the epochs
             # run (numpy releases the GIL for the fill); the events go in at the end
+            # (small outputs are filled right here: a pool hand-off costs more than the fill)
             pool = self._pool()
-            out_f = [pool.submit(np.full, (ps.nb - 1, 2), -1, np.int64) for ps in pss]
+            out_f = [pool.submit(np.full, (ps.nb - 1, 2), -1, np.int64) if ps.nb > 1 << 16 else
+                     _Done(np.full((ps.nb - 1, 2), -1, np.int64)) for ps in pss]
             self._mark("batch-0 shuffles")
             host_epochs = 0
             if self.devctl is not None and DEVICE_START and self._device_start(pss):

@@ -49,6 +49,8 @@ CTL_GRAPH = os.environ.get("DDM_CTL_GRAPH", "0") not in ("", "0")
 # (ddm_ctl_epoch.sync_flags: a one-wave store / poll kernel pair, ~12 us per epoch) instead
 # of HIP events (~30 us); DDM_CTL_FLAGS=0: events
 CTL_FLAGS = os.environ.get("DDM_CTL_FLAGS", "1") not in ("", "0")
+# developer check: _write_records' column form against its per-partition loop form
+CHECK_RECORDS = os.environ.get("DDM_CHECK_RECORDS", "0") not in ("", "0")
 
 
 class FlagTimeout(RuntimeError):
@@ -184,8 +186,101 @@ class DeviceController:
         self._E = E
         return E
 
+    def _static_records(self):
+        """The record fields that never change over the runner's life (built once)."""
+        if getattr(self, "_rec_static", None) is not None:
+            return self._rec_static
+        r = self.r
+        pb = r.s.per_batch
+        t = r._templates()
+        st = np.zeros(self.n, CTL)
+        base_d = self.parts_d.data_ptr()
+        idx = np.arange(self.n, dtype=np.uint64)
+        stg = st["stage"]
+        stg["log"] = [lg.data_ptr() for lg in self.logs]
+        stg["log_n"] = base_d + idx * np.uint64(CTL.itemsize) + np.uint64(_OFF["n_log"])
+        stg["log_cap"] = [max(1, nb) for nb in r.nbs]
+        stg["stall"] = self.pstall.data_ptr() + 4 * idx
+        bp = [b.ptrs() for b in r.dfit_bufs]
+        st["res"] = [r._sptr("dfit", i) for i in range(self.n)]
+        for k, name in enumerate(("dnodes", "droots", "dleaf", "dclasses", "dblob")):
+            st[name] = [p[k] for p in bp]
+        st["dtrees"] = [b.T for b in r.dfit_bufs]
+        st["nb"], st["n_full"], st["base"] = r.nbs, t["stage"]["n_full"], r.bases
+        st["max_win"], st["min_win"] = r.max_wins, r.s.min_window
+        st["win_rule"] = r.s.win_rule
+        st["dpb_x1024"] = int(np.ceil(expected_draws_per_batch(pb) * 1024))
+        st["pb"], st["n_words"] = pb, r.n_words
+        st["last_len"] = [part.n - (nb - 1) * pb for part, nb in zip(r.parts, r.nbs)]
+        st["done"] = 1
+        self._rec_static = st
+        return st
+
     def _write_records(self, live):
-        """The records of every partition (static templates + the host state of the live ones)."""
+        """The records of every partition (static templates + the host state of the live ones),
+        column by column (the per-partition loop of field stores, _write_records_loop, took
+        ~18 us a partition of the phase entry's host time)."""
+        r = self.r
+        r._stream_ptrs(live)             # refreshes the R / table pointers of regrown stream buffers
+        t = r._templates()
+        rec = self.rec
+        rec[:] = self._static_records()
+        ptrs = np.array([sh.ptrs for sh in r.shuffles], dtype=np.uint64).reshape(self.n, 3)
+        job = rec["job"]
+        job[:] = t["job"]
+        job["stop"] = t["stop"]
+        job["R"], job["Tpre"], job["Tchunk"] = ptrs[:, 0], ptrs[:, 1], ptrs[:, 2]
+        rec["seg"] = t["seg"]
+        static_stage = self._static_records()["stage"]
+        stg = rec["stage"]
+        stg[:] = t["stage"]
+        stg["plan_out"] = 0
+        stg["next_job"] = 0
+        stg["R"] = ptrs[:, 0]
+        for name in ("log", "log_n", "log_cap", "stall"):
+            stg[name] = static_stage[name]
+        rec["long_min_rows"], rec["long_cap_rows"] = self.long_min_rows, self.long_cap_rows
+        rec["avail"] = [sh.waited * CHUNK for sh in r.shuffles]
+        if live:
+            ix = np.array([ps.i for ps in live], dtype=np.int64)
+            rec["done"][ix] = 0
+            rec["j"][ix] = [ps.j for ps in live]
+            rec["P"][ix] = [ps.P for ps in live]
+            rec["win"][ix] = [ps.win for ps in live]
+            rec["seg_start"][ix] = [ps.seg_start for ps in live]
+            rec["state"][ix] = np.concatenate([ps.state[:1] for ps in live])
+        for ps in live:
+            if ps.retrain:                       # a device refit staged by the last epoch
+                _, P1, P2, _ = ps.staged
+                q = rec[ps.i]
+                q["retrain"], q["P1"], q["P2"] = 1, P1, P2
+                q["forest_dev"] = 1
+            else:
+                f = ps.forest
+                if isinstance(f, dfit.DeviceFitForest):
+                    rec[ps.i]["forest_dev"] = 1
+                else:
+                    q = rec[ps.i]
+                    d = f.desc
+                    s = q["seg"]
+                    s["nodes"], s["roots"], s["leaf_value"], s["classes"] = d.nodes, d.roots, d.leaf_value or 0, \
+                        d.classes
+                    s["n_trees"], s["n_classes"], s["n_nodes"], s["pure"] = d.n_trees, d.n_classes, d.n_nodes, d.pure
+                    s["cforest"], s["cf_slots"], s["cf_vote_regs"] = d.cforest or 0, d.cf_slots, d.cf_vote_regs
+                    s["cf_leaves"], s["cf_tab_words"] = d.cf_leaves, d.cf_tab_words
+                    q["host_slots"] = f.features_read
+        if CHECK_RECORDS:
+            got = rec.tobytes()
+            self._write_records_loop(live)
+            if rec.tobytes() != got:
+                bad = [n for n in CTL.names if rec[n].tobytes() != np.frombuffer(got, CTL)[n].tobytes()]
+                raise AssertionError(f"_write_records differs from the loop form in {bad}")
+        # every partition's refit job (the slab's table is rewritten by host epochs)
+        r.dfit_jobs.rec[:self.n] = r._templates()["dfit"]
+
+    def _write_records_loop(self, live):
+        """The per-partition loop form of _write_records' record fields (DDM_CHECK_RECORDS=1
+        compares the two on every phase)."""
         r = self.r
         r._stream_ptrs(live)             # refreshes the R / table pointers of regrown stream buffers
         t = r._templates()
@@ -245,18 +340,25 @@ class DeviceController:
                     s["cforest"], s["cf_slots"], s["cf_vote_regs"] = d.cforest or 0, d.cf_slots, d.cf_vote_regs
                     s["cf_leaves"], s["cf_tab_words"] = d.cf_leaves, d.cf_tab_words
                     q["host_slots"] = f.features_read
-        # every partition's refit job (the slab's table is rewritten by host epochs)
-        r.dfit_jobs.rec[:self.n] = r._templates()["dfit"]
 
     def _publish_avail(self, polled=None):
         """Stream coverage the generator finished since the last look: the epoch stream waits
         for it (free once done) and the records' avail fields are raised."""
         r = self.r
+        done = {}           # one query per event: a piece's event closes every partition's tables
         for i, sh in enumerate(r.shuffles):
             best = None
-            for cov, ev in sh.ready:
-                if cov > sh.waited and (best is None or cov > best[0]) and ev.query():
+            # coverage grows in enqueue order and the events of one stream complete in order:
+            # the newest completed event is the best, so look from the newest back
+            for cov, ev in reversed(sh.ready):
+                if cov <= sh.waited:
+                    break
+                ok = done.get(id(ev))
+                if ok is None:
+                    ok = done[id(ev)] = ev.query()
+                if ok:
                     best = (cov, ev)
+                    break
             if best is None:
                 continue
             r.stream.wait_event(best[1])
@@ -522,31 +624,39 @@ class DeviceController:
         r.stream.synchronize()
         r._mark("logs copied")
         logs_np = self.logs_h.numpy()
-        for ps in live:
-            q = rec[ps.i]
-            n_log = int(q["n_log"])
+        # the records' fields column by column (a field read of a structured scalar costs
+        # ~1 us: ~25 of them a partition were ~0.4 ms of a 16-partition phase's end)
+        ix = np.array([ps.i for ps in live], dtype=np.int64)
+        col = {name: rec[name][ix].tolist() for name in
+               ("n_log", "applied", "done", "predicted_rows", "long_scans", "predict_bytes", "permute_rows",
+                "refits", "stall", "j", "P", "win", "seg_start", "retrain", "P1", "P2", "forest_dev")}
+        states = rec["state"][ix].copy()
+        for k, ps in enumerate(live):
+            n_log = col["n_log"][k]
             if n_log:
                 o = int(self.log_off[ps.i])
                 lg = logs_np[o:o + 3 * n_log].reshape(-1, 3).astype(np.int64)
-                for col in range(2):
-                    hit = lg[:, 1 + col] >= 0
+                for c in range(2):
+                    hit = lg[:, 1 + c] >= 0
                     b = lg[hit, 0]
-                    ps.ev.append((b - 1, col, b * pb + lg[hit, 1 + col]))
+                    ps.ev.append((b - 1, c, b * pb + lg[hit, 1 + c]))
             # the last k_ctl may have applied a refit to the window it planned (P after the
             # seeds, batch j already shuffled, a fresh DDM): the host applies it itself in
             # _refit_prep, so it goes back as a pending refit
-            applied = bool(q["applied"]) and not q["done"]
+            applied = bool(col["applied"][k]) and not col["done"][k]
+            retrain = col["retrain"][k]
             if applied:
-                q["retrain"] = 1
-            st.predicted_rows += int(q["predicted_rows"])
-            st.device_rows += int(q["predicted_rows"])
-            st.long_scans += int(q["long_scans"])
-            st.predict_bytes += int(q["predict_bytes"])
-            st.device_predict_bytes += int(q["predict_bytes"])
-            st.permute_rows += int(q["permute_rows"])
-            st.refits += int(q["refits"]) - applied
-            st.device_refits += int(q["refits"]) - applied
-            stall = int(q["stall"])
+                rec[ps.i]["retrain"] = 1
+                retrain = 1
+            st.predicted_rows += col["predicted_rows"][k]
+            st.device_rows += col["predicted_rows"][k]
+            st.long_scans += col["long_scans"][k]
+            st.predict_bytes += col["predict_bytes"][k]
+            st.device_predict_bytes += col["predict_bytes"][k]
+            st.permute_rows += col["permute_rows"][k]
+            st.refits += col["refits"][k] - applied
+            st.device_refits += col["refits"][k] - applied
+            stall = col["stall"][k]
             if stall == kernels.CTL_STALL_REFIT and self._E is not None and self._E.decouple:
                 # the row-order predict's smaller LDS (csrc/forest_predict.hip) may be why
                 self.decouple_ok = False
@@ -555,11 +665,11 @@ class DeviceController:
             if stall == kernels.CTL_STALL_SCAN:
                 raise RuntimeError(f"ddm_scan_long gave up waiting for a carried state (partition {ps.i}): the "
                                    "epoch's results are void")
-            ps.j, ps.P, ps.win, ps.seg_start = int(q["j"]), int(q["P"]), int(q["win"]), int(q["seg_start"])
-            ps.state = np.array([q["state"]], dtype=kernels.STATE_DTYPE)
-            ps.done = bool(q["done"])
+            ps.j, ps.P, ps.win, ps.seg_start = col["j"][k], col["P"][k], col["win"][k], col["seg_start"][k]
+            ps.state = np.array(states[k:k + 1], dtype=kernels.STATE_DTYPE)
+            ps.done = bool(col["done"][k])
             ps.staged = None
-            if q["retrain"]:
+            if retrain:
                 ps.retrain = True
                 if stall == kernels.CTL_STALL_WORDS:
                     # the host path's own staging form: batch d's rows, the words after P
@@ -570,11 +680,11 @@ class DeviceController:
                                  r._sview("y", ps.i, np.int32, L).astype(np.int64),
                                  r._sview("w", ps.i, np.uint32, r.n_words).copy(), None, int(info[4]), int(info[5]))
                 else:
-                    ps.staged = ("device", int(q["P1"]), int(q["P2"]), None)
+                    ps.staged = ("device", col["P1"][k], col["P2"][k], None)
                     r._pending_sync = True         # _finish_pending reads (or redoes) the refit
             else:
                 ps.retrain = False
-                if q["forest_dev"]:
+                if col["forest_dev"][k]:
                     res = r._sview("dfit", ps.i, np.int64, dfit.RESULT_WORDS).copy()
                     ps.forest = dfit.DeviceFitForest(r.dfit_bufs[ps.i], res)
             if ps.j >= ps.nb:
@@ -582,6 +692,5 @@ class DeviceController:
         st.epochs += epochs
         st.device_epochs += epochs
         st.device_phases += 1
-        for i in range(self.n):
-            self.rec[i]["n_log"] = 0
+        self.rec["n_log"] = 0
         return epochs
