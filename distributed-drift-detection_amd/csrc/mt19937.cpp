@@ -135,6 +135,21 @@ extern "C" int ddm_mt_randint31(uint32_t* key, int32_t* pos, int64_t count, int6
     return 0;
 }
 
+// ABI 24: numpy's legacy RandomState(seed) for a 32-bit integer seed (the reference's
+// per-partition np.random.seed, DDM_Process.py): init_genrand into the key, pos = 624.
+// Constructing a RandomState in Python costs ~0.1 ms (it seeds a fresh bit generator from
+// the OS first), paid per partition at every run's start.
+extern "C" int ddm_mt_seed(uint32_t seed, uint32_t* key, int32_t* pos) {
+    if (!key || !pos) return DDM_E_ARG;
+    uint32_t x = seed;
+    for (int i = 0; i < kN; ++i) {
+        key[i] = x;
+        x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)(i + 1);
+    }
+    *pos = kN;
+    return 0;
+}
+
 extern "C" int ddm_mt_skip(uint32_t* key, int32_t* pos, int64_t n_draws) {
     if (!key || !pos || n_draws < 0 || *pos < 0 || *pos > kN) return DDM_E_ARG;
     Gen g{key, *pos};

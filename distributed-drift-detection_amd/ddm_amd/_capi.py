@@ -12,7 +12,7 @@ import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 # DDM_AMD_LIB: an alternative build of the same library (e.g. an instrumented one)
 LIB_PATH = os.environ.get("DDM_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libddm_amd.so")
-ABI_VERSION = 22
+ABI_VERSION = 24
 
 DDM_E_ARG = 1001
 DDM_E_FOREST = 1002
@@ -141,6 +141,7 @@ SIGNATURES = {
     "ddm_mt_perms": (ctypes.c_int, [_vp, _pi32, _vp, _i64, _vp, _vp]),
     "ddm_mt_randint31": (ctypes.c_int, [_vp, _pi32, _i64, _vp]),
     "ddm_mt_skip": (ctypes.c_int, [_vp, _pi32, _i64]),
+    "ddm_mt_seed": (ctypes.c_int, [ctypes.c_uint32, _vp, _pi32]),
     "ddm_forest_compile": (ctypes.c_int, [_vp, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _i64,
                                           ctypes.POINTER(ctypes.c_int64)]),
     "ddm_rf_fit_many": (ctypes.c_int, [_vp, _i32, _i32]),

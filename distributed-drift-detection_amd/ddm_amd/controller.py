@@ -401,9 +401,14 @@ class BatchRunner:
         # a refit every 2.25 batches in C5 takes the stream to ~1.3x); device epochs need
         # every draw a window may ask for inside the buffers (they never regrow there)
         dev_ctl = (DEVICE_CTL if device_ctl is None else device_ctl) and refit == "device"
-        for part, nb, mw in zip(self.parts, self.nbs, self.max_wins):
+        # every partition's start-state rows (mt, seg0) in one device array, uploaded in one
+        # copy per run from one pinned array (per-partition copies were ~20 us each)
+        self.state_rows_d = torch.zeros((n, 2, 640), dtype=torch.int32, device=dev)
+        self.state_rows_h = torch.zeros((n, 2, 640), dtype=torch.int32, pin_memory=True)
+        for k, (part, nb, mw) in enumerate(zip(self.parts, self.nbs, self.max_wins)):
             cap = int(nb * expected_draws_per_batch(pb) * (1.45 if dev_ctl else 1.2)) + (128 if dev_ctl else 64) * 1024
-            self.shuffles.append(GpuShuffle(dev, pb, cap, mw, self.stream, self.gen_stream, self.tab_stream))
+            self.shuffles.append(GpuShuffle(dev, pb, cap, mw, self.stream, self.gen_stream, self.tab_stream,
+                                            state_rows=self.state_rows_d[k]))
         self.stats = RunStats()
         self._gen_rest = None
         self._gen_evs = []            # (kind, begin, end, units, bytes) of timed generation launches
@@ -896,8 +901,13 @@ class BatchRunner:
         for s_ in (self.stream, self.gen_stream, self.tab_stream):   # nothing of the last run
             s_.synchronize()                                          # may still read the streams
         self._mark("streams idle")
+        sr = self.state_rows_h.numpy().view(np.uint32)     # free: the streams are idle
         for ps, rng in zip(pss, rngs):
-            self.shuffles[ps.i].reset(rng, synced=True)
+            self.shuffles[ps.i].reset(rng, synced=True, upload=False)
+            sr[ps.i, :, :624] = rng.key
+            sr[ps.i, :, 624] = int(rng.pos.value)
+        with torch.cuda.stream(self.gen_stream):
+            self.state_rows_d.copy_(self.state_rows_h, non_blocking=True)
         self._mark("MT states uploaded")
         started = []
         try:

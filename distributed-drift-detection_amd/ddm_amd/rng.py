@@ -40,6 +40,14 @@ class MTStream:
 
     @classmethod
     def from_seed(cls, seed):
+        """numpy's RandomState(seed) state; 32-bit integer seeds natively (ddm_mt_seed)."""
+        if isinstance(seed, (int, np.integer)) and 0 <= int(seed) < 2**32:
+            st = cls.__new__(cls)
+            st.key = np.empty(624, dtype=np.uint32)
+            st.pos = ctypes.c_int32(0)
+            st.gauss = (0, 0.0)
+            check(lib.ddm_mt_seed(int(seed), st.key.ctypes.data, ctypes.byref(st.pos)), "ddm_mt_seed")
+            return st
         return cls.from_numpy_state(np.random.RandomState(seed).get_state())
 
     def numpy_state(self):

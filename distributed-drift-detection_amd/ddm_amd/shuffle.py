@@ -132,14 +132,21 @@ class GpuShuffle:
     itself) in pieces, each closed by an event; consumers on `stream` wait on the event of
     the piece that covers what they read (`wait_for`), so generation overlaps the epochs."""
 
-    def __init__(self, device, L, capacity_draws, max_window, stream, gen_stream=None, tab_stream=None):
+    def __init__(self, device, L, capacity_draws, max_window, stream, gen_stream=None, tab_stream=None,
+                 state_rows=None):
         if not 2 <= L <= 256:
             raise ValueError("GPU shuffles need 2 <= batch length <= 256")
         self.device, self.L, self.S, self.stream = device, L, L - 1, stream
         self.gen_stream = gen_stream or stream
         self.tab_stream = tab_stream or self.gen_stream   # tables (after the words they read)
         self.max_window = int(max_window)
-        self.mt = torch.zeros(625, dtype=torch.int32, device=device)
+        # the stream's start state: `mt` is the key every jump reads, `seg0` segment 0's
+        # generator state (it advances as segment 0 is generated); state_rows: two device
+        # rows of >= 625 int32 the caller owns and uploads itself (a runner uploads every
+        # partition's pair in one copy, reset(upload=False))
+        if state_rows is None:
+            state_rows = torch.zeros((2, 640), dtype=torch.int32, device=device)
+        self.mt, self.seg0 = state_rows[0], state_rows[1]
         self._alloc(max(2 * CHUNK, int(capacity_draws)))
         # the window's first piece, the sub-chunks of the chunk holding its start, then chunks
         self.max_pieces = 4 + CHUNK // SUB + (self.max_window * L * 3) // CHUNK
@@ -172,29 +179,31 @@ class GpuShuffle:
         self.R, self.Tpre, self.Tchunk, self.cap = R, Tp, Tc, cap
         self.ptrs = (R.data_ptr(), Tp.data_ptr(), Tc.data_ptr())    # changes only here
 
-    def reset(self, rng, synced=False):
+    def reset(self, rng, synced=False, upload=True):
         """Draw 0 of the device stream = the next draw of `rng` (an MTStream).  synced: the
         caller has synchronised this stream's three HIP streams already (a runner resets all
-        its partitions after one synchronisation)."""
+        its partitions after one synchronisation).  upload=False: the caller uploads the
+        state rows (mt, seg0 = key[624], pos) itself, on gen_stream, before any generation."""
         self.init_key = rng.key.copy()
         self.init_pos = int(rng.pos.value)
         if not synced:
             self.stream.synchronize()
             self.gen_stream.synchronize()       # nothing of the previous run may still read R
             self.tab_stream.synchronize()
-        # the state goes up from a pinned buffer of this stream's own (asynchronous copy; the
-        # previous run's copy from it is done: gen_stream was synchronised)
-        if getattr(self, "_st_h", None) is None:
-            self._st_h = torch.empty(625, dtype=torch.int32, pin_memory=True)
-        st = self._st_h.numpy().view(np.uint32)
-        st[:624] = self.init_key
-        st[624] = self.init_pos
         self.n_seg = self._segments_for(self.cap)
         with torch.cuda.stream(self.gen_stream):   # allocated, filled and read on gen_stream
             if getattr(self, "seg", None) is None or self.seg.shape[0] < self.n_seg:
                 self.seg = torch.zeros((self.n_seg, 640), dtype=torch.int32, device=self.device)
-            self.mt.copy_(self._st_h, non_blocking=True)
-            self.seg[0, :625].copy_(self.mt)
+            if upload:
+                # from a pinned buffer of this stream's own (asynchronous copy; the previous
+                # run's copy from it is done: gen_stream was synchronised)
+                if getattr(self, "_st_h", None) is None:
+                    self._st_h = torch.empty(625, dtype=torch.int32, pin_memory=True)
+                st = self._st_h.numpy().view(np.uint32)
+                st[:624] = self.init_key
+                st[624] = self.init_pos
+                self.mt[:625].copy_(self._st_h, non_blocking=True)
+                self.seg0[:625].copy_(self.mt[:625])
         self.jumped = 1                     # segments whose start state exists
         self._keep = []
         self.gen = self.tab = self.waited = 0
@@ -278,7 +287,9 @@ class GpuShuffle:
             lo, hi = np.maximum(self.gen, starts), np.minimum(target, ends)
             keep = lo < hi
             reqs = np.empty(int(keep.sum()), dtype=kernels.GEN_DTYPE)
-            reqs["state"] = self.seg.data_ptr() + seg[keep].astype(np.uint64) * (4 * self.seg.shape[1])
+            sk = seg[keep].astype(np.uint64)
+            reqs["state"] = np.where(sk == 0, np.uint64(self.seg0.data_ptr()),
+                                     np.uint64(self.seg.data_ptr()) + sk * np.uint64(4 * self.seg.shape[1]))
             reqs["R"] = self.R.data_ptr() + 4 * lo[keep].astype(np.uint64)
             reqs["n"] = hi[keep] - lo[keep]
             self.gen = target

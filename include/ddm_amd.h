@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DDM_AMD_ABI_VERSION 22
+#define DDM_AMD_ABI_VERSION 24
 
 #define DDM_E_ARG        1001   /* invalid argument (null pointer, bad size) */
 #define DDM_E_FOREST     1002   /* forest shape not supported (classes > 256) */
@@ -353,6 +353,11 @@ int ddm_mt_randint31(uint32_t* key, int32_t* pos, int64_t count, int64_t* out);
 
 /* Advance the generator by n_draws 32-bit words. */
 int ddm_mt_skip(uint32_t* key, int32_t* pos, int64_t n_draws);
+
+/* ABI 24: numpy's legacy RandomState(seed) state for a seed < 2^32 (init_genrand, pos 624):
+ * the per-partition np.random.seed of the reference's UDF, without constructing a Python
+ * RandomState (~0.1 ms each) at every run's start. */
+int ddm_mt_seed(uint32_t seed, uint32_t* key, int32_t* pos);
 
 /* One batch's permutation(L) then T randint(2**31-1) seeds from already tempered words
  * of the stream (e.g. read back from the device copy); used[0], used[1] = words each

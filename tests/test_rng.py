@@ -69,3 +69,14 @@ def test_snapshot_restore_roundtrip():
     x = mt.perms([100, 100])
     mt.restore(snap)
     assert np.array_equal(mt.perms([100, 100]), x)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 123, 1000, 1015, 2**31 - 1, 2**32 - 1])
+def test_from_seed_native_matches_numpy(seed):
+    """ddm_mt_seed (ABI 24) == numpy's legacy RandomState(seed) state, and the draws after it."""
+    st = MTStream.from_seed(seed)
+    ref = np.random.RandomState(seed).get_state()
+    assert np.array_equal(st.key, ref[1]) and st.pos.value == ref[2] and st.gauss == (ref[3], ref[4])
+    rs = np.random.RandomState(seed)
+    want = np.concatenate([rs.permutation(100) for _ in range(5)]).astype(np.uint8)
+    assert np.array_equal(st.perms(np.full(5, 100, np.int32)), want)
