@@ -718,6 +718,7 @@ __device__ void fsm_replay(gptr<const uint32_t> __restrict__ R, gptr<const uint3
                            int L, gptr<uint8_t> __restrict__ J, gptr<int64_t> __restrict__ E,
                            gptr<uint8_t> __restrict__ perm_out, int64_t blk, int64_t nblk) {
     extern __shared__ __attribute__((aligned(16))) uint8_t rlds[];
+    __shared__ uint32_t sdraws[kSub];
     const int64_t npieces = info[0], end = info[1];
     const int S = L - 1;
     const int lane = threadIdx.x;
@@ -727,8 +728,20 @@ __device__ void fsm_replay(gptr<const uint32_t> __restrict__ R, gptr<const uint3
         const int64_t stop = (pc + 1 < npieces) ? pieces[pc + 1].pos : end;
         if (stop <= c.pos) continue;
         if (stop - c.pos <= kSub) {
+            // a piece of at most one sub-chunk, stepped by lane 0: the wave stages its draws in
+            // LDS with one load each first (lane 0 alone took 8 dependent rounds of 16-word
+            // loads: ~30 us, on the critical path of small windows' epochs, C5 / c2)
             const ReplaySink k{J, E, nullptr, 0, 0, L};
-            if (lane == 0) replay_range(R, c.pos, stop, (uint32_t)c.state, c.batch, W, L, k);
+            const int n = (int)(stop - c.pos);
+            for (int q = lane; q < n; q += 64) sdraws[q] = R[c.pos + q];
+            __syncthreads();
+            if (lane == 0) {
+                uint32_t s = (uint32_t)c.state;
+                int64_t b = c.batch;
+                const uint32_t S = (uint32_t)(L - 1);
+                for (int q = 0; q < n && b < W; ++q) replay_step(sdraws[q], c.pos + q, s, b, S, k);
+            }
+            __syncthreads();
             continue;
         }
         // this piece's own batches: those that start in it and end in it

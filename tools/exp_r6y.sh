@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 6: where a C5 epoch goes now (kernel trace of a reduced C5: 8M rows) and the c2 run's
+# host marks after the start-up changes
+set -o pipefail
+cd "$(dirname "$0")/.." && mkdir -p gpurun_out/r6y && rm -rf gpurun_out/r6y/*
+export TMPDIR=/tmp
+O=gpurun_out/r6y
+DDM_HOST_TRACE=1 DDM_HOST_TRACE_OUT=$O/ht_c2 timeout -k 10 300 python -u bench.py --workload c2 --cpu-baseline 0 > $O/c2.json 2> $O/c2.err || { tail -5 $O/c2.err; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o c5 -- python3 bench.py --workload c5 --c5-rows 8000000 --steps 1 --warmup 1 --cpu-baseline 0 > $O/c5_line.json 2> $O/c5.err || { tail -5 $O/c5.err; exit 1; }
+find $O -name "*.csv" | head
+echo done
