@@ -191,10 +191,11 @@ class GpuShuffle:
             self.gen_stream.synchronize()       # nothing of the previous run may still read R
             self.tab_stream.synchronize()
         self.n_seg = self._segments_for(self.cap)
-        with torch.cuda.stream(self.gen_stream):   # allocated, filled and read on gen_stream
-            if getattr(self, "seg", None) is None or self.seg.shape[0] < self.n_seg:
+        if getattr(self, "seg", None) is None or self.seg.shape[0] < self.n_seg:
+            with torch.cuda.stream(self.gen_stream):   # allocated, filled and read on gen_stream
                 self.seg = torch.zeros((self.n_seg, 640), dtype=torch.int32, device=self.device)
-            if upload:
+        if upload:
+            with torch.cuda.stream(self.gen_stream):
                 # from a pinned buffer of this stream's own (asynchronous copy; the previous
                 # run's copy from it is done: gen_stream was synchronised)
                 if getattr(self, "_st_h", None) is None:
