@@ -1080,6 +1080,7 @@ class BatchRunner:
                         torch.from_numpy(idx).to(self.device))
         _, p0_h, p0_idx = self._p0
         p0_h.numpy()[:] = np.stack([np.asarray(ps.train_rows, dtype=np.uint8) for ps in pss])
+        self._mark("start: batch-0 perms staged")
         with torch.cuda.stream(stream):
             self.perm_all.index_copy_(0, p0_idx, p0_h.view(-1).to(self.device, non_blocking=True))
         self._mark("start: batch-0 perms uploaded")

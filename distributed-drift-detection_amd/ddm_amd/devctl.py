@@ -631,19 +631,27 @@ class DeviceController:
         # the records' fields column by column (a field read of a structured scalar costs
         # ~1 us: ~25 of them a partition were ~0.4 ms of a 16-partition phase's end)
         ix = np.array([ps.i for ps in live], dtype=np.int64)
-        col = {name: rec[name][ix].tolist() for name in
+        sub = rec[ix]                    # one gather of the live records, then cheap field views
+        col = {name: sub[name].tolist() for name in
                ("n_log", "applied", "done", "predicted_rows", "long_scans", "predict_bytes", "permute_rows",
                 "refits", "stall", "j", "P", "win", "seg_start", "retrain", "P1", "P2", "forest_dev")}
-        states = rec["state"][ix].copy()
+        states = sub["state"]
+        # every partition's event log parsed at once: (batch, warning pos, change pos) rows
+        with_log = [(k, ps) for k, ps in enumerate(live) if col["n_log"][k]]
+        if with_log:
+            lens = [col["n_log"][k] for k, _ in with_log]
+            lg = np.concatenate([logs_np[int(self.log_off[ps.i]):int(self.log_off[ps.i]) + 3 * n]
+                                 for (k, ps), n in zip(with_log, lens)]).reshape(-1, 3).astype(np.int64)
+            bounds = np.cumsum(lens)[:-1]
+            for c in range(2):
+                hit = lg[:, 1 + c] >= 0
+                rows = np.split(lg[:, 0] - 1, bounds)
+                vals = np.split(lg[:, 0] * pb + lg[:, 1 + c], bounds)
+                hits = np.split(hit, bounds)
+                for (k, ps), r_, v_, h_ in zip(with_log, rows, vals, hits):
+                    ps.ev.append((r_[h_], c, v_[h_]))
+        r._mark("take-back: events parsed")
         for k, ps in enumerate(live):
-            n_log = col["n_log"][k]
-            if n_log:
-                o = int(self.log_off[ps.i])
-                lg = logs_np[o:o + 3 * n_log].reshape(-1, 3).astype(np.int64)
-                for c in range(2):
-                    hit = lg[:, 1 + c] >= 0
-                    b = lg[hit, 0]
-                    ps.ev.append((b - 1, c, b * pb + lg[hit, 1 + c]))
             # the last k_ctl may have applied a refit to the window it planned (P after the
             # seeds, batch j already shuffled, a fresh DDM): the host applies it itself in
             # _refit_prep, so it goes back as a pending refit
@@ -693,6 +701,7 @@ class DeviceController:
                     ps.forest = dfit.DeviceFitForest(r.dfit_bufs[ps.i], res)
             if ps.j >= ps.nb:
                 ps.done = True
+        r._mark("take-back: partitions")
         st.epochs += epochs
         st.device_epochs += epochs
         st.device_phases += 1
