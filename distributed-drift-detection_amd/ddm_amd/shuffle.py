@@ -45,17 +45,21 @@ def expected_draws_per_batch(L):
 
 
 def _untemper(y):
-    y = y.astype(np.uint64)
-    y ^= y >> 18
-    y ^= (y << 15) & 0xefc60000
+    """MT19937's tempering inverted, in uint32 arithmetic (in place on a copy: ~2x fewer
+    passes over the words than the uint64 form; the run's end untempers every partition's
+    624 words)."""
+    y = np.array(y, dtype=np.uint32)
+    y ^= y >> np.uint32(18)
+    y ^= (y << np.uint32(15)) & np.uint32(0xefc60000)
     t = y.copy()
-    for _ in range(5):
-        t = y ^ ((t << 7) & 0x9d2c5680)
-    t &= 0xffffffff
-    u = t.copy()
-    for _ in range(3):
-        u = t ^ (u >> 11)
-    return (u & 0xffffffff).astype(np.uint32)
+    tmp = np.empty_like(y)
+    for _ in range(4):                         # 7-bit steps cover the 32 bits
+        np.left_shift(t, np.uint32(7), out=tmp)
+        tmp &= np.uint32(0x9d2c5680)
+        np.bitwise_xor(y, tmp, out=t)
+    u = t ^ (t >> np.uint32(11))
+    u ^= t >> np.uint32(22)                    # x ^ x >> 11 inverted: x ^ x >> 11 ^ x >> 22
+    return u
 
 
 def untemper_keys(words):
