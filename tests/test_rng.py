@@ -80,3 +80,12 @@ def test_from_seed_native_matches_numpy(seed):
     rs = np.random.RandomState(seed)
     want = np.concatenate([rs.permutation(100) for _ in range(5)]).astype(np.uint8)
     assert np.array_equal(st.perms(np.full(5, 100, np.int32)), want)
+
+
+def test_untemper_inverts_tempering():
+    """shuffle.untemper_keys (uint32 closed forms, round 6) inverts MT19937's tempering."""
+    from ddm_amd.shuffle import _temper, untemper_keys
+    x = np.random.default_rng(5).integers(0, 2**32, 200_000, dtype=np.uint64).astype(np.uint32)
+    x[:4] = [0, 1, 0xffffffff, 0x80000000]
+    got = untemper_keys(_temper(x))
+    assert got.dtype == np.uint32 and np.array_equal(got, x)
